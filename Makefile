@@ -1,0 +1,34 @@
+# Build of the MI355X word-count engine (gfx950).  In-tree outputs so that the
+# built .so files travel with the repo snapshot to the GPU box.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
+PKG := map-oxidize_amd
+CSRC := $(PKG)/csrc
+OUT := $(PKG)/mox
+
+all: $(OUT)/libmox.so $(OUT)/libmox_corpus.so $(OUT)/meduce-gpu oracle
+
+$(OUT)/mox_kernels.o: $(CSRC)/mox_kernels.hip $(CSRC)/mox_internal.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/mox_engine.o: $(CSRC)/mox_engine.hip $(CSRC)/mox_internal.h $(CSRC)/mox_unicode_tables.h include/mox.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OUT)/libmox.so: $(OUT)/mox_kernels.o $(OUT)/mox_engine.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+$(OUT)/libmox_corpus.so: $(CSRC)/mox_corpus.c
+	gcc -O3 -fPIC -shared -Wall -Wextra -o $@ $< -lpthread -lm
+
+$(OUT)/meduce-gpu: $(CSRC)/meduce_gpu.cpp include/mox.h $(OUT)/libmox.so
+	g++ -O2 -std=c++17 -Wall -o $@ $< -Iinclude -L$(OUT) -lmox -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -f $(OUT)/*.o $(OUT)/*.so $(OUT)/meduce-gpu
+	$(MAKE) -C oracle clean
+
+.PHONY: all clean oracle

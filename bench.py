@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""Word-count throughput of the MI355X engine (BASELINE.json metric).
+
+One step = one full pass of the hot path (reference: main.rs:16-22) over the
+HBM-resident corpus: dictionary -> map -> shuffle -> reduce -> (word, count)
+table in HBM; with N > 1 also the RCCL all-to-all exchange and the final
+per-owner reduce.  The corpus is generated on the host (synthetic, seeded) and
+copied to HBM before timing.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Default workload (N = 1): config C2 of BASELINE.json, 1 GiB Zipf(1.1)
+English-like corpus.  N > 1: weak scaling, 1 GiB byte-range shard per GPU of the
+same corpus stream (rank r owns bytes [r GiB, (r+1) GiB)).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "map-oxidize_amd"))
+
+import numpy as np  # noqa: E402
+
+import mox  # noqa: E402
+from mox import corpus  # noqa: E402
+
+METRIC = "word-count input GB/s end-to-end at 1 and 8 MI355X; % of HBM peak"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HALO = 1 << 16
+
+WORKLOADS = {
+    # name: (kind, seed, bytes per rank, description)
+    "C2": (corpus.ZIPF, 0x5EED0002, 1 << 30, "C2: 1 GiB Zipf(s=1.1) English-like corpus per GPU (map+sort+reduce)"),
+    "C3": (corpus.ZIPF, 0x5EED0003, 8 << 30, "C3: 64 GiB Zipf corpus = 8 GiB shard per GPU at 8 GPUs"),
+    "C4": (corpus.HICARD, 0x5EED0004, 16 << 30, "C4: 16 GiB high-cardinality random 4-16 B tokens per GPU"),
+    "C5": (corpus.SKEW, 0x5EED0005, 16 << 30, "C5: 16 GiB heavy skew (top-10 words = 90%) per GPU"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--bytes-per-gpu", type=int, default=0, help="override the shard size")
+    ap.add_argument("--cpu-sample-mib", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dict", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_map.json"),
+                    help="PMC summary of the map kernel (tools/pmc_traffic.py) to report as roofline.traffic")
+    return ap.parse_args()
+
+
+def cpu_baseline(kind, seed, sample_bytes):
+    """Faithful C++ restatement of the reference pipeline (oracle/build/meduce_ref),
+    timed on a bounded sample of the same corpus: 8 map threads, 4 reduce threads."""
+    exe = os.path.join(ROOT, "oracle", "build", "meduce_ref")
+    if not os.path.exists(exe):
+        return None
+    data = corpus.fill(kind, seed, 0, sample_bytes)
+    tmpdir = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    with tempfile.TemporaryDirectory(dir=tmpdir) as d:
+        path = os.path.join(d, "shakes.txt")
+        data.tofile(path)
+        del data
+        r = subprocess.run([exe, path, "--workdir", d, "--quiet", "--time"], capture_output=True, timeout=600)
+        if r.returncode != 0:
+            return None
+        t = json.loads(r.stderr.decode().strip().splitlines()[-1])
+    return {
+        "value": round(sample_bytes / t["hot_s"] / 1e9, 4),
+        "unit": "GB/s",
+        "cores": 8,
+        "kind": "port",
+        "sample": "first %d MiB of the same corpus; oracle/build/meduce_ref (faithful C++ restatement of "
+                  "main.rs: line round-robin into 8 chunks, 8 map threads, spill files, 4 reduce threads "
+                  "behind one mutex), -O3, split+map+reduce wall time (main.rs:16-22)" % (sample_bytes >> 20),
+        "hot_s": t["hot_s"],
+        "host_nproc": os.cpu_count(),
+    }
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        world = a.gpus if world == 1 else world
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (rendezvous, barrier, max-time)
+        dist.init_process_group("gloo")
+    kind, seed, per_rank, desc = WORKLOADS[a.workload]
+    if a.bytes_per_gpu:
+        per_rank = a.bytes_per_gpu
+    total = per_rank * world
+    own_b = rank * per_rank
+    own_e = own_b + per_rank
+    lo = max(0, own_b - 64)
+    hi = min(total, own_e + HALO) if world > 1 else own_e
+    at_end = hi == total
+
+    eng = mox.Engine(device=local, flags=mox.MOX_F_TIMING | (mox.MOX_F_NO_DICT if a.no_dict else 0),
+                     reserve_bytes=per_rank)
+    host = corpus.fill(kind, seed, lo, hi - lo)
+    d_buf = eng.alloc(hi - lo)
+    eng.h2d(d_buf, host)
+    del host
+    if world > 1:
+        uid = mox.comm_unique_id() if rank == 0 else b""
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        eng.comm_init(world, rank, obj[0])
+
+    def step():
+        eng.run_range(d_buf, hi - lo, own_b - lo, own_e - lo, at_end)
+        if world > 1:
+            eng.exchange()
+
+    for _ in range(a.warmup):
+        step()
+    if dist:
+        dist.barrier()
+    eng.synchronize()
+    map_ms, run_ms, phases = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+        s = eng.stats()
+        map_ms.append(s["ms_map"])
+        run_ms.append(s["ms_run"])
+        phases.append(s)
+    eng.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    last = eng.stats()
+    t = eng.fetch()
+    counts, _, _ = t.arrays()
+    ok = int(counts.sum()) == t.tokens if world == 1 else True
+    t.close()
+
+    if rank == 0:
+        ms_step = elapsed / a.steps * 1e3
+        gbs = total / (elapsed / a.steps) / 1e9
+        map_avg = statistics.mean(map_ms)
+        achieved = per_rank / (map_avg * 1e-3) / 1e9
+        traffic = None
+        if a.traffic_json and os.path.exists(a.traffic_json):
+            try:
+                traffic = json.load(open(a.traffic_json)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": METRIC,
+            "value": round(gbs, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: mox_corpus kind=%d seed=%#x (Zipf(1.1) English-like text, host-generated, "
+                    "copied to HBM before timing)" % (kind, seed),
+            "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
+                       "parallelism": "dp%d byte-range shards%s" % (world, " + RCCL all-to-all" if world > 1 else "")},
+            "words_per_s": round(last["tokens"] * world / (elapsed / a.steps), 1),
+            "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * world), 2),
+            "roofline": {
+                "kernel": "k_map",
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": per_rank,
+                "avg_launch_ms": round(map_avg, 4),
+            },
+            "phases_ms": {k: round(statistics.mean(p[k] for p in phases), 4)
+                          for k in ("ms_run", "ms_dict", "ms_map", "ms_lanes", "ms_reduce", "ms_finalize",
+                                    "ms_exchange")},
+            "stats": {k: last[k] for k in ("tokens", "uniques", "dict_words", "cold_records", "weighted_records",
+                                           "unicode_tokens", "long_tokens", "chunks", "max_subpasses", "retries")},
+            "check_sum_counts_eq_tokens": ok,
+            "cpu_baseline": None,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(kind, seed, min(per_rank, a.cpu_sample_mib << 20))
+        print(json.dumps(line), flush=True)
+    eng.free(d_buf)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

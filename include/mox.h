@@ -1,0 +1,157 @@
+/* mox.h -- C ABI of the MI355X word-count engine (drop-in for the hot path of
+ * AnarchistHoneybun/map-oxidize).
+ *
+ * The reference has no plugin / FFI API: the whole hot path is the private call
+ * sequence in `main` (/root/reference/src/main.rs:16-22)
+ *
+ *     let chunks       = split_file("shakes.txt", 8).await?;                 // :16, fn :36-51
+ *     let map_results  = map_phase(&chunks, 8).await?;                      // :19, fn :53-92
+ *     let final_result = reduce_phase(map_results.clone(), 4).await?;       // :22, fn :111-150
+ *
+ * i.e. `path -> HashMap<String, usize>` consumed by write_final_result
+ * (:170-182) and print_top_words (:184-192).  mox_count_file / mox_count
+ * replace those three lines with one call that returns the same word -> count
+ * table; mox_write_final_result / mox_print_top_words reproduce the L5 output.
+ * INTEGRATION.md shows the Rust FFI binding a maintainer would add.
+ *
+ * Semantics (bit-exact with the reference): tokens are Rust
+ * `str::split_whitespace` (Unicode White_Space delimiters) of the UTF-8 text,
+ * each lowercased with Rust `str::to_lowercase` (full mapping + Final_Sigma),
+ * counted with u64.  Invalid UTF-8 returns MOX_EUTF8 and no table, like the
+ * reference's InvalidData abort at main.rs:44 -> :16.
+ *
+ * Conventions: every entry point returns an int status (0 = MOX_OK); no
+ * exception crosses the ABI; mox_last_error() holds a thread-local message.
+ * An engine is bound to one HIP device and is not thread-safe (one host thread
+ * per engine).  Calls are synchronous: they return after the result is ready.
+ */
+#ifndef MOX_H
+#define MOX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MOX_ABI_VERSION 1
+
+/* status codes */
+#define MOX_OK 0
+#define MOX_EINVAL (-1)  /* bad argument */
+#define MOX_EUTF8 (-2)   /* input is not valid UTF-8 (reference: io::ErrorKind::InvalidData) */
+#define MOX_ENOMEM (-3)  /* device or host allocation failed */
+#define MOX_EHIP (-4)    /* HIP runtime error */
+#define MOX_EIO (-5)     /* file I/O error (reference: io::Error from File::open / reads) */
+#define MOX_ERCCL (-6)   /* RCCL error */
+#define MOX_ESTATE (-7)  /* call out of order (e.g. fetch before run) */
+#define MOX_EHALO (-8)   /* a shard's token ran past the end of its buffer: halo too small */
+
+/* mox_config.flags */
+#define MOX_F_NO_DICT 0x1u      /* disable the hot-word dictionary (all tokens take the cold path) */
+#define MOX_F_SORT_BYTES 0x2u   /* fetch returns words sorted bytewise (Rust String Ord) instead of hash order */
+#define MOX_F_TIMING 0x4u       /* record per-kernel HIP-event timings into mox_stats */
+
+typedef struct mox_config {
+  int device;             /* HIP device ordinal; -1 = current device */
+  uint32_t flags;         /* MOX_F_* */
+  uint32_t dict_words;    /* hot dictionary capacity; 0 = default (3072) */
+  uint32_t sample_pieces; /* 64 KiB pieces sampled to build the dictionary; 0 = default (64) */
+  uint64_t reserve_bytes; /* pre-size device buffers for corpora of this size; 0 = grow on demand */
+  uint32_t reserved[8];
+} mox_config;
+
+typedef struct mox_engine mox_engine;
+
+/* Result table: one entry per distinct lowercased word.  Order: ascending
+ * (64-bit word hash, word bytes) -- deterministic -- or bytewise ascending with
+ * MOX_F_SORT_BYTES.  Memory is owned by the library until mox_table_free. */
+typedef struct mox_table {
+  uint64_t n;              /* distinct words */
+  uint64_t tokens;         /* total tokens counted (== sum of counts) */
+  const uint64_t* counts;  /* [n] */
+  const uint64_t* offs;    /* [n+1] byte offsets into bytes */
+  const uint8_t* bytes;    /* concatenated UTF-8 words */
+} mox_table;
+
+typedef struct mox_stats {
+  uint64_t bytes;          /* corpus bytes of the last run */
+  uint64_t tokens;
+  uint64_t uniques;
+  uint64_t dict_words;     /* words in the hot dictionary */
+  uint64_t cold_records;   /* tokens that took the cold (partitioned) path */
+  uint64_t weighted_records;
+  uint64_t unicode_tokens; /* tokens that went through the Unicode case lane */
+  uint64_t long_tokens;    /* tokens longer than 16 bytes (hashed keys + byte compare) */
+  uint64_t chunks;         /* cold-record chunks allocated */
+  uint32_t retries;        /* buffer-growth reruns in the last call */
+  uint32_t max_subpasses;  /* largest reduce sub-pass count of any bucket */
+  /* device milliseconds (HIP events on the engine stream; MOX_F_TIMING) */
+  double ms_run;           /* whole device pipeline: corpus in HBM -> table in HBM */
+  double ms_dict;          /* sample + dictionary build */
+  double ms_map;           /* map kernel (dominant kernel) */
+  double ms_lanes;         /* unicode + long lanes */
+  double ms_reduce;        /* directory + bucket reduce */
+  double ms_finalize;      /* table materialisation */
+  double ms_h2d;           /* host -> device corpus copy (mox_count / mox_count_file) */
+  double ms_d2h;           /* table fetch */
+  double ms_exchange;      /* multi-GPU all-to-all + final reduce */
+} mox_stats;
+
+const char* mox_last_error(void);
+int mox_abi_version(void);
+
+int mox_engine_create(const mox_config* cfg, mox_engine** out);
+void mox_engine_destroy(mox_engine* e);
+
+/* ---- drop-in for main.rs:16-22 ---- */
+/* Count words of a host buffer (copied to HBM first). */
+int mox_count(mox_engine* e, const uint8_t* text, size_t len, mox_table** out);
+/* Count words of a file (reference: split_file(path) .. reduce_phase). */
+int mox_count_file(mox_engine* e, const char* path, mox_table** out);
+void mox_table_free(mox_table* t);
+
+/* ---- device-resident path (bench / pipelines): corpus already in HBM ---- */
+/* One full pass: HBM corpus -> HBM table.  No host copy of the result. */
+int mox_run_device(mox_engine* e, const void* d_text, size_t len);
+/* Same over a shard window: count tokens whose first byte lies in
+ * [own_begin, own_end) of the buffer d_buf[0, buf_len).  Bytes before own_begin
+ * give the left context (own_begin == 0 means "corpus start"); bytes after
+ * own_end are look-ahead for the last token.  at_corpus_end != 0 means the
+ * buffer end is the end of the corpus; otherwise a token reaching the buffer
+ * end is an error (MOX_EHALO). */
+int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
+                  int at_corpus_end);
+/* Copy the table of the last run (or of the last exchange) to the host. */
+int mox_fetch_table(mox_engine* e, mox_table** out);
+int mox_get_stats(const mox_engine* e, mox_stats* out);
+
+/* device memory helpers so callers need no HIP headers */
+int mox_device_alloc(mox_engine* e, size_t bytes, void** d_ptr);
+int mox_device_free(mox_engine* e, void* d_ptr);
+int mox_memcpy_h2d(mox_engine* e, void* d_dst, const void* h_src, size_t bytes);
+int mox_memcpy_d2h(mox_engine* e, void* h_dst, const void* d_src, size_t bytes);
+int mox_synchronize(mox_engine* e);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ---- */
+#define MOX_UNIQUE_ID_BYTES 128
+int mox_comm_unique_id(uint8_t id[MOX_UNIQUE_ID_BYTES]);
+int mox_comm_init(mox_engine* e, int nranks, int rank, const uint8_t id[MOX_UNIQUE_ID_BYTES]);
+/* After mox_run_range on every rank: hash-partition the local table, exchange
+ * it with one RCCL all-to-all, and reduce the received partials.  Afterwards
+ * this rank owns the final counts of its hash range (disjoint across ranks). */
+int mox_exchange(mox_engine* e);
+
+/* ---- output layer (reference L5: main.rs:170-192) ---- */
+/* final_result.txt: one "{word} {count}\n" line per word.  Truncates on open
+ * (the reference does not: SURVEY.md §0.2 quirk, not reproduced). */
+int mox_write_final_result(const mox_table* t, const char* path);
+/* "Top {n} words:" then up to n lines "{word}: {count}", count descending,
+ * ties in table order (the reference's tie order is HashMap-random). */
+int mox_print_top_words(const mox_table* t, size_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MOX_H */

@@ -1,0 +1,674 @@
+// Host engine + C ABI (include/mox.h) of the MI355X word-count engine.
+//
+// Replaces the reference's hot section (/root/reference/src/main.rs:16-22:
+// split_file -> map_phase -> reduce_phase) with one device pipeline per call:
+//   corpus in HBM -> dictionary -> map (+shuffle write) -> lanes -> directory
+//   -> bucket reduce -> dense table in HBM.
+// No host round-trip inside the pipeline; one small control-block read at the
+// end decides success, UTF-8 error, or a buffer-growth rerun.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/mox.h"
+#include "mox_internal.h"
+#include "mox_unicode_tables.h"
+
+using namespace mox;
+
+extern "C" {
+__global__ void k_map(Corpus c, Work w, uint64_t ntiles);
+__global__ void k_sample(Corpus c, Work w, uint32_t npieces);
+__global__ void k_dict_build(Work w, uint32_t max_words);
+__global__ void k_dict_totals(Work w, uint32_t map_grid);
+__global__ void k_unicode(Corpus c, Work w, Tables T);
+__global__ void k_hist(Work w);
+__global__ void k_bucket_scan(Work w);
+__global__ void k_scatter(Work w);
+__global__ void k_reduce(Work w);
+__global__ void k_scan_reduce(const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
+                              uint64_t* part);
+__global__ void k_scan_parts(uint64_t* part, int nparts);
+__global__ void k_scan_apply(const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
+                             const uint64_t* part, uint64_t* out);
+__global__ void k_long_flags(Work w, uint64_t* flags);
+__global__ void k_final_scan(Work w);
+__global__ void k_mat_counts(Work w, uint64_t* lens);
+__global__ void k_mat_long(Work w, uint64_t* lens);
+__global__ void k_mat_bytes(Work w, Corpus c);
+}
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                             \
+  do {                                                                                           \
+    hipError_t e_ = (expr);                                                                      \
+    if (e_ != hipSuccess) return fail(MOX_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+#define RCCLCHK(expr)                                                                            \
+  do {                                                                                           \
+    ncclResult_t r_ = (expr);                                                                    \
+    if (r_ != ncclSuccess) return fail(MOX_ERCCL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+uint64_t next_pow2(uint64_t x) {
+  uint64_t p = 1;
+  while (p < x) p <<= 1;
+  return p;
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+};
+
+}  // namespace
+
+struct mox_engine {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 64;
+  int n_cu = 256;
+  Work w{};
+  Tables tables{};
+  Ctl* h_ctl = nullptr;       // pinned
+  Ctl* h_ctl_init = nullptr;  // pinned
+  uint64_t* d_lens = nullptr; // table_cap + 1 scratch (lengths / long flags)
+  uint64_t lens_cap = 0;
+  // engine-owned corpus staging for host inputs
+  uint8_t* d_text = nullptr;
+  size_t d_text_cap = 0;
+  // last run
+  bool have_result = false;
+  Corpus last_corpus{};
+  mox_stats stats{};
+  hipEvent_t ev[12]{};
+  // multi-GPU
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+  std::vector<DevBuf> owned;  // allocations to free
+};
+
+namespace {
+
+int dalloc(mox_engine* e, void** p, size_t bytes) {
+  if (bytes == 0) bytes = 16;
+  hipError_t err = hipMalloc(p, bytes);
+  if (err != hipSuccess) return fail(MOX_ENOMEM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(err));
+  return MOX_OK;
+}
+void dfree(void* p) {
+  if (p) (void)hipFree(p);
+}
+
+// (Re)allocate every size-dependent buffer for the given capacities.
+struct Caps {
+  uint64_t pool_cap, w_cap, u_cap, arena_cap, long_cap, table_cap, bytes_cap;
+};
+
+Caps caps_of(const Work& w) {
+  return Caps{w.pool_cap, w.w_cap, w.u_cap, w.arena_cap, w.long_cap, w.table_cap, w.bytes_cap};
+}
+
+Caps initial_caps(uint64_t n, int map_grid) {
+  Caps c;
+  c.pool_cap = std::max<uint64_t>(4096, n / ((uint64_t)CHUNK_RECS * 16) + (uint64_t)map_grid * NB * 2);
+  c.w_cap = 65536 + n / 64;
+  c.u_cap = 4096 + n / 64;
+  c.arena_cap = 65536 + n / 16;
+  c.long_cap = 65536;
+  c.table_cap = 65536 + n / 64;
+  c.bytes_cap = c.table_cap * 8;
+  return c;
+}
+
+#define FREE_FIELD(f) \
+  do {                \
+    dfree(e->w.f);    \
+    e->w.f = nullptr; \
+  } while (0)
+
+int realloc_sized(mox_engine* e, const Caps& c) {
+  (void)hipDeviceSynchronize();
+  FREE_FIELD(pool); FREE_FIELD(chunk_bucket); FREE_FIELD(chunk_fill); FREE_FIELD(dir);
+  FREE_FIELD(w); FREE_FIELD(w_sorted); FREE_FIELD(u); FREE_FIELD(arena); FREE_FIELD(ltab); FREE_FIELD(lpos);
+  FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
+  dfree(e->d_lens);
+  e->d_lens = nullptr;
+  Work& w = e->w;
+  w.pool_cap = c.pool_cap;
+  w.w_cap = c.w_cap;
+  w.u_cap = c.u_cap;
+  w.arena_cap = c.arena_cap;
+  w.long_cap = next_pow2(c.long_cap);
+  w.uniq_cap = c.pool_cap * CHUNK_RECS + c.w_cap;
+  w.table_cap = c.table_cap;
+  w.bytes_cap = c.bytes_cap;
+  int rc;
+  if ((rc = dalloc(e, (void**)&w.pool, w.pool_cap * CHUNK_RECS * 16))) return rc;
+  if ((rc = dalloc(e, (void**)&w.chunk_bucket, w.pool_cap * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.chunk_fill, w.pool_cap * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dir, w.pool_cap * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.w, w.w_cap * sizeof(WRec)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.w_sorted, w.w_cap * sizeof(WRec)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.u, w.u_cap * sizeof(URec)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.arena, w.arena_cap))) return rc;
+  if ((rc = dalloc(e, (void**)&w.ltab, w.long_cap * sizeof(LSlot)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.lpos, (w.long_cap + 1) * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.uk, w.uniq_cap * 16))) return rc;
+  if ((rc = dalloc(e, (void**)&w.uc, w.uniq_cap * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.t_counts, w.table_cap * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.t_offs, (w.table_cap + 1) * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.t_bytes, w.bytes_cap))) return rc;
+  e->lens_cap = std::max<uint64_t>(w.table_cap, w.long_cap) + 1;
+  if ((rc = dalloc(e, (void**)&e->d_lens, e->lens_cap * 8))) return rc;
+  return MOX_OK;
+}
+
+bool caps_cover(const Caps& have, const Caps& need) {
+  return have.pool_cap >= need.pool_cap && have.w_cap >= need.w_cap && have.u_cap >= need.u_cap &&
+         have.arena_cap >= need.arena_cap && have.long_cap >= need.long_cap && have.table_cap >= need.table_cap &&
+         have.bytes_cap >= need.bytes_cap;
+}
+
+Caps caps_max(const Caps& a, const Caps& b) {
+  return Caps{std::max(a.pool_cap, b.pool_cap), std::max(a.w_cap, b.w_cap), std::max(a.u_cap, b.u_cap),
+              std::max(a.arena_cap, b.arena_cap), std::max(a.long_cap, b.long_cap),
+              std::max(a.table_cap, b.table_cap), std::max(a.bytes_cap, b.bytes_cap)};
+}
+
+int ensure_caps(mox_engine* e, const Caps& need) {
+  if (e->w.pool && caps_cover(caps_of(e->w), need)) return MOX_OK;
+  Caps c = e->w.pool ? caps_max(caps_of(e->w), need) : need;
+  return realloc_sized(e, c);
+}
+
+int alloc_fixed(mox_engine* e) {
+  Work& w = e->w;
+  int rc;
+  if ((rc = dalloc(e, (void**)&w.ctl, sizeof(Ctl)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.cand_key, CAND_SLOTS * 8 * 2))) return rc;
+  w.cand_cnt = w.cand_key + CAND_SLOTS;
+  if ((rc = dalloc(e, (void**)&w.dict_img, DICT_SLOTS * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_cnt, (size_t)e->n_cu * DICT_SLOTS * 4))) return rc;
+  // bucket directory block: one allocation, zeroed per run
+  size_t dir_bytes = NB * 4 + NB * 8 + NB * 4 + 2 * NB * 4 + 3 * (NB + 1) * 8 + NB * 8 + (NB + 1) * 8;
+  uint8_t* d;
+  if ((rc = dalloc(e, (void**)&d, dir_bytes))) return rc;
+  w.b_chunks = (uint32_t*)d; d += NB * 4;
+  w.b_recs = (uint64_t*)d; d += NB * 8;
+  w.b_w = (uint32_t*)d; d += NB * 4;
+  w.b_cur = (uint32_t*)d; d += 2 * NB * 4;
+  w.dir_off = (uint64_t*)d; d += (NB + 1) * 8;
+  w.w_off = (uint64_t*)d; d += (NB + 1) * 8;
+  w.rec_off = (uint64_t*)d; d += (NB + 1) * 8;
+  w.b_uniq = (uint64_t*)d; d += NB * 8;
+  w.uniq_off = (uint64_t*)d; d += (NB + 1) * 8;
+  if ((rc = dalloc(e, (void**)&w.scan_part, (SCAN_WGS + 1) * 8))) return rc;
+  // Unicode tables
+  size_t tb = (2 * MOX_LOWER_N + 2 * MOX_CASED_N + 2 * MOX_CI_N) * 4;
+  uint32_t* t;
+  if ((rc = dalloc(e, (void**)&t, tb))) return rc;
+  uint32_t* p = t;
+  HIPCHK(hipMemcpy(p, mox_lower_src, MOX_LOWER_N * 4, hipMemcpyHostToDevice)); e->tables.lower_src = p; p += MOX_LOWER_N;
+  HIPCHK(hipMemcpy(p, mox_lower_dst, MOX_LOWER_N * 4, hipMemcpyHostToDevice)); e->tables.lower_dst = p; p += MOX_LOWER_N;
+  HIPCHK(hipMemcpy(p, mox_cased_lo, MOX_CASED_N * 4, hipMemcpyHostToDevice)); e->tables.cased_lo = p; p += MOX_CASED_N;
+  HIPCHK(hipMemcpy(p, mox_cased_hi, MOX_CASED_N * 4, hipMemcpyHostToDevice)); e->tables.cased_hi = p; p += MOX_CASED_N;
+  HIPCHK(hipMemcpy(p, mox_ci_lo, MOX_CI_N * 4, hipMemcpyHostToDevice)); e->tables.ci_lo = p; p += MOX_CI_N;
+  HIPCHK(hipMemcpy(p, mox_ci_hi, MOX_CI_N * 4, hipMemcpyHostToDevice)); e->tables.ci_hi = p; p += MOX_CI_N;
+  e->tables.n_lower = MOX_LOWER_N;
+  e->tables.n_cased = MOX_CASED_N;
+  e->tables.n_ci = MOX_CI_N;
+  HIPCHK(hipHostMalloc((void**)&e->h_ctl, sizeof(Ctl), hipHostMallocDefault));
+  HIPCHK(hipHostMalloc((void**)&e->h_ctl_init, sizeof(Ctl), hipHostMallocDefault));
+  memset(e->h_ctl_init, 0, sizeof(Ctl));
+  e->h_ctl_init->err_utf8 = ~0ull;
+  e->h_ctl_init->halo_err = ~0ull;
+  HIPCHK(hipMemset(w.dict_img, 0, DICT_SLOTS * 8));
+  return MOX_OK;
+}
+
+size_t map_lds_bytes() {
+  return (16 + TILE + 32 + 16) + (MAP_THREADS + 4) * 4 + DICT_SLOTS * 8 + DICT_SLOTS * 4 + NB * QDEPTH * 16 + 3 * NB * 4 + 64;
+}
+size_t reduce_lds_bytes() { return 4 * RT_SLOTS * 8 + RT_SLOTS * 2 + 64; }
+
+// exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)
+int launch_scan(mox_engine* e, const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
+                uint64_t* out) {
+  hipLaunchKernelGGL(k_scan_reduce, dim3(SCAN_WGS), dim3(SCAN_THREADS), 0, e->stream, v, n_ptr, n_const, n_cap,
+                     e->w.scan_part);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(64), 0, e->stream, e->w.scan_part, SCAN_WGS);
+  hipLaunchKernelGGL(k_scan_apply, dim3(SCAN_WGS), dim3(SCAN_THREADS), 0, e->stream, v, n_ptr, n_const, n_cap,
+                     (const uint64_t*)e->w.scan_part, out);
+  return MOX_OK;
+}
+
+float ev_ms(mox_engine* e, int a, int b) {
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, e->ev[a], e->ev[b]) != hipSuccess) return 0;
+  return ms;
+}
+
+// One attempt of the whole device pipeline.  Returns MOX_OK after the control
+// block has been read back into e->h_ctl (caller inspects overflow / errors).
+int pipeline_once(mox_engine* e, const Corpus& c) {
+  Work& w = e->w;
+  hipStream_t s = e->stream;
+  const bool timing = (e->flags & MOX_F_TIMING) != 0;
+  auto rec = [&](int i) {
+    if (timing) (void)hipEventRecord(e->ev[i], s);
+  };
+  rec(0);
+  HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_init, sizeof(Ctl), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(w.b_chunks, 0, NB * 4 + NB * 8 + NB * 4, s));
+  HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
+  // 1. hot dictionary from a sample
+  if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
+    HIPCHK(hipMemsetAsync(w.cand_key, 0, CAND_SLOTS * 16, s));
+    hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
+    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
+  }
+  rec(1);
+  // 2. map: one streaming pass over the corpus
+  uint64_t tile0 = c.own_lo & ~15ull;
+  uint64_t ntiles = c.own_hi > c.own_lo ? (c.own_hi - tile0 + TILE - 1) / TILE : 0;
+  int grid = e->n_cu;
+  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, ntiles);
+  rec(2);
+  // 3. lanes
+  hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
+  hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w, (uint32_t)grid);
+  rec(3);
+  // 4. shuffle directory + bucket reduce
+  hipLaunchKernelGGL(k_hist, dim3(512), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(NB), 0, s, w);
+  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);
+  rec(4);
+  // 5. table
+  hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(64), 0, s, w);
+  hipLaunchKernelGGL(k_long_flags, dim3(256), dim3(256), 0, s, w, e->d_lens);
+  launch_scan(e, e->d_lens, nullptr, w.long_cap, w.long_cap, w.lpos);
+  hipLaunchKernelGGL(k_mat_counts, dim3(1024), dim3(256), 0, s, w, e->d_lens);
+  hipLaunchKernelGGL(k_mat_long, dim3(256), dim3(256), 0, s, w, e->d_lens);
+  launch_scan(e, e->d_lens, &w.ctl->n_total, 0, w.table_cap, w.t_offs);
+  hipLaunchKernelGGL(k_mat_bytes, dim3(1024), dim3(256), 0, s, w, c);
+  rec(5);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_ctl, w.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (timing) {
+    e->stats.ms_dict = ev_ms(e, 0, 1);
+    e->stats.ms_map = ev_ms(e, 1, 2);
+    e->stats.ms_lanes = ev_ms(e, 2, 3);
+    e->stats.ms_reduce = ev_ms(e, 3, 4);
+    e->stats.ms_finalize = ev_ms(e, 4, 5);
+    e->stats.ms_run = ev_ms(e, 0, 5);
+  }
+  return MOX_OK;
+}
+
+int run_corpus(mox_engine* e, const Corpus& c) {
+  e->have_result = false;
+  uint64_t n = c.own_hi - c.own_lo;
+  int rc = ensure_caps(e, initial_caps(n, e->n_cu));
+  if (rc) return rc;
+  e->stats.retries = 0;
+  for (int attempt = 0;; attempt++) {
+    if ((rc = pipeline_once(e, c))) return rc;
+    const Ctl& h = *e->h_ctl;
+    if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
+    if (h.halo_err != ~0ull)
+      return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
+    if (!h.overflow) break;
+    if (attempt >= 4) return fail(MOX_ENOMEM, "buffer growth did not converge (overflow mask 0x%x)", h.overflow);
+    Caps need = caps_of(e->w);
+    if (h.overflow & OVF_POOL) need.pool_cap = h.pool_next + h.pool_next / 4 + 1024;
+    if (h.overflow & OVF_W) need.w_cap = h.w_n + h.w_n / 4 + 1024;
+    if (h.overflow & OVF_U) need.u_cap = h.u_n + h.u_n / 4 + 1024;
+    if (h.overflow & OVF_ARENA) need.arena_cap = h.arena_n + h.arena_n / 4 + 65536;
+    if (h.overflow & OVF_LONG) need.long_cap = next_pow2(2 * h.long_n + 1024);
+    if (h.overflow & OVF_TABLE) need.table_cap = h.n_total + h.n_total / 4 + 1024;
+    if (h.overflow & OVF_BYTES) need.bytes_cap = h.bytes_total + h.bytes_total / 4 + 65536;
+    // a table overflow also means the byte estimate is stale
+    if (h.overflow & OVF_TABLE) need.bytes_cap = std::max(need.bytes_cap, need.table_cap * 16);
+    e->stats.retries++;
+    if ((rc = ensure_caps(e, need))) return rc;
+  }
+  const Ctl& h = *e->h_ctl;
+  e->stats.bytes = n;
+  e->stats.tokens = h.tokens;
+  e->stats.uniques = h.n_total;
+  e->stats.dict_words = h.dict_n;
+  e->stats.cold_records = h.cold_recs;
+  e->stats.weighted_records = h.w_n;
+  e->stats.unicode_tokens = h.u_n;
+  e->stats.long_tokens = h.long_n;
+  e->stats.chunks = h.pool_next;
+  e->stats.max_subpasses = h.max_sub ? h.max_sub : 1;
+  e->last_corpus = c;
+  e->have_result = true;
+  return MOX_OK;
+}
+
+Corpus make_corpus(const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end, int at_end) {
+  uintptr_t addr = (uintptr_t)d_buf;
+  uint64_t mis = addr & 15;
+  Corpus c{};
+  c.base = (const uint8_t*)(addr - mis);
+  c.lo = mis;
+  c.hi = mis + buf_len;
+  c.own_lo = mis + own_begin;
+  c.own_hi = mis + own_end;
+  c.ctx_lo = mis;
+  c.at_end = at_end ? 1 : 0;
+  return c;
+}
+
+}  // namespace
+
+// ============================================================== C ABI
+extern "C" {
+
+const char* mox_last_error(void) { return g_err.c_str(); }
+int mox_abi_version(void) { return MOX_ABI_VERSION; }
+
+int mox_engine_create(const mox_config* cfg, mox_engine** out) {
+  if (!out) return fail(MOX_EINVAL, "out is NULL");
+  *out = nullptr;
+  mox_engine* e = new (std::nothrow) mox_engine();
+  if (!e) return fail(MOX_ENOMEM, "host allocation failed");
+  int dev = -1;
+  if (cfg) {
+    dev = cfg->device;
+    e->flags = cfg->flags;
+    if (cfg->dict_words) e->dict_words = std::min<uint32_t>(cfg->dict_words, DICT_MAX_WORDS);
+    if (cfg->sample_pieces) e->sample_pieces = std::min<uint32_t>(cfg->sample_pieces, 4096);
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
+    delete e;
+    return fail(MOX_EHIP, "no HIP device available");
+  }
+  if (dev < 0) {
+    if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  }
+  if (dev >= ndev) {
+    delete e;
+    return fail(MOX_EINVAL, "device %d out of range (%d devices)", dev, ndev);
+  }
+  e->device = dev;
+  hipError_t herr = hipSetDevice(dev);
+  if (herr != hipSuccess) { delete e; return fail(MOX_EHIP, "hipSetDevice: %s", hipGetErrorString(herr)); }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) == hipSuccess) e->n_cu = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete e;
+    return fail(MOX_EHIP, "hipStreamCreate failed");
+  }
+  for (auto& ev : e->ev) (void)hipEventCreate(&ev);
+  if (hipFuncSetAttribute((const void*)k_map, hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes()) != hipSuccess) {
+    mox_engine_destroy(e);
+    return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
+  }
+  int rc = alloc_fixed(e);
+  if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));
+  if (rc != MOX_OK) {
+    std::string msg = g_err;
+    mox_engine_destroy(e);
+    g_err = msg;
+    return rc;
+  }
+  *out = e;
+  return MOX_OK;
+}
+
+void mox_engine_destroy(mox_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  if (e->comm) ncclCommDestroy(e->comm);
+  Work& w = e->w;
+  void* ptrs[] = {w.ctl, w.cand_key, w.dict_img, w.dict_cnt, w.b_chunks, w.scan_part, (void*)e->tables.lower_src,
+                  w.pool, w.chunk_bucket, w.chunk_fill, w.dir, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
+                  w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_lens, e->d_text};
+  for (void* p : ptrs) dfree(p);
+  if (e->h_ctl) (void)hipHostFree(e->h_ctl);
+  if (e->h_ctl_init) (void)hipHostFree(e->h_ctl_init);
+  for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
+  if (e->stream) (void)hipStreamDestroy(e->stream);
+  delete e;
+}
+
+int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end, int at_corpus_end) {
+  if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (!d_buf && buf_len) return fail(MOX_EINVAL, "buffer is NULL");
+  if (own_begin > own_end || own_end > buf_len) return fail(MOX_EINVAL, "bad own range [%zu, %zu) of %zu", own_begin, own_end, buf_len);
+  if (own_begin > 0 && own_begin < 4) return fail(MOX_EINVAL, "own_begin must be 0 (corpus start) or >= 4 (left context)");
+  HIPCHK(hipSetDevice(e->device));
+  // an empty corpus has no tokens (reference: empty file -> empty map); any
+  // valid device address serves as its base
+  Corpus c = make_corpus(buf_len ? d_buf : (const void*)e->w.ctl, buf_len, own_begin, own_end, at_corpus_end);
+  return run_corpus(e, c);
+}
+
+int mox_run_device(mox_engine* e, const void* d_text, size_t len) { return mox_run_range(e, d_text, len, 0, len, 1); }
+
+int mox_fetch_table(mox_engine* e, mox_table** out) {
+  if (!e || !out) return fail(MOX_EINVAL, "NULL argument");
+  *out = nullptr;
+  if (!e->have_result) return fail(MOX_ESTATE, "no result: run first");
+  HIPCHK(hipSetDevice(e->device));
+  const bool timing = (e->flags & MOX_F_TIMING) != 0;
+  if (timing) HIPCHK(hipEventRecord(e->ev[6], e->stream));
+  const Ctl& h = *e->h_ctl;
+  uint64_t n = h.n_total, nb = h.bytes_total;
+  size_t bytes = sizeof(mox_table) + (n + 1) * 8 * 2 + nb + 16;
+  uint8_t* mem = (uint8_t*)malloc(bytes);
+  if (!mem) return fail(MOX_ENOMEM, "host allocation of %zu bytes failed", bytes);
+  mox_table* t = (mox_table*)mem;
+  uint64_t* counts = (uint64_t*)(mem + sizeof(mox_table));
+  uint64_t* offs = counts + n + 1;
+  uint8_t* wb = (uint8_t*)(offs + n + 1);
+  t->n = n;
+  t->tokens = h.tokens;
+  t->counts = counts;
+  t->offs = offs;
+  t->bytes = wb;
+  if (n) {
+    HIPCHK(hipMemcpyAsync(counts, e->w.t_counts, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(offs, e->w.t_offs, (n + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+    if (nb) HIPCHK(hipMemcpyAsync(wb, e->w.t_bytes, nb, hipMemcpyDeviceToHost, e->stream));
+  } else {
+    offs[0] = 0;
+  }
+  if (timing) HIPCHK(hipEventRecord(e->ev[7], e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (timing) e->stats.ms_d2h = ev_ms(e, 6, 7);
+  *out = t;
+  return MOX_OK;
+}
+
+void mox_table_free(mox_table* t) { free(t); }
+
+int mox_get_stats(const mox_engine* e, mox_stats* out) {
+  if (!e || !out) return fail(MOX_EINVAL, "NULL argument");
+  *out = e->stats;
+  return MOX_OK;
+}
+
+static int stage_host(mox_engine* e, const uint8_t* text, size_t len) {
+  if (len > e->d_text_cap) {
+    dfree(e->d_text);
+    e->d_text = nullptr;
+    e->d_text_cap = 0;
+    int rc = dalloc(e, (void**)&e->d_text, len + 64);
+    if (rc) return rc;
+    e->d_text_cap = len;
+  }
+  const bool timing = (e->flags & MOX_F_TIMING) != 0;
+  if (timing) HIPCHK(hipEventRecord(e->ev[8], e->stream));
+  if (len) HIPCHK(hipMemcpyAsync(e->d_text, text, len, hipMemcpyHostToDevice, e->stream));
+  if (timing) HIPCHK(hipEventRecord(e->ev[9], e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (timing) e->stats.ms_h2d = ev_ms(e, 8, 9);
+  return MOX_OK;
+}
+
+int mox_count(mox_engine* e, const uint8_t* text, size_t len, mox_table** out) {
+  if (!e || !out || (!text && len)) return fail(MOX_EINVAL, "NULL argument");
+  *out = nullptr;
+  HIPCHK(hipSetDevice(e->device));
+  int rc = stage_host(e, text, len);
+  if (rc) return rc;
+  if ((rc = mox_run_range(e, len ? (const void*)e->d_text : nullptr, len, 0, len, 1))) return rc;
+  return mox_fetch_table(e, out);
+}
+
+int mox_count_file(mox_engine* e, const char* path, mox_table** out) {
+  if (!e || !path || !out) return fail(MOX_EINVAL, "NULL argument");
+  *out = nullptr;
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return fail(MOX_EIO, "cannot open %s: %s", path, strerror(errno));
+  struct stat st;
+  if (fstat(fd, &st) != 0) { close(fd); return fail(MOX_EIO, "cannot stat %s: %s", path, strerror(errno)); }
+  size_t len = (size_t)st.st_size;
+  const uint8_t* p = nullptr;
+  if (len) {
+    void* m = mmap(nullptr, len, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) { close(fd); return fail(MOX_EIO, "cannot mmap %s: %s", path, strerror(errno)); }
+    p = (const uint8_t*)m;
+  }
+  close(fd);
+  int rc = mox_count(e, p, len, out);
+  if (len) munmap((void*)p, len);
+  return rc;
+}
+
+int mox_device_alloc(mox_engine* e, size_t bytes, void** d_ptr) {
+  if (!e || !d_ptr) return fail(MOX_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(e->device));
+  return dalloc(e, d_ptr, bytes);
+}
+int mox_device_free(mox_engine* e, void* d_ptr) {
+  if (!e) return fail(MOX_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(e->device));
+  if (d_ptr) HIPCHK(hipFree(d_ptr));
+  return MOX_OK;
+}
+int mox_memcpy_h2d(mox_engine* e, void* d_dst, const void* h_src, size_t bytes) {
+  if (!e || (!d_dst && bytes) || (!h_src && bytes)) return fail(MOX_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(e->device));
+  if (bytes) HIPCHK(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return MOX_OK;
+}
+int mox_memcpy_d2h(mox_engine* e, void* h_dst, const void* d_src, size_t bytes) {
+  if (!e || (!d_src && bytes) || (!h_dst && bytes)) return fail(MOX_EINVAL, "NULL argument");
+  HIPCHK(hipSetDevice(e->device));
+  if (bytes) HIPCHK(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return MOX_OK;
+}
+int mox_synchronize(mox_engine* e) {
+  if (!e) return fail(MOX_EINVAL, "NULL argument");
+  HIPCHK(hipStreamSynchronize(e->stream));
+  return MOX_OK;
+}
+
+// ---- output layer (reference L5) ----
+int mox_write_final_result(const mox_table* t, const char* path) {
+  if (!t || !path) return fail(MOX_EINVAL, "NULL argument");
+  FILE* f = fopen(path, "wb");
+  if (!f) return fail(MOX_EIO, "cannot open %s: %s", path, strerror(errno));
+  std::vector<char> buf;
+  buf.reserve(1 << 20);
+  char num[32];
+  for (uint64_t i = 0; i < t->n; i++) {
+    buf.insert(buf.end(), t->bytes + t->offs[i], t->bytes + t->offs[i + 1]);
+    int k = snprintf(num, sizeof num, " %llu\n", (unsigned long long)t->counts[i]);
+    buf.insert(buf.end(), num, num + k);
+    if (buf.size() > (1u << 20)) {
+      if (fwrite(buf.data(), 1, buf.size(), f) != buf.size()) { fclose(f); return fail(MOX_EIO, "write failed"); }
+      buf.clear();
+    }
+  }
+  if (!buf.empty() && fwrite(buf.data(), 1, buf.size(), f) != buf.size()) { fclose(f); return fail(MOX_EIO, "write failed"); }
+  if (fclose(f) != 0) return fail(MOX_EIO, "close failed");
+  return MOX_OK;
+}
+
+int mox_print_top_words(const mox_table* t, size_t n) {
+  if (!t) return fail(MOX_EINVAL, "NULL argument");
+  std::vector<uint64_t> idx(t->n);
+  for (uint64_t i = 0; i < t->n; i++) idx[i] = i;
+  size_t k = std::min<size_t>(n, t->n);
+  std::partial_sort(idx.begin(), idx.begin() + k, idx.end(), [&](uint64_t a, uint64_t b) {
+    if (t->counts[a] != t->counts[b]) return t->counts[a] > t->counts[b];
+    return a < b;
+  });
+  printf("Top %zu words:\n", n);
+  for (size_t i = 0; i < k; i++) {
+    uint64_t j = idx[i];
+    printf("%.*s: %llu\n", (int)(t->offs[j + 1] - t->offs[j]), (const char*)t->bytes + t->offs[j],
+           (unsigned long long)t->counts[j]);
+  }
+  return MOX_OK;
+}
+
+// ---- multi-GPU ----
+int mox_comm_unique_id(uint8_t id[MOX_UNIQUE_ID_BYTES]) {
+  if (!id) return fail(MOX_EINVAL, "NULL argument");
+  static_assert(sizeof(ncclUniqueId) <= MOX_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId u;
+  RCCLCHK(ncclGetUniqueId(&u));
+  memset(id, 0, MOX_UNIQUE_ID_BYTES);
+  memcpy(id, &u, sizeof u);
+  return MOX_OK;
+}
+
+int mox_comm_init(mox_engine* e, int nranks, int rank, const uint8_t id[MOX_UNIQUE_ID_BYTES]) {
+  if (!e || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad communicator arguments");
+  HIPCHK(hipSetDevice(e->device));
+  if (e->comm) { ncclCommDestroy(e->comm); e->comm = nullptr; }
+  ncclUniqueId u;
+  memcpy(&u, id, sizeof u);
+  RCCLCHK(ncclCommInitRank(&e->comm, nranks, u, rank));
+  e->nranks = nranks;
+  e->rank = rank;
+  return MOX_OK;
+}
+
+int mox_exchange(mox_engine* e) {
+  if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (!e->comm) return fail(MOX_ESTATE, "mox_comm_init first");
+  return fail(MOX_ESTATE, "mox_exchange: not implemented yet");
+}
+
+}  // extern "C"

@@ -1,0 +1,148 @@
+// Internal layout shared by the HIP kernels (mox_kernels.hip) and the host
+// engine (mox_engine.hip).  Not part of the C ABI (include/mox.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mox {
+
+// ---- geometry ----
+constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
+constexpr int TILE = MAP_THREADS * 16;      // 16 KiB: one 16-byte segment per lane
+constexpr int PREFETCH = 3;                 // tiles in flight per workgroup (registers)
+constexpr int NB_LOG2 = 8;                  // cold-record partitions (hash top bits)
+constexpr int NB = 1 << NB_LOG2;
+constexpr int QDEPTH = 16;                  // per-partition LDS staging queue (records)
+constexpr int FLUSH = 8;                    // records per flush = 128 B, one full line
+constexpr int CHUNK_RECS = 256;             // records per pool chunk (4 KiB)
+constexpr int DICT_SLOTS = 4096;            // LDS hot-dictionary hash slots (8-byte keys)
+constexpr int DICT_MAX_WORDS = 3072;
+constexpr int CAND_SLOTS = 1 << 14;         // dictionary candidate table (global)
+constexpr int SAMPLE_PIECE = 64 * 1024;
+constexpr int SAMPLE_SLOTS = 8192;
+constexpr int RT_SLOTS = 4096;              // bucket-reduce LDS hash slots
+constexpr int RT_CAP = 3072;                // max uniques per reduce sub-pass
+constexpr int RED_THREADS = 1024;
+constexpr int SCAN_THREADS = 1024;
+constexpr int SCAN_TILE = SCAN_THREADS * 4;
+constexpr int SCAN_WGS = 1024;
+
+constexpr uint64_t LONG_TAG = 0xFF00000000000000ull;   // w1 marker of a hashed (long) key
+constexpr uint64_t LONG_LEN_MASK = 0x0000FFFFFFFFFFFFull;
+constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points into the arena
+
+enum : uint32_t {
+  OVF_POOL = 1u, OVF_W = 2u, OVF_U = 4u, OVF_LONG = 8u, OVF_ARENA = 16u, OVF_PROBE = 32u,
+  OVF_TABLE = 64u, OVF_BYTES = 128u
+};
+
+// Control block: counters written by the kernels, read back once per run.
+struct Ctl {
+  unsigned long long pool_next;   // cold chunks requested
+  unsigned long long w_n;         // weighted records requested
+  unsigned long long u_n;         // unicode tokens requested
+  unsigned long long arena_n;     // arena bytes requested
+  unsigned long long long_n;      // long-token inserts
+  unsigned long long long_uniq;   // distinct long words (table slots claimed)
+  unsigned long long tokens;
+  unsigned long long err_utf8;    // min invalid byte (buffer-relative), ~0 = none
+  unsigned long long halo_err;    // min token start that ran off a non-final buffer, ~0 = none
+  unsigned long long cold_recs;   // records over all buckets
+  unsigned long long n_short;     // distinct short words
+  unsigned long long n_total;     // table entries
+  unsigned long long bytes_total; // table bytes
+  unsigned int overflow;
+  unsigned int dict_n;
+  unsigned int dict_maxprobe;
+  unsigned int max_sub;
+  unsigned int dict_thresh;
+  unsigned int pad[3];
+};
+
+// Weighted record: a key with a count (dictionary totals, spills, Unicode-lane
+// short words, received partials).
+struct WRec {
+  uint64_t w0, w1, count;
+};
+// Unicode-lane token: position + length in the corpus.
+struct URec {
+  uint64_t pos;
+  uint64_t len;
+};
+// Long-word table slot (all fields accessed with atomics only).
+struct LSlot {
+  unsigned long long h;      // hash | 1, 0 = empty
+  unsigned long long ref;    // ref + 1 (0 = not yet published)
+  unsigned long long len;
+  unsigned long long count;
+};
+
+struct Tables {  // Unicode case data in device memory
+  const uint32_t* lower_src;
+  const uint32_t* lower_dst;
+  const uint32_t* cased_lo;
+  const uint32_t* cased_hi;
+  const uint32_t* ci_lo;
+  const uint32_t* ci_hi;
+  int n_lower, n_cased, n_ci;
+};
+
+struct Corpus {
+  const uint8_t* base;   // 16-byte aligned
+  uint64_t lo, hi;       // valid bytes [lo, hi) (internal coordinates)
+  uint64_t own_lo, own_hi;
+  uint64_t ctx_lo;       // own_lo == lo of corpus start? bytes < ctx_lo read as whitespace
+  int at_end;
+};
+
+struct Work {  // device buffers of one engine
+  Ctl* ctl;
+  // dictionary
+  unsigned long long* cand_key;   // CAND_SLOTS
+  unsigned long long* cand_cnt;   // CAND_SLOTS
+  unsigned long long* dict_img;   // DICT_SLOTS
+  uint32_t* dict_cnt;             // [map_grid][DICT_SLOTS]
+  // cold pool
+  uint4* pool;                    // pool_cap * CHUNK_RECS records of 16 B
+  uint32_t* chunk_bucket;         // pool_cap
+  uint32_t* chunk_fill;           // pool_cap
+  uint64_t pool_cap;
+  // weighted records
+  WRec* w;                        // w_cap
+  WRec* w_sorted;                 // w_cap
+  uint64_t w_cap;
+  // unicode lane
+  URec* u;                        // u_cap
+  uint64_t u_cap;
+  uint8_t* arena;                 // arena_cap
+  uint64_t arena_cap;
+  // long lane
+  LSlot* ltab;                    // long_cap (power of two)
+  uint64_t long_cap;
+  // bucket directory (NB + 1 each)
+  uint32_t* b_chunks;             // chunk count per bucket
+  uint64_t* b_recs;               // cold records per bucket
+  uint32_t* b_w;                  // weighted records per bucket
+  uint32_t* b_cur;                // scatter cursors (2 * NB)
+  uint64_t* dir_off;              // NB + 1 (chunk index offsets)
+  uint64_t* w_off;                // NB + 1
+  uint64_t* rec_off;              // NB + 1 (output region offsets)
+  uint64_t* b_uniq;               // NB
+  uint64_t* uniq_off;             // NB + 1
+  uint32_t* dir;                  // pool_cap chunk ids grouped by bucket
+  // reduce output (capacity = records)
+  uint4* uk;                      // keys
+  uint64_t* uc;                   // counts
+  uint64_t uniq_cap;
+  // long uniques compaction
+  uint64_t* lpos;                 // long_cap (scan of occupancy)
+  // final table
+  uint64_t* t_counts;             // table_cap
+  uint64_t* t_offs;               // table_cap + 1
+  uint8_t* t_bytes;               // bytes_cap
+  uint64_t table_cap, bytes_cap;
+  // scan scratch
+  uint64_t* scan_part;            // SCAN_WGS + 1
+};
+
+}  // namespace mox

@@ -1,0 +1,1079 @@
+// HIP kernels of the MI355X word-count engine (gfx950 / CDNA4, wave64).
+//
+// Hot path of the reference (/root/reference/src/main.rs:16-22):
+//   split_file (:36-51) -> map_phase/count_words (:53-101) -> write/read map files
+//   (:103-109, :152-168) -> reduce_phase (:111-150)
+// re-designed as (DESIGN.md has the data layout and rooflines):
+//   k_sample + k_dict_build   hot-word dictionary from a 64 x 64 KiB sample
+//   k_map                     one streaming pass over the corpus in HBM: 16 B/lane
+//                             coalesced loads, ASCII fast path (SWAR whitespace /
+//                             case classification, per-lane token extraction from a
+//                             32-byte window), UTF-8 validation + Unicode whitespace
+//                             on tiles with non-ASCII bytes, hot words counted in an
+//                             LDS dictionary, all other words emitted as exact 16-byte
+//                             keys into 256 hash partitions through LDS queues
+//                             (= the shuffle write, main.rs:103-109)
+//   k_unicode                 full Unicode lowercase + Final_Sigma for non-ASCII tokens
+//   k_dict_totals, k_hist, k_bucket_scan, k_scatter   shuffle directory
+//   k_reduce                  per-partition LDS hash group-by (= reduce_phase merge,
+//                             main.rs:132-134) + LDS bitonic sort by hash
+//   k_long_*                  words > 16 bytes: hashed keys, byte-compare resolution
+//   k_mat_* + scans           dense (word, count) table in HBM
+#include "mox_internal.h"
+
+namespace mox {
+
+// ------------------------------------------------------------------ helpers
+__device__ __forceinline__ uint64_t mix_hash(uint64_t w0, uint64_t w1) {
+  uint64_t h = (w0 ^ 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
+  h ^= (w1 + 0x94D049BB133111EBull) * 0xD6E8FEB86659FD93ull;
+  h ^= h >> 32;
+  h *= 0x9E3779B97F4A7C15ull;
+  h ^= h >> 29;
+  return h;
+}
+
+// per-byte masks, valid only when every byte < 0x80 (ASCII fast path)
+__device__ __forceinline__ uint32_t movemask8(uint64_t m80) {  // m80: 0x80 per selected byte
+  return (uint32_t)((((m80 >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+}
+__device__ __forceinline__ uint64_t zero_bytes80(uint64_t v) {  // exact: 0x80 where byte == 0
+  uint64_t t = (v & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
+  return ~(t | v | 0x7F7F7F7F7F7F7F7Full);
+}
+__device__ __forceinline__ uint64_t ws_bytes80(uint64_t x) {  // ASCII whitespace 09..0D, 20
+  uint64_t sp = zero_bytes80(x ^ 0x2020202020202020ull);
+  uint64_t ge9 = x + 0x7777777777777777ull;   // b + 0x77 >= 0x80  <=> b >= 9
+  uint64_t ge14 = x + 0x7272727272727272ull;  // b >= 14
+  return (sp | (ge9 & ~ge14)) & 0x8080808080808080ull;
+}
+__device__ __forceinline__ uint64_t lower_ascii(uint64_t x) {
+  uint64_t ge_a = x + 0x3F3F3F3F3F3F3F3Full;  // b >= 'A'
+  uint64_t gt_z = x + 0x2525252525252525ull;  // b >= 'Z'+1
+  return x | (((ge_a & ~gt_z) & 0x8080808080808080ull) >> 2);
+}
+__device__ __forceinline__ bool is_ascii_ws(uint32_t b) { return b == 0x20 || (b >= 9 && b <= 13); }
+__device__ __forceinline__ uint8_t ascii_lower(uint8_t b) { return (b >= 'A' && b <= 'Z') ? (uint8_t)(b + 32) : b; }
+__device__ __forceinline__ uint64_t fnv_step(uint64_t h, uint8_t b) { return (h ^ b) * 0x100000001b3ull; }
+constexpr uint64_t FNV0 = 0xcbf29ce484222325ull;
+
+__device__ __forceinline__ uint64_t lo_mask(int nbytes) {  // 0 <= nbytes <= 8
+  return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1);
+}
+
+// Corpus byte with out-of-range bytes reading as ' ' (whitespace).
+__device__ __forceinline__ uint8_t byte_at(const Corpus& c, uint64_t p) {
+  if (p < c.lo || p >= c.hi) return 0x20;
+  return c.base[p];
+}
+
+// Length of the Unicode White_Space char starting at p (0 if none), valid UTF-8 assumed.
+// Rust char::is_whitespace: 09-0D 20 | 85 A0 | 1680 | 2000-200A 2028 2029 202F 205F | 3000
+__device__ __forceinline__ int ws_len_at(const Corpus& c, uint64_t p) {
+  uint8_t b0 = byte_at(c, p);
+  if (b0 < 0x80) return is_ascii_ws(b0) ? 1 : 0;
+  if (b0 != 0xC2 && b0 != 0xE1 && b0 != 0xE2 && b0 != 0xE3) return 0;
+  uint8_t b1 = byte_at(c, p + 1);
+  if (b0 == 0xC2) return (b1 == 0x85 || b1 == 0xA0) ? 2 : 0;
+  uint8_t b2 = byte_at(c, p + 2);
+  if (b0 == 0xE1) return (b1 == 0x9A && b2 == 0x80) ? 3 : 0;
+  if (b0 == 0xE3) return (b1 == 0x80 && b2 == 0x80) ? 3 : 0;
+  if (b1 == 0x80) return ((b2 >= 0x80 && b2 <= 0x8A) || b2 == 0xA8 || b2 == 0xA9 || b2 == 0xAF) ? 3 : 0;
+  if (b1 == 0x81) return b2 == 0x9F ? 3 : 0;
+  return 0;
+}
+// Is byte p part of a whitespace char?
+__device__ __forceinline__ bool in_ws(const Corpus& c, uint64_t p) {
+  if (p < c.lo || p >= c.hi) return true;
+  if (ws_len_at(c, p) >= 1) return true;
+  if (p >= 1 && ws_len_at(c, p - 1) >= 2) return true;
+  if (p >= 2 && ws_len_at(c, p - 2) >= 3) return true;
+  return false;
+}
+__device__ __forceinline__ int lead_len(uint8_t b) {
+  if (b < 0x80) return 1;
+  if (b >= 0xC2 && b <= 0xDF) return 2;
+  if (b >= 0xE0 && b <= 0xEF) return 3;
+  if (b >= 0xF0 && b <= 0xF4) return 4;
+  return 0;  // continuation or never-valid byte
+}
+// UTF-8 validity of the byte at p (Rust core::str::from_utf8 rules), given
+// neighbours up to 3 bytes away.  Returns 0 ok, 1 invalid, 2 needs more halo.
+__device__ int utf8_check(const Corpus& c, uint64_t p) {
+  uint8_t b = c.base[p];
+  bool cont = (b & 0xC0) == 0x80;
+  bool must = false;
+  for (int k = 1; k <= 3; k++) {
+    if (p < c.lo + (uint64_t)k) break;
+    uint8_t q = c.base[p - k];
+    if (lead_len(q) > k && q >= 0xC0) { must = true; break; }
+  }
+  if (cont != must) return 1;
+  if (cont || b < 0x80) return 0;
+  int L = lead_len(b);
+  if (L == 0) return 1;
+  if (p + (uint64_t)L > c.hi) return c.at_end ? 1 : 2;
+  uint8_t b1 = c.base[p + 1];
+  if (b == 0xE0 && b1 < 0xA0) return 1;
+  if (b == 0xED && b1 > 0x9F) return 1;
+  if (b == 0xF0 && b1 < 0x90) return 1;
+  if (b == 0xF4 && b1 > 0x8F) return 1;
+  return 0;
+}
+
+// ------------------------------------------------------------------ long lane
+// Lowered byte i of a long word reference (corpus refs are ASCII tokens).
+__device__ __forceinline__ uint8_t ref_byte(const uint8_t* base, const uint8_t* arena, uint64_t ref, uint64_t i) {
+  if (ref & ARENA_BIT) return arena[(ref & ~ARENA_BIT) + i];
+  return ascii_lower(base[ref + i]);
+}
+__device__ bool long_equal(const uint8_t* base, const uint8_t* arena, uint64_t ra, uint64_t rb, uint64_t len) {
+  for (uint64_t i = 0; i < len; i++)
+    if (ref_byte(base, arena, ra, i) != ref_byte(base, arena, rb, i)) return false;
+  return true;
+}
+// Exact insert into the long-word table; every access is an atomic (memory-side,
+// coherent across XCDs).  Keys: (hash, len) + byte compare on hash equality.
+__device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint64_t ref, uint64_t len, uint64_t cnt) {
+  h |= 1;
+  uint64_t mask = w.long_cap - 1, slot = h & mask;
+  uint32_t spins = 0;
+  for (uint64_t probes = 0; probes <= mask; ) {
+    if (++spins > (1u << 24)) { atomicOr(&w.ctl->overflow, OVF_PROBE); return; }
+    LSlot* s = &w.ltab[slot];
+    unsigned long long cur = atomicCAS(&s->h, 0ull, (unsigned long long)h);
+    if (cur == 0) {
+      atomicExch(&s->len, (unsigned long long)len);
+      atomicExch(&s->ref, (unsigned long long)(ref + 1));
+      atomicAdd(&s->count, (unsigned long long)cnt);
+      atomicAdd(&w.ctl->long_uniq, 1ull);
+      return;
+    }
+    if (cur == h) {
+      unsigned long long r = atomicAdd(&s->ref, 0ull);
+      if (r == 0) continue;  // claimant still publishing: retry this slot
+      unsigned long long l = atomicAdd(&s->len, 0ull);
+      if (l == len && long_equal(base, w.arena, r - 1, ref, len)) {
+        atomicAdd(&s->count, (unsigned long long)cnt);
+        return;
+      }
+    }
+    slot = (slot + 1) & mask;
+    probes++;
+  }
+  atomicOr(&w.ctl->overflow, OVF_LONG);
+}
+
+// ------------------------------------------------------------------ map kernel
+struct MapLds {
+  uint8_t* tile;                 // 16 pre + TILE + 32 post
+  uint32_t* masks;               // MAP_THREADS + 1: ws16 | zero16 << 16
+  unsigned long long* dkey;      // DICT_SLOTS
+  uint32_t* dcnt;                // DICT_SLOTS
+  uint4* q;                      // NB * QDEPTH
+  uint32_t* qcnt;                // NB
+  uint32_t* ccur;                // NB current chunk (0xFFFFFFFF none)
+  uint32_t* cfill;               // NB
+  uint32_t* flags;               // [0] nonascii, [1] dict_n, [2] maxprobe
+};
+
+struct MapCtx {
+  Corpus c;
+  Work w;
+  MapLds s;
+  uint32_t dict_n, maxprobe;
+};
+
+__device__ __forceinline__ void spill_weighted(const MapCtx& m, uint64_t w0, uint64_t w1, uint64_t cnt) {
+  unsigned long long i = atomicAdd(&m.w.ctl->w_n, 1ull);
+  if (i < m.w.w_cap) m.w.w[i] = WRec{w0, w1, cnt};
+  else atomicOr(&m.w.ctl->overflow, OVF_W);
+}
+
+// A short word (lowered length <= 16, no NUL byte): exact 16-byte key.
+__device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_t w1) {
+  uint64_t h = mix_hash(w0, w1);
+  if (w1 == 0 && m.dict_n) {
+    uint32_t slot = (uint32_t)h & (DICT_SLOTS - 1);
+    for (uint32_t i = 0; i <= m.maxprobe; i++) {
+      unsigned long long k = m.s.dkey[slot];
+      if (k == w0) { atomicAdd(&m.s.dcnt[slot], 1u); return; }
+      if (k == 0) break;
+      slot = (slot + 1) & (DICT_SLOTS - 1);
+    }
+  }
+  uint32_t b = (uint32_t)(h >> (64 - NB_LOG2));
+  uint32_t pos = atomicAdd(&m.s.qcnt[b], 1u);
+  if (pos < QDEPTH) m.s.q[b * QDEPTH + pos] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+  else spill_weighted(m, w0, w1, 1);
+}
+
+// Any token, walked byte by byte from global memory (rare: long tokens, tokens
+// running past the 32-byte window, tiles with non-ASCII bytes).
+__device__ void generic_token(const MapCtx& m, uint64_t p) {
+  const Corpus& c = m.c;
+  uint64_t q = p;
+  bool nonascii = false, nul = false;
+  for (;;) {
+    if (q >= c.hi) {
+      if (!c.at_end) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - c.lo));
+      break;
+    }
+    uint8_t b = c.base[q];
+    if (b < 0x80) {
+      if (is_ascii_ws(b)) break;
+      nul |= (b == 0);
+      q++;
+    } else {
+      if (ws_len_at(c, q)) break;
+      nonascii = true;
+      q++;
+    }
+  }
+  uint64_t len = q - p;
+  if (nonascii) {
+    unsigned long long i = atomicAdd(&m.w.ctl->u_n, 1ull);
+    if (i < m.w.u_cap) m.w.u[i] = URec{p, len};
+    else atomicOr(&m.w.ctl->overflow, OVF_U);
+    return;
+  }
+  if (len <= 16 && !nul) {
+    uint64_t w0 = 0, w1 = 0;
+    for (uint64_t i = 0; i < len; i++) {
+      uint64_t b = ascii_lower(c.base[p + i]);
+      if (i < 8) w0 |= b << (8 * i); else w1 |= b << (8 * (i - 8));
+    }
+    short_word(m, w0, w1);
+    return;
+  }
+  uint64_t h = FNV0;
+  for (uint64_t i = 0; i < len; i++) h = fnv_step(h, ascii_lower(c.base[p + i]));
+  atomicAdd(&m.w.ctl->long_n, 1ull);
+  long_insert(m.w, c.base, h, p, len, 1);
+}
+
+// 16 bytes at aligned internal position p; out-of-range bytes read as ' '.
+__device__ __forceinline__ uint4 load16(const Corpus& c, uint64_t p) {
+  if (p + 16 <= c.lo || p >= c.hi) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+  uint4 v = *reinterpret_cast<const uint4*>(c.base + p);
+  if (p >= c.lo && p + 16 <= c.hi) return v;
+  uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    uint64_t q = p + k;
+    if (q < c.lo || q >= c.hi) {
+      int wi = k >> 2, sh = (k & 3) * 8;
+      wv[wi] = (wv[wi] & ~(0xFFu << sh)) | (0x20u << sh);
+    }
+  }
+  return make_uint4(wv[0], wv[1], wv[2], wv[3]);
+}
+
+__device__ __forceinline__ uint32_t nonascii16(uint4 v) { return (v.x | v.y | v.z | v.w) & 0x80808080u; }
+
+// Flush staged cold records: every partition with >= FLUSH records writes whole
+// 128-byte groups into its current chunk.  8 lanes per partition.
+__device__ void flush_queues(const MapCtx& m, bool final_flush) {
+  const int tid = threadIdx.x;
+  for (int base = 0; base < NB; base += MAP_THREADS / 8) {
+    int b = base + tid / 8, j = tid & 7;
+    uint32_t cnt = m.s.qcnt[b];
+    if (cnt > QDEPTH) cnt = QDEPTH;
+    uint32_t nflush = final_flush ? cnt : (cnt & ~(uint32_t)(FLUSH - 1));
+    // chunk bookkeeping by lane j == 0, broadcast through registers of the 8-lane group
+    uint32_t chunkA = 0xFFFFFFFFu, fillA = 0, chunkB = 0xFFFFFFFFu, split = nflush;
+    if (nflush) {
+      uint32_t cur = m.s.ccur[b], fill = m.s.cfill[b];
+      if (j == 0) {
+        if (cur == 0xFFFFFFFFu || fill >= CHUNK_RECS) {
+          if (cur != 0xFFFFFFFFu && cur < m.w.pool_cap) m.w.chunk_fill[cur] = fill;
+          unsigned long long c = atomicAdd(&m.w.ctl->pool_next, 1ull);
+          cur = (c < m.w.pool_cap) ? (uint32_t)c : 0xFFFFFFFEu;
+          if (c < m.w.pool_cap) m.w.chunk_bucket[c] = b; else atomicOr(&m.w.ctl->overflow, OVF_POOL);
+          fill = 0;
+        }
+        chunkA = cur; fillA = fill;
+        split = CHUNK_RECS - fill;
+        if (split < nflush) {
+          if (cur < m.w.pool_cap) m.w.chunk_fill[cur] = CHUNK_RECS;
+          unsigned long long c = atomicAdd(&m.w.ctl->pool_next, 1ull);
+          chunkB = (c < m.w.pool_cap) ? (uint32_t)c : 0xFFFFFFFEu;
+          if (c < m.w.pool_cap) m.w.chunk_bucket[c] = b; else atomicOr(&m.w.ctl->overflow, OVF_POOL);
+          m.s.ccur[b] = chunkB;
+          m.s.cfill[b] = nflush - split;
+        } else {
+          split = nflush;
+          m.s.ccur[b] = cur;
+          m.s.cfill[b] = fill + nflush;
+        }
+      }
+    }
+    // broadcast within the group of 8 lanes (same wave: lanes 8g..8g+7)
+    int leader = (threadIdx.x & 63) & ~7;
+    chunkA = __shfl(chunkA, leader);
+    fillA = __shfl(fillA, leader);
+    chunkB = __shfl(chunkB, leader);
+    split = __shfl(split, leader);
+    for (uint32_t r = j; r < nflush; r += 8) {
+      uint4 v = m.s.q[b * QDEPTH + r];
+      uint32_t ch = r < split ? chunkA : chunkB;
+      uint32_t pos = r < split ? fillA + r : r - split;
+      if (ch < m.w.pool_cap) m.w.pool[(uint64_t)ch * CHUNK_RECS + pos] = v;
+    }
+    // move the remainder (< FLUSH records) to the queue front
+    uint32_t rem = cnt - nflush;
+    uint4 keep = make_uint4(0, 0, 0, 0);
+    if ((uint32_t)j < rem) keep = m.s.q[b * QDEPTH + nflush + j];
+    __builtin_amdgcn_wave_barrier();
+    if ((uint32_t)j < rem) m.s.q[b * QDEPTH + j] = keep;
+    if (j == 0) m.s.qcnt[b] = rem;
+    if (final_flush && j == 0) {
+      uint32_t cur = m.s.ccur[b];
+      if (cur < m.w.pool_cap) m.w.chunk_fill[cur] = m.s.cfill[b];
+    }
+  }
+}
+
+// Fast path: the tile (plus 4 bytes before and 16 after) is pure ASCII.
+__device__ void tile_fast(const MapCtx& m, uint64_t tbase, unsigned long long& ntok) {
+  const int tid = threadIdx.x;
+  const uint8_t* lt = m.s.tile + 16 + tid * 16;
+  uint4 a = *reinterpret_cast<const uint4*>(lt);
+  uint4 bn = *reinterpret_cast<const uint4*>(lt + 16);
+  uint32_t mk = m.s.masks[tid], mn = m.s.masks[tid + 1];
+  uint32_t ws32 = (mk & 0xFFFFu) | (mn << 16);
+  uint32_t z32 = (mk >> 16) | (mn & 0xFFFF0000u);
+  uint8_t prev = lt[-1];
+  uint64_t p0 = tbase + (uint64_t)tid * 16;
+  uint32_t prevws = is_ascii_ws(prev) ? 1u : 0u;
+  if (p0 == m.c.lo && m.c.own_lo == m.c.lo) prevws = 1;  // corpus start
+  uint32_t start = (~ws32) & ((ws32 << 1) | prevws) & 0xFFFFu;
+  // ownership window [own_lo, own_hi)
+  if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
+  if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
+  ntok += __popc(start);
+  uint64_t W0 = ((uint64_t)a.y << 32) | a.x, W1 = ((uint64_t)a.w << 32) | a.z;
+  uint64_t W2 = ((uint64_t)bn.y << 32) | bn.x, W3 = ((uint64_t)bn.w << 32) | bn.z;
+  W0 = lower_ascii(W0); W1 = lower_ascii(W1); W2 = lower_ascii(W2); W3 = lower_ascii(W3);
+  while (start) {
+    int p = __builtin_ctz(start);
+    start &= start - 1;
+    uint32_t rest = ws32 >> p;
+    if (rest == 0) { generic_token(m, p0 + p); continue; }
+    int len = __builtin_ctz(rest);
+    if (p0 + p + len >= m.c.hi && !m.c.at_end) { generic_token(m, p0 + p); continue; }
+    if (len > 16 || ((z32 >> p) & ((len >= 32) ? ~0u : ((1u << len) - 1u)))) { generic_token(m, p0 + p); continue; }
+    int k = p >> 3, r = (p & 7) * 8;
+    uint64_t A = k ? W1 : W0, B = k ? W2 : W1, C = k ? W3 : W2;
+    uint64_t w0 = r ? (A >> r) | (B << (64 - r)) : A;
+    uint64_t w1 = r ? (B >> r) | (C << (64 - r)) : B;
+    if (len <= 8) { w0 &= lo_mask(len); w1 = 0; }
+    else w1 &= lo_mask(len - 8);
+    short_word(m, w0, w1);
+  }
+}
+
+// Slow path: validate UTF-8, find tokens with Unicode whitespace, walk each.
+__device__ void tile_slow(const MapCtx& m, uint64_t tbase, unsigned long long& ntok) {
+  const int tid = threadIdx.x;
+  uint64_t p0 = tbase + (uint64_t)tid * 16;
+  for (int j = 0; j < 16; j++) {
+    uint64_t p = p0 + j;
+    if (p < m.c.own_lo || p >= m.c.own_hi) continue;
+    int v = utf8_check(m.c, p);
+    if (v == 1) atomicMin(&m.w.ctl->err_utf8, (unsigned long long)(p - m.c.lo));
+    else if (v == 2) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - m.c.lo));
+    if (in_ws(m.c, p)) continue;
+    bool start = (p == m.c.lo && m.c.own_lo == m.c.lo) ? true : in_ws(m.c, p - 1);
+    // a continuation byte never starts a token (it follows its lead byte)
+    if (start && (m.c.base[p] & 0xC0) != 0x80) {
+      ntok++;
+      generic_token(m, p);
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t ntiles) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  MapCtx m;
+  m.c = c;
+  m.w = w;
+  uint8_t* sp = smem;
+  m.s.tile = sp; sp += 16 + TILE + 32 + 16;
+  m.s.masks = (uint32_t*)sp; sp += (MAP_THREADS + 4) * 4;
+  m.s.dkey = (unsigned long long*)sp; sp += DICT_SLOTS * 8;
+  m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
+  m.s.q = (uint4*)sp; sp += NB * QDEPTH * 16;
+  m.s.qcnt = (uint32_t*)sp; sp += NB * 4;
+  m.s.ccur = (uint32_t*)sp; sp += NB * 4;
+  m.s.cfill = (uint32_t*)sp; sp += NB * 4;
+  m.s.flags = (uint32_t*)sp; sp += 64;
+  const int tid = threadIdx.x;
+
+  for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) { m.s.dkey[i] = w.dict_img[i]; m.s.dcnt[i] = 0; }
+  for (int i = tid; i < NB; i += MAP_THREADS) { m.s.qcnt[i] = 0; m.s.ccur[i] = 0xFFFFFFFFu; m.s.cfill[i] = 0; }
+  m.dict_n = w.ctl->dict_n;
+  m.maxprobe = w.ctl->dict_maxprobe;
+  unsigned long long ntok = 0;
+
+  const uint64_t tile0 = c.own_lo & ~15ull;
+  const uint64_t G = gridDim.x;
+  // register prefetch ring: segment of tile t, plus pre/post halo words for lanes 0/1
+  uint4 ring[PREFETCH];
+  uint4 halo[PREFETCH];
+#pragma unroll
+  for (int k = 0; k < PREFETCH; k++) {
+    uint64_t t = blockIdx.x + k * G;
+    uint64_t tb = tile0 + t * TILE;
+    ring[k] = t < ntiles ? load16(c, tb + tid * 16) : make_uint4(0, 0, 0, 0);
+    halo[k] = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    if (t < ntiles && tid == 0 && tb >= 16) halo[k] = load16(c, tb - 16);
+    if (t < ntiles && tid == 1) halo[k] = load16(c, tb + TILE);
+  }
+  for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
+    const uint64_t tbase = tile0 + t * TILE;
+    uint4 cur = ring[0], hcur = halo[0];
+#pragma unroll
+    for (int k = 0; k + 1 < PREFETCH; k++) { ring[k] = ring[k + 1]; halo[k] = halo[k + 1]; }
+    {
+      uint64_t tn = t + PREFETCH * G;
+      uint64_t tb = tile0 + tn * TILE;
+      ring[PREFETCH - 1] = tn < ntiles ? load16(c, tb + tid * 16) : make_uint4(0, 0, 0, 0);
+      halo[PREFETCH - 1] = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+      if (tn < ntiles && tid == 0 && tb >= 16) halo[PREFETCH - 1] = load16(c, tb - 16);
+      if (tn < ntiles && tid == 1) halo[PREFETCH - 1] = load16(c, tb + TILE);
+    }
+    if (tid == 0) m.s.flags[0] = 0;
+    *reinterpret_cast<uint4*>(m.s.tile + 16 + tid * 16) = cur;
+    uint32_t na = nonascii16(cur);
+    if (tid == 0) { *reinterpret_cast<uint4*>(m.s.tile) = hcur; na |= hcur.w; }   // 4 bytes before
+    if (tid == 1) { *reinterpret_cast<uint4*>(m.s.tile + 16 + TILE) = hcur; na |= nonascii16(hcur); }
+    na &= 0x80808080u;
+    // whitespace / zero masks of this lane's 16 bytes (valid when the tile is ASCII)
+    uint64_t lo64 = ((uint64_t)cur.y << 32) | cur.x, hi64 = ((uint64_t)cur.w << 32) | cur.z;
+    uint32_t ws16 = movemask8(ws_bytes80(lo64)) | (movemask8(ws_bytes80(hi64)) << 8);
+    uint32_t z16 = movemask8(zero_bytes80(lo64)) | (movemask8(zero_bytes80(hi64)) << 8);
+    m.s.masks[tid] = ws16 | (z16 << 16);
+    if (tid == 1) {
+      uint64_t l = ((uint64_t)hcur.y << 32) | hcur.x, h = ((uint64_t)hcur.w << 32) | hcur.z;
+      uint32_t a = movemask8(ws_bytes80(l)) | (movemask8(ws_bytes80(h)) << 8);
+      uint32_t z = movemask8(zero_bytes80(l)) | (movemask8(zero_bytes80(h)) << 8);
+      m.s.masks[MAP_THREADS] = a | (z << 16);
+    }
+    __syncthreads();  // (A) previous flush done; flags reset visible
+    if (__any(na != 0) && (tid & 63) == 0) atomicOr(&m.s.flags[0], 1u);
+    __syncthreads();  // (B) tile, masks, flag visible
+    if (m.s.flags[0]) tile_slow(m, tbase, ntok);
+    else tile_fast(m, tbase, ntok);
+    __syncthreads();  // (C) all emits done
+    flush_queues(m, false);
+    // next iteration's barrier (A) orders this flush before the next emits
+  }
+  __syncthreads();
+  flush_queues(m, true);
+  __syncthreads();
+  // per-workgroup dictionary counts (summed by k_dict_totals)
+  for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) w.dict_cnt[(uint64_t)blockIdx.x * DICT_SLOTS + i] = m.s.dcnt[i];
+  // tokens: wave reduce then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) ntok += __shfl_down(ntok, off);
+  if ((tid & 63) == 0 && ntok) atomicAdd(&w.ctl->tokens, ntok);
+}
+
+// ------------------------------------------------------------------ dictionary
+// Sample pieces of the corpus, count short ASCII words per piece in LDS, merge
+// repeated ones into a global candidate table (all-atomic).  Heuristic only:
+// the dictionary decides speed, never counts.
+extern "C" __global__ __launch_bounds__(1024) void k_sample(Corpus c, Work w, uint32_t npieces) {
+  __shared__ unsigned long long skey[SAMPLE_SLOTS];
+  __shared__ uint32_t scnt[SAMPLE_SLOTS];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < SAMPLE_SLOTS; i += 1024) { skey[i] = 0; scnt[i] = 0; }
+  __syncthreads();
+  uint64_t span = c.own_hi - c.own_lo;
+  uint64_t stride = span / npieces;
+  uint64_t ps = c.own_lo + stride * blockIdx.x;
+  uint64_t pe = ps + SAMPLE_PIECE;
+  if (pe > c.own_hi) pe = c.own_hi;
+  uint64_t s0 = ps + (uint64_t)tid * (SAMPLE_PIECE / 1024);
+  uint64_t s1 = s0 + SAMPLE_PIECE / 1024;
+  if (s1 > pe) s1 = pe;
+  for (uint64_t p = s0; p < s1; p++) {
+    uint8_t b = c.base[p];
+    if (is_ascii_ws(b) || b >= 0x80) continue;
+    if (p > c.lo) { uint8_t pb = c.base[p - 1]; if (!is_ascii_ws(pb)) continue; }
+    uint64_t key = 0;
+    int len = 0;
+    bool ok = true;
+    for (uint64_t q = p; ; q++) {
+      uint8_t x = byte_at(c, q);
+      if (is_ascii_ws(x)) break;
+      if (x >= 0x80 || x == 0 || len == 8) { ok = false; break; }
+      key |= (uint64_t)ascii_lower(x) << (8 * len);
+      len++;
+    }
+    if (!ok || len == 0) continue;
+    uint64_t h = mix_hash(key, 0);
+    uint32_t slot = (uint32_t)h & (SAMPLE_SLOTS - 1);
+    for (int pr = 0; pr < 64; pr++) {
+      unsigned long long old = atomicCAS(&skey[slot], 0ull, (unsigned long long)key);
+      if (old == 0 || old == key) { atomicAdd(&scnt[slot], 1u); break; }
+      slot = (slot + 1) & (SAMPLE_SLOTS - 1);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < SAMPLE_SLOTS; i += 1024) {
+    uint64_t key = skey[i];
+    uint32_t n = scnt[i];
+    if (key == 0 || n < 2) continue;
+    uint64_t h = mix_hash(key, 0);
+    uint32_t slot = (uint32_t)(h >> 20) & (CAND_SLOTS - 1);
+    for (int pr = 0; pr < 128; pr++) {
+      unsigned long long old = atomicCAS(&w.cand_key[slot], 0ull, (unsigned long long)key);
+      if (old == 0 || old == key) { atomicAdd(&w.cand_cnt[slot], (unsigned long long)n); break; }
+      slot = (slot + 1) & (CAND_SLOTS - 1);
+    }
+  }
+}
+
+// Select the most frequent candidates and lay them out as the LDS hash image
+// (DICT_SLOTS slots, linear probing from mix_hash & (DICT_SLOTS-1)).
+extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
+  __shared__ unsigned long long img[DICT_SLOTS];
+  __shared__ uint32_t hist[64];
+  __shared__ uint32_t maxprobe, nsel, thresh_log2;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < DICT_SLOTS; i += 1024) img[i] = 0;
+  if (tid < 64) hist[tid] = 0;
+  if (tid == 0) { maxprobe = 0; nsel = 0; }
+  __syncthreads();
+  // threshold 2^b: the smallest b with #(count >= 2^b) <= max_words
+  for (int i = tid; i < CAND_SLOTS; i += 1024) {
+    uint64_t cnt = w.cand_cnt[i];
+    if (w.cand_key[i] != 0 && cnt >= 2) atomicAdd(&hist[63 - __clzll(cnt)], 1u);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t acc = 0, b = 64;
+    for (int k = 63; k >= 1; k--) { if (acc + hist[k] > max_words) break; acc += hist[k]; b = k; }
+    thresh_log2 = b;
+  }
+  __syncthreads();
+  const uint32_t tb = thresh_log2;
+  for (int i = tid; i < CAND_SLOTS && tb < 64; i += 1024) {
+    uint64_t key = w.cand_key[i];
+    if (key == 0 || w.cand_cnt[i] < (1ull << tb)) continue;
+    uint32_t slot = (uint32_t)mix_hash(key, 0) & (DICT_SLOTS - 1);
+    for (uint32_t pr = 0; pr < DICT_SLOTS; pr++) {
+      unsigned long long old = atomicCAS(&img[slot], 0ull, (unsigned long long)key);
+      if (old == 0) { atomicMax(&maxprobe, pr); atomicAdd(&nsel, 1u); break; }
+      slot = (slot + 1) & (DICT_SLOTS - 1);
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < DICT_SLOTS; i += 1024) w.dict_img[i] = img[i];
+  if (tid == 0) { w.ctl->dict_n = nsel; w.ctl->dict_maxprobe = maxprobe; w.ctl->dict_thresh = tb; }
+}
+
+// Sum the per-workgroup dictionary counts and emit them as weighted records.
+extern "C" __global__ void k_dict_totals(Work w, uint32_t map_grid) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= DICT_SLOTS) return;
+  uint64_t key = w.dict_img[s];
+  if (key == 0) return;
+  uint64_t tot = 0;
+  for (uint32_t g = 0; g < map_grid; g++) tot += w.dict_cnt[(uint64_t)g * DICT_SLOTS + s];
+  if (tot == 0) return;
+  unsigned long long i = atomicAdd(&w.ctl->w_n, 1ull);
+  if (i < w.w_cap) w.w[i] = WRec{key, 0, tot};
+  else atomicOr(&w.ctl->overflow, OVF_W);
+}
+
+// ------------------------------------------------------------------ Unicode lane
+__device__ bool t_in_ranges(uint32_t c, const uint32_t* lo, const uint32_t* hi, int n) {
+  int a = 0, b = n - 1;
+  while (a <= b) {
+    int m = (a + b) >> 1;
+    if (c < lo[m]) b = m - 1;
+    else if (c > hi[m]) a = m + 1;
+    else return true;
+  }
+  return false;
+}
+__device__ uint32_t t_lower(const Tables& T, uint32_t c) {
+  if (c < 0x80) return (c >= 'A' && c <= 'Z') ? c + 32 : c;
+  int a = 0, b = T.n_lower - 1;
+  while (a <= b) {
+    int m = (a + b) >> 1;
+    uint32_t s = T.lower_src[m];
+    if (c < s) b = m - 1;
+    else if (c > s) a = m + 1;
+    else return T.lower_dst[m];
+  }
+  return c;
+}
+__device__ __forceinline__ uint32_t dec_at(const uint8_t* s, uint64_t& i) {
+  uint8_t c = s[i];
+  if (c < 0x80) { i += 1; return c; }
+  if (c < 0xE0) { uint32_t v = ((c & 0x1Fu) << 6) | (s[i + 1] & 0x3Fu); i += 2; return v; }
+  if (c < 0xF0) { uint32_t v = ((c & 0x0Fu) << 12) | ((s[i + 1] & 0x3Fu) << 6) | (s[i + 2] & 0x3Fu); i += 3; return v; }
+  uint32_t v = ((c & 0x07u) << 18) | ((s[i + 1] & 0x3Fu) << 12) | ((s[i + 2] & 0x3Fu) << 6) | (s[i + 3] & 0x3Fu);
+  i += 4;
+  return v;
+}
+// decode the code point that ENDS right before byte i (valid UTF-8), moving i back
+__device__ __forceinline__ uint32_t dec_back(const uint8_t* s, uint64_t lo, uint64_t& i) {
+  uint64_t j = i - 1;
+  while (j > lo && (s[j] & 0xC0) == 0x80) j--;
+  uint64_t k = j;
+  uint32_t v = dec_at(s, k);
+  i = j;
+  return v;
+}
+__device__ __forceinline__ int enc_to(uint32_t cp, uint8_t* o) {
+  if (cp < 0x80) { o[0] = (uint8_t)cp; return 1; }
+  if (cp < 0x800) { o[0] = (uint8_t)(0xC0 | (cp >> 6)); o[1] = (uint8_t)(0x80 | (cp & 0x3F)); return 2; }
+  if (cp < 0x10000) {
+    o[0] = (uint8_t)(0xE0 | (cp >> 12)); o[1] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F)); o[2] = (uint8_t)(0x80 | (cp & 0x3F));
+    return 3;
+  }
+  o[0] = (uint8_t)(0xF0 | (cp >> 18)); o[1] = (uint8_t)(0x80 | ((cp >> 12) & 0x3F));
+  o[2] = (uint8_t)(0x80 | ((cp >> 6) & 0x3F)); o[3] = (uint8_t)(0x80 | (cp & 0x3F));
+  return 4;
+}
+
+// Rust str::to_lowercase of one token (full mapping + Final_Sigma), written to
+// the arena; then routed as a short key (weighted record) or a long word.
+extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
+  if (w.ctl->err_utf8 != ~0ull) return;  // invalid input: no result is produced anyway
+  uint64_t n = w.ctl->u_n;
+  if (n > w.u_cap) n = w.u_cap;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (uint64_t)gridDim.x * blockDim.x) {
+    URec r = w.u[t];
+    const uint8_t* s = c.base;
+    uint64_t cap = r.len + r.len / 2 + 4;
+    unsigned long long ao = atomicAdd(&w.ctl->arena_n, (unsigned long long)cap);
+    if (ao + cap > w.arena_cap) { atomicOr(&w.ctl->overflow, OVF_ARENA); continue; }
+    uint8_t* out = w.arena + ao;
+    uint64_t o = 0, i = r.pos, end = r.pos + r.len;
+    while (i < end) {
+      uint64_t at = i;
+      uint32_t cp = dec_at(s, i);
+      if (cp == 0x3A3) {
+        // Final_Sigma (Rust map_uppercase_sigma): cased before (skipping
+        // case-ignorable) and NOT (case-ignorable* cased) after, within the token.
+        bool fin = false;
+        uint64_t b = at;
+        while (b > r.pos) {
+          uint32_t pc = dec_back(s, r.pos, b);
+          if (t_in_ranges(pc, T.ci_lo, T.ci_hi, T.n_ci)) continue;
+          fin = t_in_ranges(pc, T.cased_lo, T.cased_hi, T.n_cased);
+          break;
+        }
+        if (fin) {
+          uint64_t f = i;
+          while (f < end) {
+            uint32_t nc = dec_at(s, f);
+            if (t_in_ranges(nc, T.ci_lo, T.ci_hi, T.n_ci)) continue;
+            if (t_in_ranges(nc, T.cased_lo, T.cased_hi, T.n_cased)) fin = false;
+            break;
+          }
+        }
+        o += enc_to(fin ? 0x3C2u : 0x3C3u, out + o);
+        continue;
+      }
+      uint32_t l = t_lower(T, cp);
+      if (l == 0x110000u) { o += enc_to(0x69u, out + o); o += enc_to(0x307u, out + o); }
+      else o += enc_to(l, out + o);
+    }
+    bool nul = false;
+    for (uint64_t k = 0; k < o; k++) nul |= (out[k] == 0);
+    if (o <= 16 && !nul) {
+      uint64_t w0 = 0, w1 = 0;
+      for (uint64_t k = 0; k < o; k++) {
+        if (k < 8) w0 |= (uint64_t)out[k] << (8 * k); else w1 |= (uint64_t)out[k] << (8 * (k - 8));
+      }
+      unsigned long long i2 = atomicAdd(&w.ctl->w_n, 1ull);
+      if (i2 < w.w_cap) w.w[i2] = WRec{w0, w1, 1};
+      else atomicOr(&w.ctl->overflow, OVF_W);
+    } else {
+      uint64_t h = FNV0;
+      for (uint64_t k = 0; k < o; k++) h = fnv_step(h, out[k]);
+      atomicAdd(&w.ctl->long_n, 1ull);
+      long_insert(w, c.base, h, ARENA_BIT | ao, o, 1);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ shuffle directory
+// Count chunks / records per bucket and weighted records per bucket.
+extern "C" __global__ void k_hist(Work w) {
+  __shared__ uint32_t hc[NB], hw[NB];
+  __shared__ unsigned long long hr[NB];
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) { hc[i] = 0; hw[i] = 0; hr[i] = 0; }
+  __syncthreads();
+  uint64_t nch = w.ctl->pool_next; if (nch > w.pool_cap) nch = w.pool_cap;
+  uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nch; i += stride) {
+    uint32_t b = w.chunk_bucket[i];
+    atomicAdd(&hc[b], 1u);
+    atomicAdd(&hr[b], (unsigned long long)w.chunk_fill[i]);
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
+    WRec r = w.w[i];
+    uint32_t b = (uint32_t)(mix_hash(r.w0, r.w1) >> (64 - NB_LOG2));
+    atomicAdd(&hw[b], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) {
+    if (hc[i]) atomicAdd(&w.b_chunks[i], hc[i]);
+    if (hr[i]) atomicAdd((unsigned long long*)&w.b_recs[i], hr[i]);
+    if (hw[i]) atomicAdd(&w.b_w[i], hw[i]);
+  }
+}
+
+extern "C" __global__ void k_bucket_scan(Work w) {  // one workgroup of NB threads
+  __shared__ uint64_t a[NB], bw[NB], r[NB];
+  int b = threadIdx.x;
+  a[b] = w.b_chunks[b];
+  bw[b] = w.b_w[b];
+  r[b] = w.b_recs[b] + w.b_w[b];
+  __syncthreads();
+  if (b == 0) {
+    uint64_t sa = 0, sw = 0, sr = 0, cold = 0;
+    for (int i = 0; i < NB; i++) {
+      w.dir_off[i] = sa; w.w_off[i] = sw; w.rec_off[i] = sr;
+      sa += a[i]; sw += bw[i]; sr += r[i];
+      cold += w.b_recs[i];
+    }
+    w.dir_off[NB] = sa; w.w_off[NB] = sw; w.rec_off[NB] = sr;
+    w.ctl->cold_recs = cold;
+  }
+  w.b_cur[b] = 0;
+  w.b_cur[NB + b] = 0;
+}
+
+extern "C" __global__ void k_scatter(Work w) {
+  uint64_t nch = w.ctl->pool_next; if (nch > w.pool_cap) nch = w.pool_cap;
+  uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nch; i += stride) {
+    uint32_t b = w.chunk_bucket[i];
+    uint32_t k = atomicAdd(&w.b_cur[b], 1u);
+    w.dir[w.dir_off[b] + k] = (uint32_t)i;
+  }
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
+    WRec r = w.w[i];
+    uint32_t b = (uint32_t)(mix_hash(r.w0, r.w1) >> (64 - NB_LOG2));
+    uint32_t k = atomicAdd(&w.b_cur[NB + b], 1u);
+    w.w_sorted[w.w_off[b] + k] = r;
+  }
+}
+
+// ------------------------------------------------------------------ bucket reduce
+struct RedLds {
+  unsigned long long* h;   // RT_SLOTS (hash | 1, 0 = empty)
+  unsigned long long* k0;  // RT_SLOTS (0 = not yet published)
+  unsigned long long* k1;
+  unsigned long long* cnt;
+  uint16_t* idx;           // RT_SLOTS
+  uint32_t* misc;          // [0] uniques, [1] overflow, [2] processed-at-overflow
+};
+
+__device__ __forceinline__ void red_insert(const RedLds& s, uint64_t h, uint64_t w0, uint64_t w1, uint64_t cnt) {
+  uint64_t hh = h | 1;
+  uint32_t slot = (uint32_t)(h >> 1) & (RT_SLOTS - 1);
+  for (uint32_t it = 0; it < (1u << 22); it++) {
+    unsigned long long cur = s.h[slot];
+    if (cur == 0) {
+      cur = atomicCAS(&s.h[slot], 0ull, (unsigned long long)hh);
+      if (cur == 0) {
+        s.k1[slot] = w1;
+        __threadfence_block();
+        atomicExch(&s.k0[slot], (unsigned long long)w0);
+        atomicAdd(&s.cnt[slot], (unsigned long long)cnt);
+        uint32_t u = atomicAdd(&s.misc[0], 1u);
+        if (u >= RT_CAP) s.misc[1] = 1;
+        return;
+      }
+    }
+    if (cur == hh) {
+      unsigned long long a0 = __atomic_load_n(&s.k0[slot], __ATOMIC_RELAXED);
+      if (a0 == 0) continue;  // claimant still publishing this slot: retry it
+      __threadfence_block();
+      if (a0 == w0 && s.k1[slot] == w1) { atomicAdd(&s.cnt[slot], (unsigned long long)cnt); return; }
+    }
+    slot = (slot + 1) & (RT_SLOTS - 1);
+  }
+  s.misc[1] = 1;
+}
+
+__device__ __forceinline__ bool red_less(const RedLds& s, uint16_t a, uint16_t b) {
+  if (a == 0xFFFF) return false;
+  if (b == 0xFFFF) return true;
+  uint64_t ha = s.h[a], hb = s.h[b];
+  if (ha != hb) return ha < hb;
+  if (s.k0[a] != s.k0[b]) return s.k0[a] < s.k0[b];
+  return s.k1[a] < s.k1[b];
+}
+
+extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  RedLds s;
+  uint8_t* sp = smem;
+  s.h = (unsigned long long*)sp; sp += RT_SLOTS * 8;
+  s.k0 = (unsigned long long*)sp; sp += RT_SLOTS * 8;
+  s.k1 = (unsigned long long*)sp; sp += RT_SLOTS * 8;
+  s.cnt = (unsigned long long*)sp; sp += RT_SLOTS * 8;
+  s.idx = (uint16_t*)sp; sp += RT_SLOTS * 2;
+  s.misc = (uint32_t*)sp; sp += 64;
+  const int tid = threadIdx.x;
+  const uint32_t b = blockIdx.x;
+  const uint64_t d0 = w.dir_off[b], d1 = w.dir_off[b + 1];
+  const uint64_t ws0 = w.w_off[b], ws1 = w.w_off[b + 1];
+  const uint64_t nrec = w.b_recs[b] + (ws1 - ws0);
+  const uint64_t out0 = w.rec_off[b];
+  uint32_t k_log2 = 0;
+  uint64_t written = 0;
+  uint32_t sub = 0;
+  while (sub < (1u << k_log2)) {
+    for (int i = tid; i < RT_SLOTS; i += RED_THREADS) { s.h[i] = 0; s.k0[i] = 0; s.k1[i] = 0; s.cnt[i] = 0; }
+    if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
+    __syncthreads();
+    const uint32_t kk = k_log2;
+    uint64_t seen = 0;  // records examined before an overflow was noticed (estimate for k)
+    // cold chunks: 4 chunks per pass of 1024 lanes, one 16-byte record per lane
+    for (uint64_t ci = d0; ci < d1; ci += RED_THREADS / CHUNK_RECS) {
+      uint64_t my = ci + tid / CHUNK_RECS;
+      uint32_t r = tid % CHUNK_RECS;
+      if (my < d1) {
+        uint32_t ch = w.dir[my];
+        if (r < w.chunk_fill[ch]) {
+          uint4 v = w.pool[(uint64_t)ch * CHUNK_RECS + r];
+          uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
+          uint64_t h = mix_hash(w0, w1);
+          if (kk == 0 || (uint32_t)((h << NB_LOG2) >> (64 - kk)) == sub) red_insert(s, h, w0, w1, 1);
+        }
+      }
+      seen += RED_THREADS;
+      __syncthreads();
+      const bool ovf = s.misc[1] != 0;
+      __syncthreads();
+      if (ovf) break;
+    }
+    if (!s.misc[1]) {
+      for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
+        WRec r = w.w_sorted[i];
+        uint64_t h = mix_hash(r.w0, r.w1);
+        if (kk == 0 || (uint32_t)((h << NB_LOG2) >> (64 - kk)) == sub) red_insert(s, h, r.w0, r.w1, r.count);
+      }
+      seen = nrec;
+    }
+    __syncthreads();
+    if (s.misc[1]) {
+      // too many distinct words for one LDS table: split this bucket into
+      // 2^k sub-ranges of the next hash bits and restart it
+      uint64_t est = (nrec + (seen ? seen : 1) - 1) / (seen ? seen : 1);
+      uint32_t need = kk + 1;
+      while ((1ull << need) < est * 2 && need < 20) need++;
+      k_log2 = need;
+      sub = 0;
+      written = 0;
+      __syncthreads();
+      continue;
+    }
+    // compact + bitonic sort (hash, key) for a deterministic order
+    const uint32_t nu = s.misc[0];
+    __syncthreads();
+    if (tid == 0) s.misc[3] = 0;
+    __syncthreads();
+    for (int i = tid; i < RT_SLOTS; i += RED_THREADS) {
+      if (s.h[i]) { uint32_t p = atomicAdd(&s.misc[3], 1u); s.idx[p] = (uint16_t)i; }
+    }
+    __syncthreads();
+    for (int i = nu + tid; i < RT_SLOTS; i += RED_THREADS) s.idx[i] = 0xFFFF;
+    uint32_t N = 1;
+    while (N < nu) N <<= 1;
+    __syncthreads();
+    for (uint32_t size = 2; size <= N; size <<= 1) {
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = tid; i < N / 2; i += RED_THREADS) {
+          uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+          bool up = (lo & size) == 0;
+          uint16_t a = s.idx[lo], c2 = s.idx[hi];
+          bool swap = up ? red_less(s, c2, a) : red_less(s, a, c2);
+          if (swap) { s.idx[lo] = c2; s.idx[hi] = a; }
+        }
+        __syncthreads();
+      }
+    }
+    for (uint32_t i = tid; i < nu; i += RED_THREADS) {
+      uint16_t sl = s.idx[i];
+      w.uk[out0 + written + i] = make_uint4((uint32_t)s.k0[sl], (uint32_t)(s.k0[sl] >> 32), (uint32_t)s.k1[sl],
+                                            (uint32_t)(s.k1[sl] >> 32));
+      w.uc[out0 + written + i] = s.cnt[sl];
+    }
+    written += nu;
+    sub++;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    w.b_uniq[b] = written;
+    if (k_log2) atomicMax(&w.ctl->max_sub, 1u << k_log2);
+  }
+}
+
+// ------------------------------------------------------------------ scans
+// Exclusive scan of v[0..n) (n = *n_ptr) into out[0..n], out[n] = total.
+// Three launches: per-WG totals, one-WG scan of totals, per-WG rescan + offset.
+extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint64_t* v, const unsigned long long* n_ptr,
+                                                                      uint64_t n_const, uint64_t n_cap, uint64_t* part) {
+  __shared__ uint64_t red[SCAN_THREADS / 64];
+  uint64_t n = n_ptr ? *n_ptr : n_const;
+  if (n > n_cap) n = n_cap;
+  uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  uint64_t a = per * blockIdx.x, e = a + per;
+  if (e > n) e = n;
+  uint64_t sum = 0;
+  for (uint64_t i = a + threadIdx.x; i < e; i += SCAN_THREADS) sum += v[i];
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (int i = 0; i < SCAN_THREADS / 64; i++) t += red[i];
+    part[blockIdx.x] = t;
+  }
+}
+extern "C" __global__ void k_scan_parts(uint64_t* part, int nparts) {  // one thread is plenty
+  if (threadIdx.x || blockIdx.x) return;
+  uint64_t s = 0;
+  for (int i = 0; i < nparts; i++) { uint64_t x = part[i]; part[i] = s; s += x; }
+  part[nparts] = s;
+}
+extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint64_t* v, const unsigned long long* n_ptr,
+                                                                     uint64_t n_const, uint64_t n_cap, const uint64_t* part,
+                                                                     uint64_t* out) {
+  __shared__ uint64_t wsum[SCAN_THREADS / 64];
+  __shared__ uint64_t carry;
+  uint64_t n = n_ptr ? *n_ptr : n_const;
+  if (n > n_cap) n = n_cap;
+  uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  uint64_t a = per * blockIdx.x, e = a + per;
+  if (e > n) e = n;
+  if (threadIdx.x == 0) carry = part[blockIdx.x];
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint64_t base = a; base < e; base += SCAN_THREADS) {
+    uint64_t i = base + threadIdx.x;
+    uint64_t x = i < e ? v[i] : 0;
+    uint64_t incl = x;
+    for (int off = 1; off < 64; off <<= 1) {
+      uint64_t y = __shfl_up(incl, off);
+      if (lane >= off) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    uint64_t wpre = 0, tot = 0;
+    for (int k = 0; k < SCAN_THREADS / 64; k++) { if (k < wv) wpre += wsum[k]; tot += wsum[k]; }
+    if (i < e) out[i] = carry + wpre + incl - x;
+    __syncthreads();
+    if (threadIdx.x == 0) carry += tot;
+    __syncthreads();
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = part[gridDim.x];
+}
+
+// ------------------------------------------------------------------ long-word compaction
+extern "C" __global__ void k_long_flags(Work w, uint64_t* flags) {
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w.long_cap; i += stride)
+    flags[i] = w.ltab[i].h != 0 ? 1 : 0;
+}
+
+// ------------------------------------------------------------------ table materialisation
+__device__ __forceinline__ uint32_t short_len(uint64_t w0, uint64_t w1) {
+  if (w1) return 16 - (__clzll(w1) >> 3);
+  return 8 - (__clzll(w0) >> 3);
+}
+
+// After k_reduce: total short uniques + offsets; n_total = short + long.
+extern "C" __global__ void k_final_scan(Work w) {  // one workgroup of NB threads
+  if (threadIdx.x == 0) {
+    uint64_t s = 0;
+    for (int i = 0; i < NB; i++) { w.uniq_off[i] = s; s += w.b_uniq[i]; }
+    w.uniq_off[NB] = s;
+    w.ctl->n_short = s;
+    unsigned long long nl = w.ctl->long_uniq;
+    w.ctl->n_total = s + nl;
+    if (s + nl > w.table_cap) atomicOr(&w.ctl->overflow, OVF_TABLE);
+  }
+}
+
+// counts + lengths in dense order; lengths go to t_offs[] (scanned in place afterwards)
+extern "C" __global__ void k_mat_counts(Work w, uint64_t* lens) {
+  __shared__ uint64_t uoff[NB + 1];
+  __shared__ uint64_t roff[NB + 1];
+  for (int i = threadIdx.x; i <= NB; i += blockDim.x) { uoff[i] = w.uniq_off[i]; roff[i] = w.rec_off[i]; }
+  __syncthreads();
+  uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
+  if (nt > w.table_cap) return;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    {
+      int a = 0, b = NB - 1;  // bucket with uoff[bk] <= i < uoff[bk+1]
+      while (a < b) { int m = (a + b + 1) >> 1; if (uoff[m] <= i) a = m; else b = m - 1; }
+      uint64_t src = roff[a] + (i - uoff[a]);
+      uint4 k = w.uk[src];
+      uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
+      w.t_counts[i] = w.uc[src];
+      lens[i] = short_len(w0, w1);
+    }
+  }
+}
+
+// long uniques in slot order: slot s occupied -> dense index ns + lpos[s]
+extern "C" __global__ void k_mat_long(Work w, uint64_t* lens) {
+  uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
+  if (nt > w.table_cap) return;
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
+    LSlot e = w.ltab[s];
+    if (!e.h) continue;
+    uint64_t i = ns + w.lpos[s];
+    w.t_counts[i] = e.count;
+    lens[i] = e.len;
+  }
+}
+
+extern "C" __global__ void k_mat_bytes(Work w, Corpus c) {
+  __shared__ uint64_t uoff[NB + 1];
+  __shared__ uint64_t roff[NB + 1];
+  for (int i = threadIdx.x; i <= NB; i += blockDim.x) { uoff[i] = w.uniq_off[i]; roff[i] = w.rec_off[i]; }
+  __syncthreads();
+  uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
+  if (nt > w.table_cap) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->bytes_total = w.t_offs[nt];
+  if (w.t_offs[nt] > w.bytes_cap) { if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&w.ctl->overflow, OVF_BYTES); return; }
+  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    int a = 0, b = NB - 1;
+    while (a < b) { int m = (a + b + 1) >> 1; if (uoff[m] <= i) a = m; else b = m - 1; }
+    uint64_t src = roff[a] + (i - uoff[a]);
+    uint4 k = w.uk[src];
+    uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
+    uint32_t L = short_len(w0, w1);
+    uint8_t* o = w.t_bytes + w.t_offs[i];
+    for (uint32_t j = 0; j < L; j++) o[j] = (uint8_t)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xFF);
+  }
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
+    LSlot e = w.ltab[s];
+    if (!e.h) continue;
+    uint64_t i = ns + w.lpos[s];
+    uint8_t* o = w.t_bytes + w.t_offs[i];
+    uint64_t ref = e.ref - 1;
+    for (uint64_t j = 0; j < e.len; j++) o[j] = ref_byte(c.base, w.arena, ref, j);
+  }
+}
+
+}  // namespace mox

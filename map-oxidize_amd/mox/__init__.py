@@ -1,0 +1,293 @@
+"""Python binding of the MI355X word-count engine (ctypes over include/mox.h).
+
+Host-side mirror of the reference's hot path (/root/reference/src/main.rs):
+
+* ``count_words(data)`` / ``Engine.count`` -- ``split_file`` + ``map_phase`` +
+  ``reduce_phase`` (main.rs:16-22): bytes -> {word: count}.  Invalid UTF-8 raises
+  ``Utf8Error`` (the reference's ``io::ErrorKind::InvalidData`` abort, main.rs:44).
+* ``Engine.count_file(path)`` -- the same from a file (main.rs:10, :36-51).
+* ``write_final_result`` / ``top_words`` -- the reference's output layer
+  (main.rs:170-192).
+
+The compute runs in libmox.so (HIP kernels for gfx950).  There is no CPU
+fallback: if the library is missing or no GPU is present, calls raise.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmox.so")
+
+MOX_OK = 0
+MOX_EINVAL = -1
+MOX_EUTF8 = -2
+MOX_ENOMEM = -3
+MOX_EHIP = -4
+MOX_EIO = -5
+MOX_ERCCL = -6
+MOX_ESTATE = -7
+MOX_EHALO = -8
+
+MOX_F_NO_DICT = 0x1
+MOX_F_TIMING = 0x4
+
+UNIQUE_ID_BYTES = 128
+
+
+class MoxError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("mox error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Utf8Error(MoxError):
+    """Input is not valid UTF-8 (reference: tokio lines() -> InvalidData)."""
+
+
+class Config(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int),
+        ("flags", ctypes.c_uint32),
+        ("dict_words", ctypes.c_uint32),
+        ("sample_pieces", ctypes.c_uint32),
+        ("reserve_bytes", ctypes.c_uint64),
+        ("reserved", ctypes.c_uint32 * 8),
+    ]
+
+
+class _Table(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("tokens", ctypes.c_uint64),
+        ("counts", ctypes.POINTER(ctypes.c_uint64)),
+        ("offs", ctypes.POINTER(ctypes.c_uint64)),
+        ("bytes", ctypes.POINTER(ctypes.c_uint8)),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("bytes", ctypes.c_uint64),
+        ("tokens", ctypes.c_uint64),
+        ("uniques", ctypes.c_uint64),
+        ("dict_words", ctypes.c_uint64),
+        ("cold_records", ctypes.c_uint64),
+        ("weighted_records", ctypes.c_uint64),
+        ("unicode_tokens", ctypes.c_uint64),
+        ("long_tokens", ctypes.c_uint64),
+        ("chunks", ctypes.c_uint64),
+        ("retries", ctypes.c_uint32),
+        ("max_subpasses", ctypes.c_uint32),
+        ("ms_run", ctypes.c_double),
+        ("ms_dict", ctypes.c_double),
+        ("ms_map", ctypes.c_double),
+        ("ms_lanes", ctypes.c_double),
+        ("ms_reduce", ctypes.c_double),
+        ("ms_finalize", ctypes.c_double),
+        ("ms_h2d", ctypes.c_double),
+        ("ms_d2h", ctypes.c_double),
+        ("ms_exchange", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib():
+    """Load libmox.so (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MoxError(MOX_ESTATE, "%s not built (run `make` or __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        P, U64, I, VP = ctypes.POINTER, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+        sz = ctypes.c_size_t
+        sig = {
+            "mox_last_error": ([], ctypes.c_char_p),
+            "mox_abi_version": ([], I),
+            "mox_engine_create": ([P(Config), P(VP)], I),
+            "mox_engine_destroy": ([VP], None),
+            "mox_count": ([VP, VP, sz, P(P(_Table))], I),
+            "mox_count_file": ([VP, ctypes.c_char_p, P(P(_Table))], I),
+            "mox_table_free": ([P(_Table)], None),
+            "mox_run_device": ([VP, VP, sz], I),
+            "mox_run_range": ([VP, VP, sz, sz, sz, I], I),
+            "mox_fetch_table": ([VP, P(P(_Table))], I),
+            "mox_get_stats": ([VP, P(Stats)], I),
+            "mox_device_alloc": ([VP, sz, P(VP)], I),
+            "mox_device_free": ([VP, VP], I),
+            "mox_memcpy_h2d": ([VP, VP, VP, sz], I),
+            "mox_memcpy_d2h": ([VP, VP, VP, sz], I),
+            "mox_synchronize": ([VP], I),
+            "mox_comm_unique_id": ([ctypes.c_char_p], I),
+            "mox_comm_init": ([VP, I, I, ctypes.c_char_p], I),
+            "mox_exchange": ([VP], I),
+            "mox_write_final_result": ([P(_Table), ctypes.c_char_p], I),
+            "mox_print_top_words": ([P(_Table), sz], I),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != MOX_OK:
+        msg = lib().mox_last_error().decode("utf-8", "replace")
+        if rc == MOX_EUTF8:
+            raise Utf8Error(rc, msg)
+        raise MoxError(rc, msg)
+
+
+class Table:
+    """Owning wrapper of a mox_table (words are bytes, counts are ints)."""
+
+    def __init__(self, ptr):
+        self._p = ptr
+        t = ptr.contents
+        self.n = int(t.n)
+        self.tokens = int(t.tokens)
+
+    def _raw(self):
+        import numpy as np
+
+        t = self._p.contents
+        n = self.n
+        counts = np.ctypeslib.as_array(t.counts, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
+        offs = np.ctypeslib.as_array(t.offs, shape=(n + 1,)).copy()
+        nb = int(offs[-1]) if n else 0
+        data = ctypes.string_at(t.bytes, nb) if nb else b""
+        return counts, offs, data
+
+    def arrays(self):
+        """(counts uint64[n], offs uint64[n+1], bytes) in table order."""
+        return self._raw()
+
+    def items(self):
+        counts, offs, data = self._raw()
+        for i in range(self.n):
+            yield data[offs[i]:offs[i + 1]], int(counts[i])
+
+    def as_dict(self):
+        return dict(self.items())
+
+    def sorted_items(self):
+        """Deterministic key sort (bytewise, Rust String Ord) used for parity."""
+        return sorted(self.items(), key=lambda kv: kv[0])
+
+    def write_final_result(self, path):
+        _check(lib().mox_write_final_result(self._p, path.encode()))
+
+    def close(self):
+        if self._p is not None:
+            lib().mox_table_free(self._p)
+            self._p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Engine:
+    def __init__(self, device=-1, flags=0, dict_words=0, sample_pieces=0, reserve_bytes=0):
+        cfg = Config()
+        cfg.device = device
+        cfg.flags = flags
+        cfg.dict_words = dict_words
+        cfg.sample_pieces = sample_pieces
+        cfg.reserve_bytes = reserve_bytes
+        h = ctypes.c_void_p()
+        _check(lib().mox_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+
+    # -- drop-in for main.rs:16-22
+    def count(self, data):
+        buf = bytes(data)
+        t = ctypes.POINTER(_Table)()
+        _check(lib().mox_count(self._h, buf, len(buf), ctypes.byref(t)))
+        return Table(t)
+
+    def count_file(self, path):
+        t = ctypes.POINTER(_Table)()
+        _check(lib().mox_count_file(self._h, os.fsencode(path), ctypes.byref(t)))
+        return Table(t)
+
+    # -- device-resident path
+    def run_device(self, d_ptr, n):
+        _check(lib().mox_run_device(self._h, ctypes.c_void_p(d_ptr), n))
+
+    def run_range(self, d_ptr, buf_len, own_begin, own_end, at_end):
+        _check(lib().mox_run_range(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
+
+    def fetch(self):
+        t = ctypes.POINTER(_Table)()
+        _check(lib().mox_fetch_table(self._h, ctypes.byref(t)))
+        return Table(t)
+
+    def stats(self):
+        s = Stats()
+        _check(lib().mox_get_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def alloc(self, nbytes):
+        p = ctypes.c_void_p()
+        _check(lib().mox_device_alloc(self._h, nbytes, ctypes.byref(p)))
+        return p.value
+
+    def free(self, d_ptr):
+        _check(lib().mox_device_free(self._h, ctypes.c_void_p(d_ptr)))
+
+    def h2d(self, d_ptr, host_buf, nbytes=None):
+        if nbytes is None:
+            nbytes = len(host_buf)
+        src = ctypes.c_char_p(host_buf) if isinstance(host_buf, bytes) else host_buf
+        if hasattr(host_buf, "ctypes"):
+            src = ctypes.c_void_p(host_buf.ctypes.data)
+        _check(lib().mox_memcpy_h2d(self._h, ctypes.c_void_p(d_ptr), src, nbytes))
+
+    def synchronize(self):
+        _check(lib().mox_synchronize(self._h))
+
+    # -- multi-GPU
+    def comm_init(self, nranks, rank, uid):
+        _check(lib().mox_comm_init(self._h, nranks, rank, uid))
+
+    def exchange(self):
+        _check(lib().mox_exchange(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().mox_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(UNIQUE_ID_BYTES)
+    _check(lib().mox_comm_unique_id(buf))
+    return buf.raw
+
+
+def count_words(data, **kw):
+    """One-shot: bytes -> {word(bytes): count} on the GPU."""
+    e = Engine(**kw)
+    try:
+        t = e.count(data)
+        try:
+            return t.as_dict()
+        finally:
+            t.close()
+    finally:
+        e.close()

@@ -1,0 +1,103 @@
+"""ORACLE -- test infrastructure only: ctypes binding of oracle/build/libmox_oracle.so
+(the C restatement, oracle/mox_oracle.c).  PARITY UNPINNED (see mox_oracle.c)."""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "build", "libmox_oracle.so")
+MEDUCE_REF = os.path.join(_HERE, "build", "meduce_ref")
+EUTF8 = -2
+
+
+class _T(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("tokens", ctypes.c_uint64),
+                ("counts", ctypes.POINTER(ctypes.c_uint64)), ("offs", ctypes.POINTER(ctypes.c_uint64)),
+                ("bytes", ctypes.POINTER(ctypes.c_uint8)), ("bytes_len", ctypes.c_uint64),
+                ("invalid_at", ctypes.c_int64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        L = ctypes.CDLL(LIB)
+        L.moxo_count.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(_T)]
+        L.moxo_count.restype = ctypes.c_int
+        L.moxo_free.argtypes = [ctypes.POINTER(_T)]
+        L.moxo_count_range.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                       ctypes.POINTER(_T)]
+        L.moxo_count_range.restype = ctypes.c_int
+        L.moxo_utf8_invalid_at.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
+        L.moxo_utf8_invalid_at.restype = ctypes.c_int64
+        _lib = L
+    return _lib
+
+
+class InvalidUtf8(ValueError):
+    pass
+
+
+def count(data, nthreads=8):
+    """Returns (sorted [(word bytes, count)], total tokens); raises InvalidUtf8."""
+    import numpy as np
+    if isinstance(data, np.ndarray):
+        ptr, n = data.ctypes.data, data.nbytes
+        keep = data
+    else:
+        keep = bytes(data)
+        ptr, n = ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p).value, len(keep)
+    t = _T()
+    rc = lib().moxo_count(ptr, n, nthreads, ctypes.byref(t))
+    del keep
+    if rc == EUTF8:
+        raise InvalidUtf8(t.invalid_at)
+    try:
+        nn = t.n
+        if nn == 0:
+            return [], int(t.tokens)
+        counts = np.ctypeslib.as_array(t.counts, shape=(nn,)).copy()
+        offs = np.ctypeslib.as_array(t.offs, shape=(nn + 1,)).copy()
+        raw = ctypes.string_at(t.bytes, int(offs[-1]))
+        return [(raw[offs[i]:offs[i + 1]], int(counts[i])) for i in range(nn)], int(t.tokens)
+    finally:
+        lib().moxo_free(ctypes.byref(t))
+
+
+def count_arrays(data, nthreads=8):
+    """Like count() but returns numpy arrays (counts, offs, bytes) -- for big inputs."""
+    import numpy as np
+    t = _T()
+    rc = lib().moxo_count(data.ctypes.data, data.nbytes, nthreads, ctypes.byref(t))
+    if rc == EUTF8:
+        raise InvalidUtf8(t.invalid_at)
+    try:
+        nn = t.n
+        counts = np.ctypeslib.as_array(t.counts, shape=(nn,)).copy() if nn else np.zeros(0, np.uint64)
+        offs = np.ctypeslib.as_array(t.offs, shape=(nn + 1,)).copy()
+        raw = ctypes.string_at(t.bytes, int(offs[-1])) if nn else b""
+        return counts, offs, raw, int(t.tokens)
+    finally:
+        lib().moxo_free(ctypes.byref(t))
+
+
+def count_range(data, own_begin, own_end):
+    """Tokens whose first byte lies in [own_begin, own_end) (shard ownership rule)."""
+    keep = bytes(data)
+    ptr = ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p).value
+    t = _T()
+    rc = lib().moxo_count_range(ptr, len(keep), own_begin, own_end, ctypes.byref(t))
+    if rc == EUTF8:
+        raise InvalidUtf8(t.invalid_at)
+    try:
+        import numpy as np
+        nn = t.n
+        if nn == 0:
+            return [], int(t.tokens)
+        counts = np.ctypeslib.as_array(t.counts, shape=(nn,)).copy()
+        offs = np.ctypeslib.as_array(t.offs, shape=(nn + 1,)).copy()
+        raw = ctypes.string_at(t.bytes, int(offs[-1]))
+        return [(raw[offs[i]:offs[i + 1]], int(counts[i])) for i in range(nn)], int(t.tokens)
+    finally:
+        lib().moxo_free(ctypes.byref(t))

@@ -1,0 +1,230 @@
+"""GPU parity: the HIP path (through the C ABI) vs the oracle, bit-exact.
+
+Word counts are integers, so the bar is exact equality of the (word, count)
+multiset after a deterministic bytewise key sort.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import coracle
+import mox
+from mox import corpus
+from conftest import kat_expected
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def eng():
+    e = mox.Engine(flags=mox.MOX_F_TIMING)
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def eng_nodict():
+    e = mox.Engine(flags=mox.MOX_F_NO_DICT)
+    yield e
+    e.close()
+
+
+def gpu_items(e, data):
+    try:
+        t = e.count(data)
+    except mox.Utf8Error:
+        return "error"
+    try:
+        items = t.sorted_items()
+        assert sum(c for _, c in items) == t.tokens
+        return items
+    finally:
+        t.close()
+
+
+def oracle_items(data):
+    try:
+        return coracle.count(data)[0]
+    except coracle.InvalidUtf8:
+        return "error"
+
+
+def test_kats(eng, kat_cases):
+    for case in kat_cases:
+        data = bytes.fromhex(case["input_hex"])
+        assert gpu_items(eng, data) == kat_expected(case), case["name"]
+
+
+def test_kats_without_dictionary(eng_nodict, kat_cases):
+    for case in kat_cases:
+        data = bytes.fromhex(case["input_hex"])
+        assert gpu_items(eng_nodict, data) == kat_expected(case), case["name"]
+
+
+ALPH = [b"a", b"B", b"z", b"Q", b"the", b"THE", b" ", b"\t", b"\n", b"\r\n", b"\x0b", b"\x0c", b"\x1c", b"\x00",
+        b",", " ".encode(), "　".encode(), " ".encode(), "\u0085".encode(), "​".encode(),
+        "Σ".encode(), "σ".encode(), "İ".encode(), "K".encode(), "é".encode(),
+        "É".encode(), "́".encode(), "'".encode(), "­".encode(), "日".encode(),
+        "\U0001F600".encode(), "Ǆ".encode(), "ß".encode()]
+
+
+def rand_text(rng, n):
+    return b"".join(rng.choice(ALPH) for _ in range(n))
+
+
+def test_fuzz_small(eng):
+    rng = random.Random(2024)
+    for i in range(300):
+        data = rand_text(rng, rng.randint(0, 80))
+        if i % 13 == 0 and data:
+            k = rng.randrange(len(data))
+            data = data[:k] + bytes([rng.choice([0x80, 0xC3, 0xE2, 0xF5, 0xFF])]) + data[k:]
+        assert gpu_items(eng, data) == oracle_items(data), data
+
+
+def test_tile_boundaries(eng):
+    """Tokens, multi-byte whitespace and UTF-8 sequences straddling 16 B lanes and 16 KiB tiles."""
+    rng = random.Random(77)
+    tile = 16 * 1024
+    for _ in range(40):
+        n = rng.randint(tile - 64, 3 * tile + 64)
+        buf = bytearray(rng.choice(b"abcdefghABCDEF  \n") for _ in range(n))
+        for _ in range(30):  # plant tricky items at lane / tile edges
+            edge = rng.choice([tile, 2 * tile, 16 * rng.randint(1, n // 16 - 1)]) + rng.randint(-3, 2)
+            item = rng.choice([b"W" * rng.randint(15, 40), "　".encode(), " ".encode(),
+                               "ΣΣ".encode(), "xİy".encode(), b"\x00\x00", b"Q" * 16, b"q" * 17])
+            if 0 <= edge and edge + len(item) <= n:
+                buf[edge:edge + len(item)] = item
+        data = bytes(buf)
+        try:
+            data.decode("utf-8")
+        except UnicodeDecodeError:
+            continue
+        assert gpu_items(eng, data) == oracle_items(data)
+
+
+def test_huge_single_token(eng):
+    data = b"x" * (3 << 20) + b" tail " + b"Y" * (1 << 20)
+    assert gpu_items(eng, data) == oracle_items(data)
+
+
+@pytest.mark.parametrize("kind", ["zipf", "hicard", "skew", "unicode"])
+def test_corpora_exact(eng, kind):
+    k = corpus.KINDS[kind]
+    data = corpus.fill(k, 0x1234 + k, 0, 24 << 20)
+    t = eng.count(data.tobytes())
+    got = t.sorted_items()
+    tokens = t.tokens
+    t.close()
+    want, wtok = coracle.count(data, nthreads=16)
+    assert tokens == wtok
+    assert got == want
+
+
+def test_misaligned_and_ranges(eng):
+    """run_range on a misaligned device pointer and a sub-range equals the oracle's range rule."""
+    data = corpus.fill(corpus.UNICODE, 5, 0, 3 << 20).tobytes()
+    d = eng.alloc(len(data) + 64)
+    try:
+        for mis in (0, 1, 7, 13):
+            eng.h2d(d + mis, data)
+            for a, b in [(0, len(data)), (4, len(data) - 1000), (123457, 2 * 1024 * 1024 + 5)]:
+                eng.run_range(d + mis, len(data), a, b, True)
+                t = eng.fetch()
+                got = t.sorted_items()
+                t.close()
+                want = coracle.count_range(data, a, b)[0]
+                assert got == want, (mis, a, b)
+    finally:
+        eng.free(d)
+
+
+def test_shards_merge_to_whole(eng):
+    """Byte-range shards with word-boundary fixup sum to the global count."""
+    data = corpus.fill(corpus.ZIPF, 11, 0, 8 << 20).tobytes()
+    d = eng.alloc(len(data))
+    try:
+        eng.h2d(d, data)
+        cuts = [0, 1 << 20, (3 << 20) + 5, (5 << 20) + 9, len(data)]
+        merged = {}
+        for a, b in zip(cuts, cuts[1:]):
+            eng.run_range(d, len(data), a, b, True)
+            t = eng.fetch()
+            for w, c in t.items():
+                merged[w] = merged.get(w, 0) + c
+            t.close()
+        assert sorted(merged.items()) == coracle.count(data)[0]
+    finally:
+        eng.free(d)
+
+
+def test_dictionary_does_not_change_counts(eng, eng_nodict):
+    data = corpus.fill(corpus.SKEW, 3, 0, 8 << 20).tobytes()
+    assert gpu_items(eng, data) == gpu_items(eng_nodict, data)
+
+
+def test_order_is_deterministic(eng):
+    data = corpus.fill(corpus.ZIPF, 21, 0, 16 << 20).tobytes()
+    t1 = eng.count(data)
+    a = t1.arrays()
+    t1.close()
+    t2 = eng.count(data)
+    b = t2.arrays()
+    t2.close()
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+
+
+def test_invalid_utf8_in_big_corpus(eng):
+    data = bytearray(corpus.fill(corpus.ZIPF, 8, 0, 4 << 20).tobytes())
+    data[3_000_001] = 0xFF
+    with pytest.raises(mox.Utf8Error):
+        eng.count(bytes(data))
+    # the engine stays usable afterwards
+    assert gpu_items(eng, b"a b a") == [(b"a", 2), (b"b", 1)]
+
+
+def test_count_file_and_cli(tmp_path, eng):
+    import subprocess
+    import os
+    from conftest import ROOT
+    data = corpus.fill(corpus.ZIPF, 1, 0, 5 << 20).tobytes()  # C1 stand-in for shakes.txt
+    (tmp_path / "shakes.txt").write_bytes(data)
+    t = eng.count_file(str(tmp_path / "shakes.txt"))
+    assert t.sorted_items() == coracle.count(data)[0]
+    t.close()
+    cli = os.path.join(ROOT, "map-oxidize_amd", "mox", "meduce-gpu")
+    r = subprocess.run([cli], cwd=tmp_path, capture_output=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.decode().splitlines()
+    assert lines[0] == "Top 10 words:" and len(lines) == 11
+    final = {}
+    for line in (tmp_path / "final_result.txt").read_bytes().split(b"\n"):
+        if line:
+            w, c = line.rsplit(b" ", 1)
+            final[w] = int(c)
+    assert sorted(final.items()) == coracle.count(data)[0]
+
+
+@pytest.mark.slow
+def test_full_size_c2(eng):
+    """BASELINE config C2 (1 GiB Zipf) exact against the oracle, plus size-independent checks."""
+    cfg = corpus.CONFIGS["C2"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
+    d = eng.alloc(data.nbytes)
+    try:
+        eng.h2d(d, data)
+        eng.run_device(d, data.nbytes)
+        t = eng.fetch()
+        counts, offs, raw = t.arrays()
+        tokens = t.tokens
+        t.close()
+    finally:
+        eng.free(d)
+    assert int(counts.sum()) == tokens
+    wc, wo, wraw, wtok = coracle.count_arrays(data, nthreads=16)
+    assert tokens == wtok and counts.size == wc.size
+    # sort the GPU table bytewise and compare arrays
+    words = [raw[offs[i]:offs[i + 1]] for i in range(counts.size)]
+    order = sorted(range(counts.size), key=words.__getitem__)
+    assert all(words[j] == wraw[wo[i]:wo[i + 1]] and counts[j] == wc[i] for i, j in enumerate(order))
