@@ -143,7 +143,10 @@ __device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint
     LSlot* s = &w.ltab[slot];
     unsigned long long cur = atomicCAS(&s->h, 0ull, (unsigned long long)h);
     if (cur == 0) {
+      // publish len before ref: memory-side atomics to different words complete
+      // in any order, so the fence (s_waitcnt vmcnt(0)) orders them
       atomicExch(&s->len, (unsigned long long)len);
+      __threadfence();
       atomicExch(&s->ref, (unsigned long long)(ref + 1));
       atomicAdd(&s->count, (unsigned long long)cnt);
       atomicAdd(&w.ctl->long_uniq, 1ull);
