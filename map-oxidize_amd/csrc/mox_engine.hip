@@ -127,16 +127,18 @@ void dfree(void* p) {
 
 // (Re)allocate every size-dependent buffer for the given capacities.
 struct Caps {
-  uint64_t pool_cap, w_cap, u_cap, arena_cap, long_cap, table_cap, bytes_cap;
+  uint64_t cold_cap, spill_cap, w_cap, u_cap, arena_cap, long_cap, table_cap, bytes_cap;
 };
 
 Caps caps_of(const Work& w) {
-  return Caps{w.pool_cap, w.w_cap, w.u_cap, w.arena_cap, w.long_cap, w.table_cap, w.bytes_cap};
+  return Caps{w.cold_cap, w.spill_cap, w.w_cap, w.u_cap, w.arena_cap, w.long_cap, w.table_cap, w.bytes_cap};
 }
 
 Caps initial_caps(uint64_t n, int map_grid) {
   Caps c;
-  c.pool_cap = std::max<uint64_t>(4096, n / ((uint64_t)CHUNK_RECS * 16) + (uint64_t)map_grid * NB * 2);
+  // cold records per (workgroup, partition) region: about one per 8 input bytes
+  c.cold_cap = std::max<uint64_t>(64, n / ((uint64_t)map_grid * NB * 8));
+  c.spill_cap = std::max<uint64_t>(1024, n / ((uint64_t)map_grid * 64));
   c.w_cap = 65536 + n / 64;
   c.u_cap = 4096 + n / 64;
   c.arena_cap = 65536 + n / 16;
@@ -154,25 +156,24 @@ Caps initial_caps(uint64_t n, int map_grid) {
 
 int realloc_sized(mox_engine* e, const Caps& c) {
   (void)hipDeviceSynchronize();
-  FREE_FIELD(pool); FREE_FIELD(chunk_bucket); FREE_FIELD(chunk_fill); FREE_FIELD(dir);
+  FREE_FIELD(cold); FREE_FIELD(spill);
   FREE_FIELD(w); FREE_FIELD(w_sorted); FREE_FIELD(u); FREE_FIELD(arena); FREE_FIELD(ltab); FREE_FIELD(lpos);
   FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
   dfree(e->d_lens);
   e->d_lens = nullptr;
   Work& w = e->w;
-  w.pool_cap = c.pool_cap;
+  w.cold_cap = (uint32_t)std::min<uint64_t>(c.cold_cap, 0xFFFFFFF0u);
+  w.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
   w.w_cap = c.w_cap;
   w.u_cap = c.u_cap;
   w.arena_cap = c.arena_cap;
   w.long_cap = next_pow2(c.long_cap);
-  w.uniq_cap = c.pool_cap * CHUNK_RECS + c.w_cap;
+  w.uniq_cap = (uint64_t)w.map_grid * NB * w.cold_cap + c.w_cap;
   w.table_cap = c.table_cap;
   w.bytes_cap = c.bytes_cap;
   int rc;
-  if ((rc = dalloc(e, (void**)&w.pool, w.pool_cap * CHUNK_RECS * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.chunk_bucket, w.pool_cap * 4))) return rc;
-  if ((rc = dalloc(e, (void**)&w.chunk_fill, w.pool_cap * 4))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dir, w.pool_cap * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.cold, (uint64_t)w.map_grid * NB * w.cold_cap * 16))) return rc;
+  if ((rc = dalloc(e, (void**)&w.spill, (uint64_t)w.map_grid * w.spill_cap * 16))) return rc;
   if ((rc = dalloc(e, (void**)&w.w, w.w_cap * sizeof(WRec)))) return rc;
   if ((rc = dalloc(e, (void**)&w.w_sorted, w.w_cap * sizeof(WRec)))) return rc;
   if ((rc = dalloc(e, (void**)&w.u, w.u_cap * sizeof(URec)))) return rc;
@@ -190,20 +191,20 @@ int realloc_sized(mox_engine* e, const Caps& c) {
 }
 
 bool caps_cover(const Caps& have, const Caps& need) {
-  return have.pool_cap >= need.pool_cap && have.w_cap >= need.w_cap && have.u_cap >= need.u_cap &&
+  return have.cold_cap >= need.cold_cap && have.spill_cap >= need.spill_cap && have.w_cap >= need.w_cap && have.u_cap >= need.u_cap &&
          have.arena_cap >= need.arena_cap && have.long_cap >= need.long_cap && have.table_cap >= need.table_cap &&
          have.bytes_cap >= need.bytes_cap;
 }
 
 Caps caps_max(const Caps& a, const Caps& b) {
-  return Caps{std::max(a.pool_cap, b.pool_cap), std::max(a.w_cap, b.w_cap), std::max(a.u_cap, b.u_cap),
+  return Caps{std::max(a.cold_cap, b.cold_cap), std::max(a.spill_cap, b.spill_cap), std::max(a.w_cap, b.w_cap), std::max(a.u_cap, b.u_cap),
               std::max(a.arena_cap, b.arena_cap), std::max(a.long_cap, b.long_cap),
               std::max(a.table_cap, b.table_cap), std::max(a.bytes_cap, b.bytes_cap)};
 }
 
 int ensure_caps(mox_engine* e, const Caps& need) {
-  if (e->w.pool && caps_cover(caps_of(e->w), need)) return MOX_OK;
-  Caps c = e->w.pool ? caps_max(caps_of(e->w), need) : need;
+  if (e->w.cold && caps_cover(caps_of(e->w), need)) return MOX_OK;
+  Caps c = e->w.cold ? caps_max(caps_of(e->w), need) : need;
   return realloc_sized(e, c);
 }
 
@@ -211,19 +212,20 @@ int alloc_fixed(mox_engine* e) {
   Work& w = e->w;
   int rc;
   if ((rc = dalloc(e, (void**)&w.ctl, sizeof(Ctl)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.cand_key, CAND_SLOTS * 8 * 2))) return rc;
-  w.cand_cnt = w.cand_key + CAND_SLOTS;
-  if ((rc = dalloc(e, (void**)&w.dict_img, DICT_SLOTS * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.cand_key, CAND_SLOTS * 8 * 3))) return rc;
+  w.cand_cnt = w.cand_key + 2 * CAND_SLOTS;
+  if ((rc = dalloc(e, (void**)&w.dict_img, DICT_SLOTS * 16))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_cnt, (size_t)e->n_cu * DICT_SLOTS * 4))) return rc;
+  w.map_grid = (uint32_t)std::min(e->n_cu, MAX_MAP_GRID);
+  if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.spill_n, (size_t)w.map_grid * 4))) return rc;
   // bucket directory block: one allocation, zeroed per run
-  size_t dir_bytes = NB * 4 + NB * 8 + NB * 4 + 2 * NB * 4 + 3 * (NB + 1) * 8 + NB * 8 + (NB + 1) * 8;
+  size_t dir_bytes = NB * 8 + NB * 4 + NB * 4 + 2 * (NB + 1) * 8 + NB * 8 + (NB + 1) * 8;
   uint8_t* d;
   if ((rc = dalloc(e, (void**)&d, dir_bytes))) return rc;
-  w.b_chunks = (uint32_t*)d; d += NB * 4;
   w.b_recs = (uint64_t*)d; d += NB * 8;
   w.b_w = (uint32_t*)d; d += NB * 4;
-  w.b_cur = (uint32_t*)d; d += 2 * NB * 4;
-  w.dir_off = (uint64_t*)d; d += (NB + 1) * 8;
+  w.b_cur = (uint32_t*)d; d += NB * 4;
   w.w_off = (uint64_t*)d; d += (NB + 1) * 8;
   w.rec_off = (uint64_t*)d; d += (NB + 1) * 8;
   w.b_uniq = (uint64_t*)d; d += NB * 8;
@@ -248,14 +250,12 @@ int alloc_fixed(mox_engine* e) {
   memset(e->h_ctl_init, 0, sizeof(Ctl));
   e->h_ctl_init->err_utf8 = ~0ull;
   e->h_ctl_init->halo_err = ~0ull;
-  HIPCHK(hipMemset(w.dict_img, 0, DICT_SLOTS * 8));
+  HIPCHK(hipMemset(w.dict_img, 0, DICT_SLOTS * 16));
   return MOX_OK;
 }
 
-size_t map_lds_bytes() {
-  return (16 + TILE + 32 + 16) + (MAP_THREADS + 4) * 4 + DICT_SLOTS * 8 + DICT_SLOTS * 4 + NB * QDEPTH * 16 + 3 * NB * 4 + 64;
-}
-size_t reduce_lds_bytes() { return 4 * RT_SLOTS * 8 + RT_SLOTS * 2 + 64; }
+size_t map_lds_bytes() { return DICT_SLOTS * 16 + DICT_SLOTS * 4 + NB * 4 + 16; }
+size_t reduce_lds_bytes() { return 4608 * (8 * 3 + 4) + 4096 * 2 + (MAX_MAP_GRID + 4) * 4 + 32768 / 8 + 64; }
 
 // exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)
 int launch_scan(mox_engine* e, const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
@@ -285,20 +285,20 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   };
   rec(0);
   HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_init, sizeof(Ctl), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(w.b_chunks, 0, NB * 4 + NB * 8 + NB * 4, s));
+  HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
   HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
   // 1. hot dictionary from a sample
   if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
-    HIPCHK(hipMemsetAsync(w.cand_key, 0, CAND_SLOTS * 16, s));
+    HIPCHK(hipMemsetAsync(w.cand_key, 0, CAND_SLOTS * 24, s));
     hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
     hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
   }
   rec(1);
   // 2. map: one streaming pass over the corpus
-  uint64_t tile0 = c.own_lo & ~15ull;
-  uint64_t ntiles = c.own_hi > c.own_lo ? (c.own_hi - tile0 + TILE - 1) / TILE : 0;
-  int grid = e->n_cu;
-  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, ntiles);
+  const uint64_t row0 = c.own_lo & ~15ull;
+  const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + 1023) / 1024 : 0;
+  const int grid = (int)w.map_grid;
+  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows);
   rec(2);
   // 3. lanes
   hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
@@ -342,13 +342,21 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   for (int attempt = 0;; attempt++) {
     if ((rc = pipeline_once(e, c))) return rc;
     const Ctl& h = *e->h_ctl;
+    if (getenv("MOX_VERBOSE"))
+      fprintf(stderr, "[mox] attempt %d: overflow 0x%x cold_need %llu spill_need %llu w_total %llu u_n %llu n_total %llu caps cold %u spill %u w %llu run %.3f ms\n",
+              attempt, h.overflow, h.cold_need, h.spill_need, h.w_total, h.u_n, h.n_total, e->w.cold_cap, e->w.spill_cap,
+              (unsigned long long)e->w.w_cap, e->stats.ms_run);
     if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
     if (h.halo_err != ~0ull)
       return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
     if (!h.overflow) break;
     if (attempt >= 4) return fail(MOX_ENOMEM, "buffer growth did not converge (overflow mask 0x%x)", h.overflow);
     Caps need = caps_of(e->w);
-    if (h.overflow & OVF_POOL) need.pool_cap = h.pool_next + h.pool_next / 4 + 1024;
+    if (h.overflow & OVF_POOL) {
+      need.cold_cap = std::max<uint64_t>(need.cold_cap, h.cold_need + h.cold_need / 8 + 16);
+      need.spill_cap = std::max<uint64_t>(need.spill_cap, h.spill_need + h.spill_need / 4 + 1024);
+    }
+    if (h.overflow & OVF_W) need.w_cap = std::max<uint64_t>(need.w_cap, h.w_total + h.w_total / 4 + 1024);
     if (h.overflow & OVF_W) need.w_cap = h.w_n + h.w_n / 4 + 1024;
     if (h.overflow & OVF_U) need.u_cap = h.u_n + h.u_n / 4 + 1024;
     if (h.overflow & OVF_ARENA) need.arena_cap = h.arena_n + h.arena_n / 4 + 65536;
@@ -369,7 +377,7 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   e->stats.weighted_records = h.w_n;
   e->stats.unicode_tokens = h.u_n;
   e->stats.long_tokens = h.long_n;
-  e->stats.chunks = h.pool_next;
+  e->stats.chunks = h.cold_need;
   e->stats.max_subpasses = h.max_sub ? h.max_sub : 1;
   e->last_corpus = c;
   e->have_result = true;
@@ -437,6 +445,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     mox_engine_destroy(e);
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
+  if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
   int rc = alloc_fixed(e);
   if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));
   if (rc != MOX_OK) {
@@ -455,8 +464,8 @@ void mox_engine_destroy(mox_engine* e) {
   (void)hipDeviceSynchronize();
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
-  void* ptrs[] = {w.ctl, w.cand_key, w.dict_img, w.dict_cnt, w.b_chunks, w.scan_part, (void*)e->tables.lower_src,
-                  w.pool, w.chunk_bucket, w.chunk_fill, w.dir, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
+  void* ptrs[] = {w.ctl, w.cand_key, w.dict_img, w.dict_cnt, w.cold_n, w.spill_n, w.b_recs, w.scan_part, (void*)e->tables.lower_src,
+                  w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_lens, e->d_text};
   for (void* p : ptrs) dfree(p);
   if (e->h_ctl) (void)hipHostFree(e->h_ctl);

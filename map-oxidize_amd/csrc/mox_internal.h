@@ -8,29 +8,23 @@ namespace mox {
 
 // ---- geometry ----
 constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
-constexpr int TILE = MAP_THREADS * 16;      // 16 KiB: one 16-byte segment per lane
-constexpr int PREFETCH = 3;                 // tiles in flight per workgroup (registers)
+constexpr int MAX_MAP_GRID = 1024;          // map workgroups (one per CU)
 constexpr int NB_LOG2 = 8;                  // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
-constexpr int QDEPTH = 16;                  // per-partition LDS staging queue (records)
-constexpr int FLUSH = 8;                    // records per flush = 128 B, one full line
-constexpr int CHUNK_RECS = 256;             // records per pool chunk (4 KiB)
-constexpr int DICT_SLOTS = 4096;            // LDS hot-dictionary hash slots (8-byte keys)
+constexpr int DICT_SLOTS = 4096;            // LDS hot-dictionary hash slots (16-byte keys)
 constexpr int DICT_MAX_WORDS = 3072;
 constexpr int CAND_SLOTS = 1 << 14;         // dictionary candidate table (global)
 constexpr int SAMPLE_PIECE = 64 * 1024;
-constexpr int SAMPLE_SLOTS = 8192;
-constexpr int RT_SLOTS = 4096;              // bucket-reduce LDS hash slots
-constexpr int RT_CAP = 3072;                // max uniques per reduce sub-pass
+constexpr int SAMPLE_SLOTS = 4096;
 constexpr int RED_THREADS = 1024;
 constexpr int SCAN_THREADS = 1024;
-constexpr int SCAN_TILE = SCAN_THREADS * 4;
 constexpr int SCAN_WGS = 1024;
 
 constexpr uint64_t LONG_TAG = 0xFF00000000000000ull;   // w1 marker of a hashed (long) key
 constexpr uint64_t LONG_LEN_MASK = 0x0000FFFFFFFFFFFFull;
 constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points into the arena
 
+enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u };
 enum : uint32_t {
   OVF_POOL = 1u, OVF_W = 2u, OVF_U = 4u, OVF_LONG = 8u, OVF_ARENA = 16u, OVF_PROBE = 32u,
   OVF_TABLE = 64u, OVF_BYTES = 128u
@@ -38,7 +32,6 @@ enum : uint32_t {
 
 // Control block: counters written by the kernels, read back once per run.
 struct Ctl {
-  unsigned long long pool_next;   // cold chunks requested
   unsigned long long w_n;         // weighted records requested
   unsigned long long u_n;         // unicode tokens requested
   unsigned long long arena_n;     // arena bytes requested
@@ -57,6 +50,9 @@ struct Ctl {
   unsigned int max_sub;
   unsigned int dict_thresh;
   unsigned int pad[3];
+  unsigned long long cold_need;   // max records any (workgroup, partition) region asked for
+  unsigned long long spill_need;  // max spill records of any map workgroup
+  unsigned long long w_total;     // weighted + spilled records
 };
 
 // Weighted record: a key with a count (dictionary totals, spills, Unicode-lane
@@ -98,15 +94,18 @@ struct Corpus {
 struct Work {  // device buffers of one engine
   Ctl* ctl;
   // dictionary
-  unsigned long long* cand_key;   // CAND_SLOTS
+  unsigned long long* cand_key;   // 2 * CAND_SLOTS (w0, w1 | 1<<63)
   unsigned long long* cand_cnt;   // CAND_SLOTS
-  unsigned long long* dict_img;   // DICT_SLOTS
+  uint4* dict_img;                // DICT_SLOTS 16-byte keys
   uint32_t* dict_cnt;             // [map_grid][DICT_SLOTS]
-  // cold pool
-  uint4* pool;                    // pool_cap * CHUNK_RECS records of 16 B
-  uint32_t* chunk_bucket;         // pool_cap
-  uint32_t* chunk_fill;           // pool_cap
-  uint64_t pool_cap;
+  // cold records: region (map workgroup g, partition b) = cold[(g*NB + b)*cold_cap ...]
+  uint4* cold;                    // map_grid * NB * cold_cap records of 16 B
+  uint32_t* cold_n;               // map_grid * NB records written per region
+  uint32_t cold_cap;
+  uint32_t map_grid;
+  uint4* spill;                   // map_grid * spill_cap records (regions that overflowed)
+  uint32_t* spill_n;              // map_grid
+  uint32_t spill_cap;
   // weighted records
   WRec* w;                        // w_cap
   WRec* w_sorted;                 // w_cap
@@ -119,17 +118,14 @@ struct Work {  // device buffers of one engine
   // long lane
   LSlot* ltab;                    // long_cap (power of two)
   uint64_t long_cap;
-  // bucket directory (NB + 1 each)
-  uint32_t* b_chunks;             // chunk count per bucket
-  uint64_t* b_recs;               // cold records per bucket
-  uint32_t* b_w;                  // weighted records per bucket
-  uint32_t* b_cur;                // scatter cursors (2 * NB)
-  uint64_t* dir_off;              // NB + 1 (chunk index offsets)
+  // partition directory
+  uint64_t* b_recs;               // NB cold records per partition
+  uint32_t* b_w;                  // NB weighted records per partition
+  uint32_t* b_cur;                // NB scatter cursors
   uint64_t* w_off;                // NB + 1
   uint64_t* rec_off;              // NB + 1 (output region offsets)
   uint64_t* b_uniq;               // NB
   uint64_t* uniq_off;             // NB + 1
-  uint32_t* dir;                  // pool_cap chunk ids grouped by bucket
   // reduce output (capacity = records)
   uint4* uk;                      // keys
   uint64_t* uc;                   // counts
@@ -143,6 +139,7 @@ struct Work {  // device buffers of one engine
   uint64_t table_cap, bytes_cap;
   // scan scratch
   uint64_t* scan_part;            // SCAN_WGS + 1
+  uint32_t dbg;                   // ablation switches (MOX_DBG env), 0 in production
 };
 
 }  // namespace mox

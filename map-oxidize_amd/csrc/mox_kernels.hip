@@ -24,15 +24,6 @@
 namespace mox {
 
 // ------------------------------------------------------------------ helpers
-__device__ __forceinline__ uint64_t mix_hash(uint64_t w0, uint64_t w1) {
-  uint64_t h = (w0 ^ 0x9E3779B97F4A7C15ull) * 0xBF58476D1CE4E5B9ull;
-  h ^= (w1 + 0x94D049BB133111EBull) * 0xD6E8FEB86659FD93ull;
-  h ^= h >> 32;
-  h *= 0x9E3779B97F4A7C15ull;
-  h ^= h >> 29;
-  return h;
-}
-
 // per-byte masks, valid only when every byte < 0x80 (ASCII fast path)
 __device__ __forceinline__ uint32_t movemask8(uint64_t m80) {  // m80: 0x80 per selected byte
   return (uint32_t)((((m80 >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
@@ -168,16 +159,25 @@ __device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint
 }
 
 // ------------------------------------------------------------------ map kernel
+// 32-bit key hash for short (<= 16 byte) keys: bucket = top 8 bits, LDS slots
+// use the low bits.  Final table order is (h32, key), so it is deterministic.
+__device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
+  uint32_t h = (uint32_t)w0 * 0x9E3779B1u + (uint32_t)(w0 >> 32) * 0x85EBCA77u + (uint32_t)w1 * 0xC2B2AE3Du +
+               (uint32_t)(w1 >> 32) * 0x27D4EB2Fu;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h;
+}
+__device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - NB_LOG2); }
+
 struct MapLds {
-  uint8_t* tile;                 // 16 pre + TILE + 32 post
-  uint32_t* masks;               // MAP_THREADS + 1: ws16 | zero16 << 16
-  unsigned long long* dkey;      // DICT_SLOTS
-  uint32_t* dcnt;                // DICT_SLOTS
-  uint4* q;                      // NB * QDEPTH
-  uint32_t* qcnt;                // NB
-  uint32_t* ccur;                // NB current chunk (0xFFFFFFFF none)
-  uint32_t* cfill;               // NB
-  uint32_t* flags;               // [0] nonascii, [1] dict_n, [2] maxprobe
+  uint4* dkey;      // DICT_SLOTS 16-byte keys (0 = empty)
+  uint32_t* dcnt;   // DICT_SLOTS
+  uint32_t* bcnt;   // NB: cold records this workgroup wrote per partition
+  uint32_t* misc;   // [0] spills
 };
 
 struct MapCtx {
@@ -187,32 +187,42 @@ struct MapCtx {
   uint32_t dict_n, maxprobe;
 };
 
-__device__ __forceinline__ void spill_weighted(const MapCtx& m, uint64_t w0, uint64_t w1, uint64_t cnt) {
-  unsigned long long i = atomicAdd(&m.w.ctl->w_n, 1ull);
-  if (i < m.w.w_cap) m.w.w[i] = WRec{w0, w1, cnt};
-  else atomicOr(&m.w.ctl->overflow, OVF_W);
-}
-
 // A short word (lowered length <= 16, no NUL byte): exact 16-byte key.
+// Hot words: LDS dictionary count.  Others: appended to this workgroup's
+// region of the word's partition (the shuffle write), no global atomics.
 __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_t w1) {
-  uint64_t h = mix_hash(w0, w1);
-  if (w1 == 0 && m.dict_n) {
-    uint32_t slot = (uint32_t)h & (DICT_SLOTS - 1);
+  const uint32_t h = key_hash(w0, w1);
+  if (m.w.dbg & DBG_NO_EMIT) { asm volatile("" ::"v"(h)); return; }
+  const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+  if (m.dict_n && !(m.w.dbg & DBG_NO_DICT)) {
+    uint32_t slot = h & (DICT_SLOTS - 1);
     for (uint32_t i = 0; i <= m.maxprobe; i++) {
-      unsigned long long k = m.s.dkey[slot];
-      if (k == w0) { atomicAdd(&m.s.dcnt[slot], 1u); return; }
-      if (k == 0) break;
+      const uint4 k = m.s.dkey[slot];
+      if (k.x == key.x && k.y == key.y && k.z == key.z && k.w == key.w) {
+        if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
+        return;
+      }
+      if ((k.x | k.y | k.z | k.w) == 0) break;
       slot = (slot + 1) & (DICT_SLOTS - 1);
     }
   }
-  uint32_t b = (uint32_t)(h >> (64 - NB_LOG2));
-  uint32_t pos = atomicAdd(&m.s.qcnt[b], 1u);
-  if (pos < QDEPTH) m.s.q[b * QDEPTH + pos] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-  else spill_weighted(m, w0, w1, 1);
+  const uint32_t b = bucket_of(h);
+  if (m.w.dbg & DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
+  const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
+  if (pos < m.w.cold_cap) {
+    m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
+    return;
+  }
+  const uint32_t sp = atomicAdd(&m.s.misc[0], 1u);
+  if (sp < m.w.spill_cap) {
+    m.w.spill[(uint64_t)blockIdx.x * m.w.spill_cap + sp] = key;
+    return;
+  }
+  atomicOr(&m.w.ctl->overflow, OVF_POOL);
 }
 
 // Any token, walked byte by byte from global memory (rare: long tokens, tokens
-// running past the 32-byte window, tiles with non-ASCII bytes).
+// running past the 32-byte window, rows with non-ASCII bytes).
 __device__ void generic_token(const MapCtx& m, uint64_t p) {
   const Corpus& c = m.c;
   uint64_t q = p;
@@ -222,7 +232,7 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
       if (!c.at_end) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - c.lo));
       break;
     }
-    uint8_t b = c.base[q];
+    const uint8_t b = c.base[q];
     if (b < 0x80) {
       if (is_ascii_ws(b)) break;
       nul |= (b == 0);
@@ -233,9 +243,9 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
       q++;
     }
   }
-  uint64_t len = q - p;
+  const uint64_t len = q - p;
   if (nonascii) {
-    unsigned long long i = atomicAdd(&m.w.ctl->u_n, 1ull);
+    const unsigned long long i = atomicAdd(&m.w.ctl->u_n, 1ull);
     if (i < m.w.u_cap) m.w.u[i] = URec{p, len};
     else atomicOr(&m.w.ctl->overflow, OVF_U);
     return;
@@ -243,7 +253,7 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
   if (len <= 16 && !nul) {
     uint64_t w0 = 0, w1 = 0;
     for (uint64_t i = 0; i < len; i++) {
-      uint64_t b = ascii_lower(c.base[p + i]);
+      const uint64_t b = ascii_lower(c.base[p + i]);
       if (i < 8) w0 |= b << (8 * i); else w1 |= b << (8 * (i - 8));
     }
     short_word(m, w0, w1);
@@ -255,119 +265,70 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
   long_insert(m.w, c.base, h, p, len, 1);
 }
 
-// 16 bytes at aligned internal position p; out-of-range bytes read as ' '.
-__device__ __forceinline__ uint4 load16(const Corpus& c, uint64_t p) {
-  if (p + 16 <= c.lo || p >= c.hi) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-  uint4 v = *reinterpret_cast<const uint4*>(c.base + p);
+// Clamped aligned 16-byte load: the block always overlaps [lo, hi), so it never
+// leaves the allocation; bytes out of range are fixed up by fix16.
+__device__ __forceinline__ uint4 raw16(const Corpus& c, uint64_t p) {
+  const uint64_t first = c.lo & ~15ull, last = (c.hi - 1) & ~15ull;
+  p = p < first ? first : (p > last ? last : p);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(c.base + p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 fix16(const Corpus& c, uint64_t p, uint4 v) {
   if (p >= c.lo && p + 16 <= c.hi) return v;
+  if (p + 16 <= c.lo || p >= c.hi) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
   uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int k = 0; k < 16; k++) {
-    uint64_t q = p + k;
+    const uint64_t q = p + k;
     if (q < c.lo || q >= c.hi) {
-      int wi = k >> 2, sh = (k & 3) * 8;
+      const int wi = k >> 2, sh = (k & 3) * 8;
       wv[wi] = (wv[wi] & ~(0xFFu << sh)) | (0x20u << sh);
     }
   }
   return make_uint4(wv[0], wv[1], wv[2], wv[3]);
 }
-
 __device__ __forceinline__ uint32_t nonascii16(uint4 v) { return (v.x | v.y | v.z | v.w) & 0x80808080u; }
-
-// Flush staged cold records: every partition with >= FLUSH records writes whole
-// 128-byte groups into its current chunk.  8 lanes per partition.
-__device__ void flush_queues(const MapCtx& m, bool final_flush) {
-  const int tid = threadIdx.x;
-  for (int base = 0; base < NB; base += MAP_THREADS / 8) {
-    int b = base + tid / 8, j = tid & 7;
-    uint32_t cnt = m.s.qcnt[b];
-    if (cnt > QDEPTH) cnt = QDEPTH;
-    uint32_t nflush = final_flush ? cnt : (cnt & ~(uint32_t)(FLUSH - 1));
-    // chunk bookkeeping by lane j == 0, broadcast through registers of the 8-lane group
-    uint32_t chunkA = 0xFFFFFFFFu, fillA = 0, chunkB = 0xFFFFFFFFu, split = nflush;
-    if (nflush) {
-      uint32_t cur = m.s.ccur[b], fill = m.s.cfill[b];
-      if (j == 0) {
-        if (cur == 0xFFFFFFFFu || fill >= CHUNK_RECS) {
-          if (cur != 0xFFFFFFFFu && cur < m.w.pool_cap) m.w.chunk_fill[cur] = fill;
-          unsigned long long c = atomicAdd(&m.w.ctl->pool_next, 1ull);
-          cur = (c < m.w.pool_cap) ? (uint32_t)c : 0xFFFFFFFEu;
-          if (c < m.w.pool_cap) m.w.chunk_bucket[c] = b; else atomicOr(&m.w.ctl->overflow, OVF_POOL);
-          fill = 0;
-        }
-        chunkA = cur; fillA = fill;
-        split = CHUNK_RECS - fill;
-        if (split < nflush) {
-          if (cur < m.w.pool_cap) m.w.chunk_fill[cur] = CHUNK_RECS;
-          unsigned long long c = atomicAdd(&m.w.ctl->pool_next, 1ull);
-          chunkB = (c < m.w.pool_cap) ? (uint32_t)c : 0xFFFFFFFEu;
-          if (c < m.w.pool_cap) m.w.chunk_bucket[c] = b; else atomicOr(&m.w.ctl->overflow, OVF_POOL);
-          m.s.ccur[b] = chunkB;
-          m.s.cfill[b] = nflush - split;
-        } else {
-          split = nflush;
-          m.s.ccur[b] = cur;
-          m.s.cfill[b] = fill + nflush;
-        }
-      }
-    }
-    // broadcast within the group of 8 lanes (same wave: lanes 8g..8g+7)
-    int leader = (threadIdx.x & 63) & ~7;
-    chunkA = __shfl(chunkA, leader);
-    fillA = __shfl(fillA, leader);
-    chunkB = __shfl(chunkB, leader);
-    split = __shfl(split, leader);
-    for (uint32_t r = j; r < nflush; r += 8) {
-      uint4 v = m.s.q[b * QDEPTH + r];
-      uint32_t ch = r < split ? chunkA : chunkB;
-      uint32_t pos = r < split ? fillA + r : r - split;
-      if (ch < m.w.pool_cap) m.w.pool[(uint64_t)ch * CHUNK_RECS + pos] = v;
-    }
-    // move the remainder (< FLUSH records) to the queue front
-    uint32_t rem = cnt - nflush;
-    uint4 keep = make_uint4(0, 0, 0, 0);
-    if ((uint32_t)j < rem) keep = m.s.q[b * QDEPTH + nflush + j];
-    __builtin_amdgcn_wave_barrier();
-    if ((uint32_t)j < rem) m.s.q[b * QDEPTH + j] = keep;
-    if (j == 0) m.s.qcnt[b] = rem;
-    if (final_flush && j == 0) {
-      uint32_t cur = m.s.ccur[b];
-      if (cur < m.w.pool_cap) m.w.chunk_fill[cur] = m.s.cfill[b];
-    }
-  }
+__device__ __forceinline__ uint32_t ws_mask16(uint4 v) {
+  const uint64_t l = ((uint64_t)v.y << 32) | v.x, h = ((uint64_t)v.w << 32) | v.z;
+  return movemask8(ws_bytes80(l)) | (movemask8(ws_bytes80(h)) << 8);
+}
+__device__ __forceinline__ uint32_t zero_mask16(uint4 v) {
+  const uint64_t l = ((uint64_t)v.y << 32) | v.x, h = ((uint64_t)v.w << 32) | v.z;
+  return movemask8(zero_bytes80(l)) | (movemask8(zero_bytes80(h)) << 8);
+}
+__device__ __forceinline__ uint4 shfl_down1(uint4 v) {
+  return make_uint4(__shfl_down(v.x, 1), __shfl_down(v.y, 1), __shfl_down(v.z, 1), __shfl_down(v.w, 1));
+}
+__device__ __forceinline__ uint4 lane0(uint4 v) {
+  return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                    __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
 
-// Fast path: the tile (plus 4 bytes before and 16 after) is pure ASCII.
-__device__ void tile_fast(const MapCtx& m, uint64_t tbase, unsigned long long& ntok) {
-  const int tid = threadIdx.x;
-  const uint8_t* lt = m.s.tile + 16 + tid * 16;
-  uint4 a = *reinterpret_cast<const uint4*>(lt);
-  uint4 bn = *reinterpret_cast<const uint4*>(lt + 16);
-  uint32_t mk = m.s.masks[tid], mn = m.s.masks[tid + 1];
-  uint32_t ws32 = (mk & 0xFFFFu) | (mn << 16);
-  uint32_t z32 = (mk >> 16) | (mn & 0xFFFF0000u);
-  uint8_t prev = lt[-1];
-  uint64_t p0 = tbase + (uint64_t)tid * 16;
-  uint32_t prevws = is_ascii_ws(prev) ? 1u : 0u;
-  if (p0 == m.c.lo && m.c.own_lo == m.c.lo) prevws = 1;  // corpus start
+// Fast path of one row (64 lanes x 16 B, all ASCII): per-lane token extraction
+// from a 32-byte window (own 16 B + the next lane's 16 B).
+__device__ __forceinline__ void row_fast(const MapCtx& m, uint64_t p0, uint4 a, uint4 bn, uint32_t prevws,
+                                         unsigned long long& ntok) {
+  const uint32_t ws32 = ws_mask16(a) | (ws_mask16(bn) << 16);
+  const uint32_t z32 = zero_mask16(a) | (zero_mask16(bn) << 16);
   uint32_t start = (~ws32) & ((ws32 << 1) | prevws) & 0xFFFFu;
-  // ownership window [own_lo, own_hi)
   if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
   if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
+  if (m.w.dbg & DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
   ntok += __popc(start);
   uint64_t W0 = ((uint64_t)a.y << 32) | a.x, W1 = ((uint64_t)a.w << 32) | a.z;
   uint64_t W2 = ((uint64_t)bn.y << 32) | bn.x, W3 = ((uint64_t)bn.w << 32) | bn.z;
   W0 = lower_ascii(W0); W1 = lower_ascii(W1); W2 = lower_ascii(W2); W3 = lower_ascii(W3);
   while (start) {
-    int p = __builtin_ctz(start);
+    const int p = __builtin_ctz(start);
     start &= start - 1;
-    uint32_t rest = ws32 >> p;
-    if (rest == 0) { generic_token(m, p0 + p); continue; }
-    int len = __builtin_ctz(rest);
-    if (p0 + p + len >= m.c.hi && !m.c.at_end) { generic_token(m, p0 + p); continue; }
-    if (len > 16 || ((z32 >> p) & ((len >= 32) ? ~0u : ((1u << len) - 1u)))) { generic_token(m, p0 + p); continue; }
-    int k = p >> 3, r = (p & 7) * 8;
-    uint64_t A = k ? W1 : W0, B = k ? W2 : W1, C = k ? W3 : W2;
+    const uint32_t rest = ws32 >> p;
+    const int len = rest ? __builtin_ctz(rest) : 32;
+    const bool odd = rest == 0 || len > 16 || (p0 + p + len >= m.c.hi && !m.c.at_end) ||
+                     ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
+    if (odd) { generic_token(m, p0 + p); continue; }
+    const int k = p >> 3, r = (p & 7) * 8;
+    const uint64_t A = k ? W1 : W0, B = k ? W2 : W1, C = k ? W3 : W2;
     uint64_t w0 = r ? (A >> r) | (B << (64 - r)) : A;
     uint64_t w1 = r ? (B >> r) | (C << (64 - r)) : B;
     if (len <= 8) { w0 &= lo_mask(len); w1 = 0; }
@@ -376,19 +337,17 @@ __device__ void tile_fast(const MapCtx& m, uint64_t tbase, unsigned long long& n
   }
 }
 
-// Slow path: validate UTF-8, find tokens with Unicode whitespace, walk each.
-__device__ void tile_slow(const MapCtx& m, uint64_t tbase, unsigned long long& ntok) {
-  const int tid = threadIdx.x;
-  uint64_t p0 = tbase + (uint64_t)tid * 16;
+// Slow path of one row: validate UTF-8, find tokens with Unicode whitespace.
+__device__ void row_slow(const MapCtx& m, uint64_t p0, unsigned long long& ntok) {
   for (int j = 0; j < 16; j++) {
-    uint64_t p = p0 + j;
+    const uint64_t p = p0 + j;
     if (p < m.c.own_lo || p >= m.c.own_hi) continue;
-    int v = utf8_check(m.c, p);
+    const int v = utf8_check(m.c, p);
     if (v == 1) atomicMin(&m.w.ctl->err_utf8, (unsigned long long)(p - m.c.lo));
     else if (v == 2) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - m.c.lo));
+    if (m.w.dbg & DBG_NO_TOKENS) continue;
     if (in_ws(m.c, p)) continue;
-    bool start = (p == m.c.lo && m.c.own_lo == m.c.lo) ? true : in_ws(m.c, p - 1);
-    // a continuation byte never starts a token (it follows its lead byte)
+    const bool start = (p == m.c.lo) ? true : in_ws(m.c, p - 1);
     if (start && (m.c.base[p] & 0xC0) != 0x80) {
       ntok++;
       generic_token(m, p);
@@ -396,163 +355,169 @@ __device__ void tile_slow(const MapCtx& m, uint64_t tbase, unsigned long long& n
   }
 }
 
-extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t ntiles) {
+// Every wave streams its own contiguous range of 1 KiB rows, ROWB rows per
+// batch (one wait per batch; 16 independent waves per CU keep ~64 KiB of loads
+// in flight).  No workgroup barrier inside the loop.
+constexpr int ROWB = 4;
+
+extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t nrows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   MapCtx m;
   m.c = c;
   m.w = w;
   uint8_t* sp = smem;
-  m.s.tile = sp; sp += 16 + TILE + 32 + 16;
-  m.s.masks = (uint32_t*)sp; sp += (MAP_THREADS + 4) * 4;
-  m.s.dkey = (unsigned long long*)sp; sp += DICT_SLOTS * 8;
+  m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
-  m.s.q = (uint4*)sp; sp += NB * QDEPTH * 16;
-  m.s.qcnt = (uint32_t*)sp; sp += NB * 4;
-  m.s.ccur = (uint32_t*)sp; sp += NB * 4;
-  m.s.cfill = (uint32_t*)sp; sp += NB * 4;
-  m.s.flags = (uint32_t*)sp; sp += 64;
-  const int tid = threadIdx.x;
-
+  m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
+  m.s.misc = (uint32_t*)sp; sp += 16;
+  const int tid = threadIdx.x, lane = tid & 63;
   for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) { m.s.dkey[i] = w.dict_img[i]; m.s.dcnt[i] = 0; }
-  for (int i = tid; i < NB; i += MAP_THREADS) { m.s.qcnt[i] = 0; m.s.ccur[i] = 0xFFFFFFFFu; m.s.cfill[i] = 0; }
+  for (int i = tid; i < NB; i += MAP_THREADS) m.s.bcnt[i] = 0;
+  if (tid == 0) m.s.misc[0] = 0;
   m.dict_n = w.ctl->dict_n;
   m.maxprobe = w.ctl->dict_maxprobe;
+  __syncthreads();
   unsigned long long ntok = 0;
 
-  const uint64_t tile0 = c.own_lo & ~15ull;
-  const uint64_t G = gridDim.x;
-  // register prefetch ring: segment of tile t, plus pre/post halo words for lanes 0/1
-  uint4 ring[PREFETCH];
-  uint4 halo[PREFETCH];
-#pragma unroll
-  for (int k = 0; k < PREFETCH; k++) {
-    uint64_t t = blockIdx.x + k * G;
-    uint64_t tb = tile0 + t * TILE;
-    ring[k] = t < ntiles ? load16(c, tb + tid * 16) : make_uint4(0, 0, 0, 0);
-    halo[k] = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    if (t < ntiles && tid == 0 && tb >= 16) halo[k] = load16(c, tb - 16);
-    if (t < ntiles && tid == 1) halo[k] = load16(c, tb + TILE);
-  }
-  for (uint64_t t = blockIdx.x; t < ntiles; t += G) {
-    const uint64_t tbase = tile0 + t * TILE;
-    uint4 cur = ring[0], hcur = halo[0];
-#pragma unroll
-    for (int k = 0; k + 1 < PREFETCH; k++) { ring[k] = ring[k + 1]; halo[k] = halo[k + 1]; }
+  const uint64_t base0 = c.own_lo & ~15ull;
+  const uint64_t nwaves = (uint64_t)gridDim.x * (MAP_THREADS / 64);
+  const uint64_t wid = (uint64_t)blockIdx.x * (MAP_THREADS / 64) + (tid >> 6);
+  const uint64_t per = nrows / nwaves, rem = nrows % nwaves;
+  const uint64_t rb = wid * per + (wid < rem ? wid : rem);
+  const uint64_t re = rb + per + (wid < rem ? 1 : 0);
+  if (rb < re) {
+    // the byte before this wave's first row (lane 0's left context)
+    uint32_t prev_last;
     {
-      uint64_t tn = t + PREFETCH * G;
-      uint64_t tb = tile0 + tn * TILE;
-      ring[PREFETCH - 1] = tn < ntiles ? load16(c, tb + tid * 16) : make_uint4(0, 0, 0, 0);
-      halo[PREFETCH - 1] = make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-      if (tn < ntiles && tid == 0 && tb >= 16) halo[PREFETCH - 1] = load16(c, tb - 16);
-      if (tn < ntiles && tid == 1) halo[PREFETCH - 1] = load16(c, tb + TILE);
+      const uint64_t pb = base0 + rb * 1024;
+      prev_last = (pb > c.lo && pb - 1 < c.hi) ? c.base[pb - 1] : 0x20u;
     }
-    if (tid == 0) m.s.flags[0] = 0;
-    *reinterpret_cast<uint4*>(m.s.tile + 16 + tid * 16) = cur;
-    uint32_t na = nonascii16(cur);
-    if (tid == 0) { *reinterpret_cast<uint4*>(m.s.tile) = hcur; na |= hcur.w; }   // 4 bytes before
-    if (tid == 1) { *reinterpret_cast<uint4*>(m.s.tile + 16 + TILE) = hcur; na |= nonascii16(hcur); }
-    na &= 0x80808080u;
-    // whitespace / zero masks of this lane's 16 bytes (valid when the tile is ASCII)
-    uint64_t lo64 = ((uint64_t)cur.y << 32) | cur.x, hi64 = ((uint64_t)cur.w << 32) | cur.z;
-    uint32_t ws16 = movemask8(ws_bytes80(lo64)) | (movemask8(ws_bytes80(hi64)) << 8);
-    uint32_t z16 = movemask8(zero_bytes80(lo64)) | (movemask8(zero_bytes80(hi64)) << 8);
-    m.s.masks[tid] = ws16 | (z16 << 16);
-    if (tid == 1) {
-      uint64_t l = ((uint64_t)hcur.y << 32) | hcur.x, h = ((uint64_t)hcur.w << 32) | hcur.z;
-      uint32_t a = movemask8(ws_bytes80(l)) | (movemask8(ws_bytes80(h)) << 8);
-      uint32_t z = movemask8(zero_bytes80(l)) | (movemask8(zero_bytes80(h)) << 8);
-      m.s.masks[MAP_THREADS] = a | (z << 16);
+    for (uint64_t r = rb; r < re; r += ROWB) {
+      const uint32_t nb = (uint32_t)((re - r) < ROWB ? (re - r) : ROWB);
+      uint4 seg[ROWB];
+#pragma unroll
+      for (int k = 0; k < ROWB; k++) seg[k] = raw16(c, base0 + (r + (k < (int)nb ? k : nb - 1)) * 1024 + lane * 16);
+      uint4 extra = raw16(c, base0 + (r + nb) * 1024);  // lane-0 segment of the following row
+      const uint64_t bstart = base0 + r * 1024, bend = base0 + (r + nb) * 1024 + 16;
+      const bool edge = bstart < c.lo || bend > c.hi;
+      if (edge) {
+#pragma unroll
+        for (int k = 0; k < ROWB; k++) seg[k] = fix16(c, base0 + (r + k) * 1024 + lane * 16, seg[k]);
+        extra = fix16(c, base0 + (r + nb) * 1024, extra);
+      }
+#pragma unroll
+      for (int k = 0; k < ROWB; k++) {
+        if ((uint32_t)k >= nb) break;
+        const uint4 a = seg[k];
+        const uint4 nxt = lane0(k + 1 < (int)nb ? seg[k + 1 < ROWB ? k + 1 : k] : extra);
+        uint4 bn = shfl_down1(a);
+        if (lane == 63) bn = nxt;
+        const uint32_t up = __shfl_up(a.w >> 24, 1);
+        const uint32_t prev = lane == 0 ? prev_last : up;
+        const uint64_t p0 = base0 + (r + k) * 1024 + lane * 16;
+        const bool slow = __any(nonascii16(a) | nonascii16(bn) | (prev & 0x80u));
+        if (slow) row_slow(m, p0, ntok);
+        else row_fast(m, p0, a, bn, is_ascii_ws(prev) ? 1u : 0u, ntok);
+        prev_last = __shfl(a.w >> 24, 63);
+      }
     }
-    __syncthreads();  // (A) previous flush done; flags reset visible
-    if (__any(na != 0) && (tid & 63) == 0) atomicOr(&m.s.flags[0], 1u);
-    __syncthreads();  // (B) tile, masks, flag visible
-    if (m.s.flags[0]) tile_slow(m, tbase, ntok);
-    else tile_fast(m, tbase, ntok);
-    __syncthreads();  // (C) all emits done
-    flush_queues(m, false);
-    // next iteration's barrier (A) orders this flush before the next emits
   }
   __syncthreads();
-  flush_queues(m, true);
-  __syncthreads();
-  // per-workgroup dictionary counts (summed by k_dict_totals)
   for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) w.dict_cnt[(uint64_t)blockIdx.x * DICT_SLOTS + i] = m.s.dcnt[i];
-  // tokens: wave reduce then one atomic per wave
+  for (int i = tid; i < NB; i += MAP_THREADS) {
+    const uint32_t n = m.s.bcnt[i];
+    w.cold_n[(uint64_t)blockIdx.x * NB + i] = n < w.cold_cap ? n : w.cold_cap;
+    if (n) atomicMax(&w.ctl->cold_need, n);
+  }
+  if (tid == 0) {
+    const uint32_t sn = m.s.misc[0];
+    w.spill_n[blockIdx.x] = sn < w.spill_cap ? sn : w.spill_cap;
+    if (sn) atomicMax(&w.ctl->spill_need, sn);
+  }
   for (int off = 32; off > 0; off >>= 1) ntok += __shfl_down(ntok, off);
-  if ((tid & 63) == 0 && ntok) atomicAdd(&w.ctl->tokens, ntok);
+  if (lane == 0 && ntok) atomicAdd(&w.ctl->tokens, ntok);
 }
 
 // ------------------------------------------------------------------ dictionary
+// Two-CAS claim of a 16-byte key in a global or LDS table (w1 is stored with the
+// top bit set so that 0 always means "unclaimed"); used only for heuristics.
+__device__ __forceinline__ bool claim16(unsigned long long* k0, unsigned long long* k1, uint64_t w0, uint64_t w1) {
+  const unsigned long long t1 = w1 | (1ull << 63);
+  unsigned long long o0 = atomicCAS(k0, 0ull, (unsigned long long)w0);
+  if (o0 != 0 && o0 != w0) return false;
+  unsigned long long o1 = atomicCAS(k1, 0ull, t1);
+  return o1 == 0 || o1 == t1;
+}
+
 // Sample pieces of the corpus, count short ASCII words per piece in LDS, merge
-// repeated ones into a global candidate table (all-atomic).  Heuristic only:
-// the dictionary decides speed, never counts.
+// repeated ones into a global candidate table.  Heuristic only: the dictionary
+// decides speed, never counts.
 extern "C" __global__ __launch_bounds__(1024) void k_sample(Corpus c, Work w, uint32_t npieces) {
-  __shared__ unsigned long long skey[SAMPLE_SLOTS];
+  __shared__ unsigned long long sk0[SAMPLE_SLOTS], sk1[SAMPLE_SLOTS];
   __shared__ uint32_t scnt[SAMPLE_SLOTS];
   const int tid = threadIdx.x;
-  for (int i = tid; i < SAMPLE_SLOTS; i += 1024) { skey[i] = 0; scnt[i] = 0; }
+  for (int i = tid; i < SAMPLE_SLOTS; i += 1024) { sk0[i] = 0; sk1[i] = 0; scnt[i] = 0; }
   __syncthreads();
-  uint64_t span = c.own_hi - c.own_lo;
-  uint64_t stride = span / npieces;
-  uint64_t ps = c.own_lo + stride * blockIdx.x;
+  const uint64_t span = c.own_hi - c.own_lo;
+  const uint64_t stride = span / npieces;
+  const uint64_t ps = c.own_lo + stride * blockIdx.x;
   uint64_t pe = ps + SAMPLE_PIECE;
   if (pe > c.own_hi) pe = c.own_hi;
-  uint64_t s0 = ps + (uint64_t)tid * (SAMPLE_PIECE / 1024);
+  const uint64_t s0 = ps + (uint64_t)tid * (SAMPLE_PIECE / 1024);
   uint64_t s1 = s0 + SAMPLE_PIECE / 1024;
   if (s1 > pe) s1 = pe;
   for (uint64_t p = s0; p < s1; p++) {
     uint8_t b = c.base[p];
     if (is_ascii_ws(b) || b >= 0x80) continue;
-    if (p > c.lo) { uint8_t pb = c.base[p - 1]; if (!is_ascii_ws(pb)) continue; }
-    uint64_t key = 0;
+    if (p > c.lo && !is_ascii_ws(c.base[p - 1])) continue;
+    uint64_t w0 = 0, w1 = 0;
     int len = 0;
     bool ok = true;
-    for (uint64_t q = p; ; q++) {
+    for (uint64_t q = p;; q++) {
       uint8_t x = byte_at(c, q);
       if (is_ascii_ws(x)) break;
-      if (x >= 0x80 || x == 0 || len == 8) { ok = false; break; }
-      key |= (uint64_t)ascii_lower(x) << (8 * len);
+      if (x >= 0x80 || x == 0 || len == 16) { ok = false; break; }
+      uint64_t lx = ascii_lower(x);
+      if (len < 8) w0 |= lx << (8 * len); else w1 |= lx << (8 * (len - 8));
       len++;
     }
     if (!ok || len == 0) continue;
-    uint64_t h = mix_hash(key, 0);
-    uint32_t slot = (uint32_t)h & (SAMPLE_SLOTS - 1);
+    uint32_t slot = key_hash(w0, w1) & (SAMPLE_SLOTS - 1);
     for (int pr = 0; pr < 64; pr++) {
-      unsigned long long old = atomicCAS(&skey[slot], 0ull, (unsigned long long)key);
-      if (old == 0 || old == key) { atomicAdd(&scnt[slot], 1u); break; }
+      if (claim16(&sk0[slot], &sk1[slot], w0, w1)) { atomicAdd(&scnt[slot], 1u); break; }
       slot = (slot + 1) & (SAMPLE_SLOTS - 1);
     }
   }
   __syncthreads();
   for (int i = tid; i < SAMPLE_SLOTS; i += 1024) {
-    uint64_t key = skey[i];
-    uint32_t n = scnt[i];
-    if (key == 0 || n < 2) continue;
-    uint64_t h = mix_hash(key, 0);
-    uint32_t slot = (uint32_t)(h >> 20) & (CAND_SLOTS - 1);
+    const uint64_t w0 = sk0[i], w1 = sk1[i] & ~(1ull << 63);
+    const uint32_t n = scnt[i];
+    if (w0 == 0 || sk1[i] == 0 || n < 2) continue;
+    uint32_t slot = (key_hash(w0, w1) >> 8) & (CAND_SLOTS - 1);
     for (int pr = 0; pr < 128; pr++) {
-      unsigned long long old = atomicCAS(&w.cand_key[slot], 0ull, (unsigned long long)key);
-      if (old == 0 || old == key) { atomicAdd(&w.cand_cnt[slot], (unsigned long long)n); break; }
+      if (claim16(&w.cand_key[2 * slot], &w.cand_key[2 * slot + 1], w0, w1)) {
+        atomicAdd(&w.cand_cnt[slot], (unsigned long long)n);
+        break;
+      }
       slot = (slot + 1) & (CAND_SLOTS - 1);
     }
   }
 }
 
 // Select the most frequent candidates and lay them out as the LDS hash image
-// (DICT_SLOTS slots, linear probing from mix_hash & (DICT_SLOTS-1)).
+// (DICT_SLOTS 16-byte keys, linear probing from key_hash & (DICT_SLOTS-1)).
 extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
-  __shared__ unsigned long long img[DICT_SLOTS];
+  __shared__ uint32_t claim[DICT_SLOTS];
   __shared__ uint32_t hist[64];
   __shared__ uint32_t maxprobe, nsel, thresh_log2;
   const int tid = threadIdx.x;
-  for (int i = tid; i < DICT_SLOTS; i += 1024) img[i] = 0;
+  for (int i = tid; i < DICT_SLOTS; i += 1024) { claim[i] = 0; w.dict_img[i] = make_uint4(0, 0, 0, 0); }
   if (tid < 64) hist[tid] = 0;
   if (tid == 0) { maxprobe = 0; nsel = 0; }
   __syncthreads();
-  // threshold 2^b: the smallest b with #(count >= 2^b) <= max_words
   for (int i = tid; i < CAND_SLOTS; i += 1024) {
-    uint64_t cnt = w.cand_cnt[i];
-    if (w.cand_key[i] != 0 && cnt >= 2) atomicAdd(&hist[63 - __clzll(cnt)], 1u);
+    const uint64_t cnt = w.cand_cnt[i];
+    if (w.cand_key[2 * i] != 0 && cnt >= 2) atomicAdd(&hist[63 - __clzll(cnt)], 1u);
   }
   __syncthreads();
   if (tid == 0) {
@@ -563,31 +528,35 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
   __syncthreads();
   const uint32_t tb = thresh_log2;
   for (int i = tid; i < CAND_SLOTS && tb < 64; i += 1024) {
-    uint64_t key = w.cand_key[i];
-    if (key == 0 || w.cand_cnt[i] < (1ull << tb)) continue;
-    uint32_t slot = (uint32_t)mix_hash(key, 0) & (DICT_SLOTS - 1);
+    const uint64_t w0 = w.cand_key[2 * i], w1t = w.cand_key[2 * i + 1];
+    if (w0 == 0 || w1t == 0 || w.cand_cnt[i] < (1ull << tb)) continue;
+    const uint64_t w1 = w1t & ~(1ull << 63);
+    uint32_t slot = key_hash(w0, w1) & (DICT_SLOTS - 1);
     for (uint32_t pr = 0; pr < DICT_SLOTS; pr++) {
-      unsigned long long old = atomicCAS(&img[slot], 0ull, (unsigned long long)key);
-      if (old == 0) { atomicMax(&maxprobe, pr); atomicAdd(&nsel, 1u); break; }
+      if (atomicCAS(&claim[slot], 0u, 1u) == 0u) {
+        w.dict_img[slot] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+        atomicMax(&maxprobe, pr);
+        atomicAdd(&nsel, 1u);
+        break;
+      }
       slot = (slot + 1) & (DICT_SLOTS - 1);
     }
   }
   __syncthreads();
-  for (int i = tid; i < DICT_SLOTS; i += 1024) w.dict_img[i] = img[i];
   if (tid == 0) { w.ctl->dict_n = nsel; w.ctl->dict_maxprobe = maxprobe; w.ctl->dict_thresh = tb; }
 }
 
 // Sum the per-workgroup dictionary counts and emit them as weighted records.
 extern "C" __global__ void k_dict_totals(Work w, uint32_t map_grid) {
-  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= DICT_SLOTS) return;
-  uint64_t key = w.dict_img[s];
-  if (key == 0) return;
+  const uint4 k = w.dict_img[s];
+  if ((k.x | k.y | k.z | k.w) == 0) return;
   uint64_t tot = 0;
   for (uint32_t g = 0; g < map_grid; g++) tot += w.dict_cnt[(uint64_t)g * DICT_SLOTS + s];
   if (tot == 0) return;
   unsigned long long i = atomicAdd(&w.ctl->w_n, 1ull);
-  if (i < w.w_cap) w.w[i] = WRec{key, 0, tot};
+  if (i < w.w_cap) w.w[i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, tot};
   else atomicOr(&w.ctl->overflow, OVF_W);
 }
 
@@ -708,105 +677,135 @@ extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
 }
 
 // ------------------------------------------------------------------ shuffle directory
-// Count chunks / records per bucket and weighted records per bucket.
+// Records per partition: cold regions (map workgroup x partition) and weighted
+// records (dictionary totals, Unicode-lane words, map spills).
 extern "C" __global__ void k_hist(Work w) {
-  __shared__ uint32_t hc[NB], hw[NB];
+  __shared__ uint32_t hw[NB];
   __shared__ unsigned long long hr[NB];
-  for (int i = threadIdx.x; i < NB; i += blockDim.x) { hc[i] = 0; hw[i] = 0; hr[i] = 0; }
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) { hw[i] = 0; hr[i] = 0; }
   __syncthreads();
-  uint64_t nch = w.ctl->pool_next; if (nch > w.pool_cap) nch = w.pool_cap;
-  uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nch; i += stride) {
-    uint32_t b = w.chunk_bucket[i];
-    atomicAdd(&hc[b], 1u);
-    atomicAdd(&hr[b], (unsigned long long)w.chunk_fill[i]);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint64_t ncell = (uint64_t)w.map_grid * NB;
+  for (uint64_t i = gtid; i < ncell; i += stride) {
+    const uint32_t n = w.cold_n[i];
+    if (n) atomicAdd(&hr[i % NB], (unsigned long long)n);
   }
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
-    WRec r = w.w[i];
-    uint32_t b = (uint32_t)(mix_hash(r.w0, r.w1) >> (64 - NB_LOG2));
-    atomicAdd(&hw[b], 1u);
+  uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
+  for (uint64_t i = gtid; i < nw; i += stride) {
+    const WRec r = w.w[i];
+    atomicAdd(&hw[bucket_of(key_hash(r.w0, r.w1))], 1u);
+  }
+  const uint64_t nsp = (uint64_t)w.map_grid * w.spill_cap;
+  for (uint64_t i = gtid; i < nsp; i += stride) {
+    if (i % w.spill_cap >= w.spill_n[i / w.spill_cap]) continue;
+    const uint4 k = w.spill[i];
+    atomicAdd(&hw[bucket_of(key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z))], 1u);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < NB; i += blockDim.x) {
-    if (hc[i]) atomicAdd(&w.b_chunks[i], hc[i]);
     if (hr[i]) atomicAdd((unsigned long long*)&w.b_recs[i], hr[i]);
     if (hw[i]) atomicAdd(&w.b_w[i], hw[i]);
   }
 }
 
 extern "C" __global__ void k_bucket_scan(Work w) {  // one workgroup of NB threads
-  __shared__ uint64_t a[NB], bw[NB], r[NB];
-  int b = threadIdx.x;
-  a[b] = w.b_chunks[b];
+  __shared__ uint64_t bw[NB], r[NB];
+  const int b = threadIdx.x;
   bw[b] = w.b_w[b];
   r[b] = w.b_recs[b] + w.b_w[b];
   __syncthreads();
   if (b == 0) {
-    uint64_t sa = 0, sw = 0, sr = 0, cold = 0;
+    uint64_t sw = 0, sr = 0, cold = 0;
     for (int i = 0; i < NB; i++) {
-      w.dir_off[i] = sa; w.w_off[i] = sw; w.rec_off[i] = sr;
-      sa += a[i]; sw += bw[i]; sr += r[i];
+      w.w_off[i] = sw; w.rec_off[i] = sr;
+      sw += bw[i]; sr += r[i];
       cold += w.b_recs[i];
     }
-    w.dir_off[NB] = sa; w.w_off[NB] = sw; w.rec_off[NB] = sr;
+    w.w_off[NB] = sw; w.rec_off[NB] = sr;
     w.ctl->cold_recs = cold;
+    if (sw > w.w_cap) atomicOr(&w.ctl->overflow, OVF_W);
+    if (sr > w.uniq_cap) atomicOr(&w.ctl->overflow, OVF_POOL);
+    w.ctl->w_total = sw;
   }
   w.b_cur[b] = 0;
-  w.b_cur[NB + b] = 0;
 }
 
 extern "C" __global__ void k_scatter(Work w) {
-  uint64_t nch = w.ctl->pool_next; if (nch > w.pool_cap) nch = w.pool_cap;
+  if (w.ctl->w_total > w.w_cap) return;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nch; i += stride) {
-    uint32_t b = w.chunk_bucket[i];
-    uint32_t k = atomicAdd(&w.b_cur[b], 1u);
-    w.dir[w.dir_off[b] + k] = (uint32_t)i;
-  }
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw; i += stride) {
-    WRec r = w.w[i];
-    uint32_t b = (uint32_t)(mix_hash(r.w0, r.w1) >> (64 - NB_LOG2));
-    uint32_t k = atomicAdd(&w.b_cur[NB + b], 1u);
+  for (uint64_t i = gtid; i < nw; i += stride) {
+    const WRec r = w.w[i];
+    const uint32_t b = bucket_of(key_hash(r.w0, r.w1));
+    const uint32_t k = atomicAdd(&w.b_cur[b], 1u);
     w.w_sorted[w.w_off[b] + k] = r;
+  }
+  const uint64_t nsp = (uint64_t)w.map_grid * w.spill_cap;
+  for (uint64_t i = gtid; i < nsp; i += stride) {
+    if (i % w.spill_cap >= w.spill_n[i / w.spill_cap]) continue;
+    const uint4 k = w.spill[i];
+    const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
+    const uint32_t b = bucket_of(key_hash(w0, w1));
+    const uint32_t j = atomicAdd(&w.b_cur[b], 1u);
+    w.w_sorted[w.w_off[b] + j] = WRec{w0, w1, 1};
   }
 }
 
 // ------------------------------------------------------------------ bucket reduce
+// One workgroup per partition: group its cold records (count 1, one contiguous
+// region per map workgroup) and weighted records by exact 16-byte key in an LDS
+// hash table, sort the distinct keys by (h32, key) with an LDS bitonic sort and
+// write them out.  A partition with more distinct keys than one table holds is
+// processed in 2^k sub-passes over the next hash bits; k comes from a
+// linear-counting estimate taken during pass 1.
+constexpr int RT2_SLOTS = 4608;
+constexpr int RT2_CAP = 3584;
+constexpr int LC_BITS = 32768;   // linear-counting bitmap
+constexpr int RED_UNROLL = 4;
+
 struct RedLds {
-  unsigned long long* h;   // RT_SLOTS (hash | 1, 0 = empty)
-  unsigned long long* k0;  // RT_SLOTS (0 = not yet published)
-  unsigned long long* k1;
-  unsigned long long* cnt;
-  uint16_t* idx;           // RT_SLOTS
-  uint32_t* misc;          // [0] uniques, [1] overflow, [2] processed-at-overflow
+  unsigned long long* k0;  // RT2_SLOTS (0 = free)
+  unsigned long long* k1;  // RT2_SLOTS
+  unsigned long long* cnt; // RT2_SLOTS (0 = not yet published)
+  uint32_t* hh;            // RT2_SLOTS key hash
+  uint16_t* idx;           // 4096
+  uint32_t* gpre;          // MAX_MAP_GRID + 1 prefix of region sizes
+  uint32_t* lc;            // LC_BITS / 32
+  uint32_t* misc;          // [0] uniques [1] overflow [2],[3] scratch
 };
 
-__device__ __forceinline__ void red_insert(const RedLds& s, uint64_t h, uint64_t w0, uint64_t w1, uint64_t cnt) {
-  uint64_t hh = h | 1;
-  uint32_t slot = (uint32_t)(h >> 1) & (RT_SLOTS - 1);
+__device__ __forceinline__ uint32_t red_slot(uint32_t h) {
+  return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * RT2_SLOTS) >> 32);
+}
+
+// Exact insert.  A slot is claimed by CAS on k0 (short keys have a non-zero
+// first byte, so w0 != 0); the claimant then stores k1, hh and finally
+// publishes cnt (> 0).  Readers retry a slot whose cnt is still 0 -- no
+// spinning inside divergent code.
+__device__ __forceinline__ void red_insert(const RedLds& s, uint32_t h, uint64_t w0, uint64_t w1, uint64_t c) {
+  uint32_t slot = red_slot(h);
   for (uint32_t it = 0; it < (1u << 22); it++) {
-    unsigned long long cur = s.h[slot];
+    unsigned long long cur = s.k0[slot];
     if (cur == 0) {
-      cur = atomicCAS(&s.h[slot], 0ull, (unsigned long long)hh);
+      cur = atomicCAS(&s.k0[slot], 0ull, (unsigned long long)w0);
       if (cur == 0) {
         s.k1[slot] = w1;
+        s.hh[slot] = h;
         __threadfence_block();
-        atomicExch(&s.k0[slot], (unsigned long long)w0);
-        atomicAdd(&s.cnt[slot], (unsigned long long)cnt);
-        uint32_t u = atomicAdd(&s.misc[0], 1u);
-        if (u >= RT_CAP) s.misc[1] = 1;
+        atomicAdd(&s.cnt[slot], (unsigned long long)c);
+        const uint32_t u = atomicAdd(&s.misc[0], 1u);
+        if (u >= RT2_CAP) s.misc[1] = 1;
         return;
       }
     }
-    if (cur == hh) {
-      unsigned long long a0 = __atomic_load_n(&s.k0[slot], __ATOMIC_RELAXED);
-      if (a0 == 0) continue;  // claimant still publishing this slot: retry it
+    if (cur == w0) {
+      if (__atomic_load_n(&s.cnt[slot], __ATOMIC_RELAXED) == 0) continue;  // claimant still publishing
       __threadfence_block();
-      if (a0 == w0 && s.k1[slot] == w1) { atomicAdd(&s.cnt[slot], (unsigned long long)cnt); return; }
+      if (s.k1[slot] == w1) { atomicAdd(&s.cnt[slot], (unsigned long long)c); return; }
     }
-    slot = (slot + 1) & (RT_SLOTS - 1);
+    slot = slot + 1 == RT2_SLOTS ? 0 : slot + 1;
   }
   s.misc[1] = 1;
 }
@@ -814,104 +813,134 @@ __device__ __forceinline__ void red_insert(const RedLds& s, uint64_t h, uint64_t
 __device__ __forceinline__ bool red_less(const RedLds& s, uint16_t a, uint16_t b) {
   if (a == 0xFFFF) return false;
   if (b == 0xFFFF) return true;
-  uint64_t ha = s.h[a], hb = s.h[b];
-  if (ha != hb) return ha < hb;
+  if (s.hh[a] != s.hh[b]) return s.hh[a] < s.hh[b];
   if (s.k0[a] != s.k0[b]) return s.k0[a] < s.k0[b];
   return s.k1[a] < s.k1[b];
+}
+
+__device__ __forceinline__ bool in_sub(uint32_t h, uint32_t kk, uint32_t sub) {
+  return kk == 0 || ((h << NB_LOG2) >> (32 - kk)) == sub;
 }
 
 extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   RedLds s;
   uint8_t* sp = smem;
-  s.h = (unsigned long long*)sp; sp += RT_SLOTS * 8;
-  s.k0 = (unsigned long long*)sp; sp += RT_SLOTS * 8;
-  s.k1 = (unsigned long long*)sp; sp += RT_SLOTS * 8;
-  s.cnt = (unsigned long long*)sp; sp += RT_SLOTS * 8;
-  s.idx = (uint16_t*)sp; sp += RT_SLOTS * 2;
+  s.k0 = (unsigned long long*)sp; sp += RT2_SLOTS * 8;
+  s.k1 = (unsigned long long*)sp; sp += RT2_SLOTS * 8;
+  s.cnt = (unsigned long long*)sp; sp += RT2_SLOTS * 8;
+  s.hh = (uint32_t*)sp; sp += RT2_SLOTS * 4;
+  s.idx = (uint16_t*)sp; sp += 4096 * 2;
+  s.gpre = (uint32_t*)sp; sp += (MAX_MAP_GRID + 4) * 4;
+  s.lc = (uint32_t*)sp; sp += LC_BITS / 8;
   s.misc = (uint32_t*)sp; sp += 64;
   const int tid = threadIdx.x;
   const uint32_t b = blockIdx.x;
-  const uint64_t d0 = w.dir_off[b], d1 = w.dir_off[b + 1];
+  const uint32_t G = w.map_grid;
   const uint64_t ws0 = w.w_off[b], ws1 = w.w_off[b + 1];
-  const uint64_t nrec = w.b_recs[b] + (ws1 - ws0);
   const uint64_t out0 = w.rec_off[b];
-  uint32_t k_log2 = 0;
+  // prefix over map workgroups of this partition's region sizes
+  if (tid == 0) {
+    uint32_t acc = 0;
+    for (uint32_t g = 0; g < G; g++) { s.gpre[g] = acc; acc += w.cold_n[(uint64_t)g * NB + b]; }
+    s.gpre[G] = acc;
+  }
+  for (int i = tid; i < LC_BITS / 32; i += RED_THREADS) s.lc[i] = 0;
+  __syncthreads();
+  const uint32_t ncold = s.gpre[G];
+  uint32_t kk = 0;
+  bool estimated = false;
   uint64_t written = 0;
-  uint32_t sub = 0;
-  while (sub < (1u << k_log2)) {
-    for (int i = tid; i < RT_SLOTS; i += RED_THREADS) { s.h[i] = 0; s.k0[i] = 0; s.k1[i] = 0; s.cnt[i] = 0; }
-    if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
+  for (uint32_t sub = 0; sub < (1u << kk);) {
+    for (int i = tid; i < RT2_SLOTS; i += RED_THREADS) { s.k0[i] = 0; s.cnt[i] = 0; }
+    if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; }
     __syncthreads();
-    const uint32_t kk = k_log2;
-    uint64_t seen = 0;  // records examined before an overflow was noticed (estimate for k)
-    // cold chunks: 4 chunks per pass of 1024 lanes, one 16-byte record per lane
-    for (uint64_t ci = d0; ci < d1; ci += RED_THREADS / CHUNK_RECS) {
-      uint64_t my = ci + tid / CHUNK_RECS;
-      uint32_t r = tid % CHUNK_RECS;
-      if (my < d1) {
-        uint32_t ch = w.dir[my];
-        if (r < w.chunk_fill[ch]) {
-          uint4 v = w.pool[(uint64_t)ch * CHUNK_RECS + r];
-          uint64_t w0 = ((uint64_t)v.y << 32) | v.x, w1 = ((uint64_t)v.w << 32) | v.z;
-          uint64_t h = mix_hash(w0, w1);
-          if (kk == 0 || (uint32_t)((h << NB_LOG2) >> (64 - kk)) == sub) red_insert(s, h, w0, w1, 1);
+    const bool first = !estimated;
+    for (uint32_t i0 = 0; i0 < ncold; i0 += RED_THREADS * RED_UNROLL) {
+      uint4 v[RED_UNROLL];
+      bool ok[RED_UNROLL];
+#pragma unroll
+      for (int u = 0; u < RED_UNROLL; u++) {
+        const uint32_t i = i0 + u * RED_THREADS + tid;
+        ok[u] = i < ncold;
+        if (ok[u]) {
+          int a = 0, z = (int)G - 1;  // region g with gpre[g] <= i < gpre[g+1]
+          while (a < z) { const int mid = (a + z + 1) >> 1; if (s.gpre[mid] <= i) a = mid; else z = mid - 1; }
+          v[u] = w.cold[((uint64_t)a * NB + b) * w.cold_cap + (i - s.gpre[a])];
         }
       }
-      seen += RED_THREADS;
-      __syncthreads();
-      const bool ovf = s.misc[1] != 0;
-      __syncthreads();
-      if (ovf) break;
-    }
-    if (!s.misc[1]) {
-      for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
-        WRec r = w.w_sorted[i];
-        uint64_t h = mix_hash(r.w0, r.w1);
-        if (kk == 0 || (uint32_t)((h << NB_LOG2) >> (64 - kk)) == sub) red_insert(s, h, r.w0, r.w1, r.count);
+      const bool stop = __atomic_load_n(&s.misc[1], __ATOMIC_RELAXED) != 0;
+#pragma unroll
+      for (int u = 0; u < RED_UNROLL; u++) {
+        if (!ok[u]) continue;
+        const uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x, w1 = ((uint64_t)v[u].w << 32) | v[u].z;
+        const uint32_t h = key_hash(w0, w1);
+        if (first) { const uint32_t bit = (h * 0x85EBCA6Bu) >> 17; atomicOr(&s.lc[bit >> 5], 1u << (bit & 31)); }
+        if (!stop && in_sub(h, kk, sub)) red_insert(s, h, w0, w1, 1);
       }
-      seen = nrec;
+      if (!first) {  // later passes: stop early on overflow (uniform decision)
+        __syncthreads();
+        const bool ovf = s.misc[1] != 0;
+        __syncthreads();
+        if (ovf) break;
+      }
+    }
+    for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
+      const WRec rr = w.w_sorted[i];
+      const uint32_t h = key_hash(rr.w0, rr.w1);
+      if (first) { const uint32_t bit = (h * 0x85EBCA6Bu) >> 17; atomicOr(&s.lc[bit >> 5], 1u << (bit & 31)); }
+      if (!__atomic_load_n(&s.misc[1], __ATOMIC_RELAXED) && in_sub(h, kk, sub)) red_insert(s, h, rr.w0, rr.w1, rr.count);
     }
     __syncthreads();
     if (s.misc[1]) {
-      // too many distinct words for one LDS table: split this bucket into
-      // 2^k sub-ranges of the next hash bits and restart it
-      uint64_t est = (nrec + (seen ? seen : 1) - 1) / (seen ? seen : 1);
-      uint32_t need = kk + 1;
-      while ((1ull << need) < est * 2 && need < 20) need++;
-      k_log2 = need;
+      if (first) {  // too many distinct keys for one table: estimate them, then split
+        uint32_t z = 0;
+        for (int i = tid; i < LC_BITS / 32; i += RED_THREADS) z += 32 - __popc(s.lc[i]);
+        __syncthreads();
+        if (tid == 0) s.misc[2] = 0;
+        __syncthreads();
+        atomicAdd(&s.misc[2], z);
+        __syncthreads();
+        const double zf = s.misc[2] ? (double)s.misc[2] / LC_BITS : 0.5 / LC_BITS;
+        const double est = -(double)LC_BITS * log(zf);
+        uint32_t need = 1;
+        while ((double)(1u << need) * RT2_CAP < est * 1.25 && need < 20) need++;
+        kk = need;
+      } else {
+        kk++;
+      }
+      estimated = true;
       sub = 0;
       written = 0;
       __syncthreads();
       continue;
     }
-    // compact + bitonic sort (hash, key) for a deterministic order
+    estimated = true;
+    // compact + bitonic sort by (h32, key) for a deterministic order
     const uint32_t nu = s.misc[0];
     __syncthreads();
     if (tid == 0) s.misc[3] = 0;
     __syncthreads();
-    for (int i = tid; i < RT_SLOTS; i += RED_THREADS) {
-      if (s.h[i]) { uint32_t p = atomicAdd(&s.misc[3], 1u); s.idx[p] = (uint16_t)i; }
-    }
+    for (int i = tid; i < RT2_SLOTS; i += RED_THREADS)
+      if (s.cnt[i]) { const uint32_t p = atomicAdd(&s.misc[3], 1u); s.idx[p] = (uint16_t)i; }
     __syncthreads();
-    for (int i = nu + tid; i < RT_SLOTS; i += RED_THREADS) s.idx[i] = 0xFFFF;
+    for (int i = nu + tid; i < 4096; i += RED_THREADS) s.idx[i] = 0xFFFF;
     uint32_t N = 1;
     while (N < nu) N <<= 1;
     __syncthreads();
     for (uint32_t size = 2; size <= N; size <<= 1) {
       for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
         for (uint32_t i = tid; i < N / 2; i += RED_THREADS) {
-          uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-          bool up = (lo & size) == 0;
-          uint16_t a = s.idx[lo], c2 = s.idx[hi];
-          bool swap = up ? red_less(s, c2, a) : red_less(s, a, c2);
-          if (swap) { s.idx[lo] = c2; s.idx[hi] = a; }
+          const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+          const bool up = (lo & size) == 0;
+          const uint16_t a = s.idx[lo], c2 = s.idx[hi];
+          if (up ? red_less(s, c2, a) : red_less(s, a, c2)) { s.idx[lo] = c2; s.idx[hi] = a; }
         }
         __syncthreads();
       }
     }
     for (uint32_t i = tid; i < nu; i += RED_THREADS) {
-      uint16_t sl = s.idx[i];
+      const uint16_t sl = s.idx[i];
       w.uk[out0 + written + i] = make_uint4((uint32_t)s.k0[sl], (uint32_t)(s.k0[sl] >> 32), (uint32_t)s.k1[sl],
                                             (uint32_t)(s.k1[sl] >> 32));
       w.uc[out0 + written + i] = s.cnt[sl];
@@ -922,7 +951,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
   }
   if (tid == 0) {
     w.b_uniq[b] = written;
-    if (k_log2) atomicMax(&w.ctl->max_sub, 1u << k_log2);
+    if (kk) atomicMax(&w.ctl->max_sub, 1u << kk);
   }
 }
 
