@@ -93,6 +93,7 @@ struct mox_engine {
   hipStream_t stream = nullptr;
   uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 64;
   int n_cu = 256;
+  bool sync_each = false;
   Work w{};
   Tables tables{};
   Ctl* h_ctl = nullptr;       // pinned
@@ -283,6 +284,12 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   auto rec = [&](int i) {
     if (timing) (void)hipEventRecord(e->ev[i], s);
   };
+  // MOX_SYNC_EACH=1: synchronise after every launch and name it (hang / fault triage)
+  auto step = [&](const char* name) {
+    if (!e->sync_each) return;
+    hipError_t er = hipStreamSynchronize(s);
+    fprintf(stderr, "[mox] %s done: %s\n", name, hipGetErrorString(er));
+  };
   rec(0);
   HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_init, sizeof(Ctl), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
@@ -291,7 +298,9 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
     HIPCHK(hipMemsetAsync(w.cand_key, 0, CAND_SLOTS * 24, s));
     hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
+  step("k_sample");
     hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
+  step("k_dict_build");
   }
   rec(1);
   // 2. map: one streaming pass over the corpus
@@ -299,25 +308,39 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + 1023) / 1024 : 0;
   const int grid = (int)w.map_grid;
   hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows);
+  step("k_map");
   rec(2);
   // 3. lanes
   hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
+  step("k_unicode");
   hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w, (uint32_t)grid);
+  step("k_dict_totals");
   rec(3);
   // 4. shuffle directory + bucket reduce
   hipLaunchKernelGGL(k_hist, dim3(512), dim3(256), 0, s, w);
+  step("k_hist");
   hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(NB), 0, s, w);
+  step("k_bucket_scan");
   hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, s, w);
+  step("k_scatter");
   hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);
+  step("k_reduce");
   rec(4);
   // 5. table
   hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(64), 0, s, w);
+  step("k_final_scan");
   hipLaunchKernelGGL(k_long_flags, dim3(256), dim3(256), 0, s, w, e->d_lens);
+  step("k_long_flags");
   launch_scan(e, e->d_lens, nullptr, w.long_cap, w.long_cap, w.lpos);
+  step("scan_long");
   hipLaunchKernelGGL(k_mat_counts, dim3(1024), dim3(256), 0, s, w, e->d_lens);
+  step("k_mat_counts");
   hipLaunchKernelGGL(k_mat_long, dim3(256), dim3(256), 0, s, w, e->d_lens);
+  step("k_mat_long");
   launch_scan(e, e->d_lens, &w.ctl->n_total, 0, w.table_cap, w.t_offs);
+  step("scan_offs");
   hipLaunchKernelGGL(k_mat_bytes, dim3(1024), dim3(256), 0, s, w, c);
+  step("k_mat_bytes");
   rec(5);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(e->h_ctl, w.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s));
@@ -350,6 +373,8 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     if (h.halo_err != ~0ull)
       return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
     if (!h.overflow) break;
+    if (h.overflow & OVF_REDUCE)
+      return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
     if (attempt >= 4) return fail(MOX_ENOMEM, "buffer growth did not converge (overflow mask 0x%x)", h.overflow);
     Caps need = caps_of(e->w);
     if (h.overflow & OVF_POOL) {
@@ -446,6 +471,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
   if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
+  e->sync_each = getenv("MOX_SYNC_EACH") != nullptr;
   int rc = alloc_fixed(e);
   if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));
   if (rc != MOX_OK) {

@@ -27,7 +27,9 @@ constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points 
 enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u };
 enum : uint32_t {
   OVF_POOL = 1u, OVF_W = 2u, OVF_U = 4u, OVF_LONG = 8u, OVF_ARENA = 16u, OVF_PROBE = 32u,
-  OVF_TABLE = 64u, OVF_BYTES = 128u
+  OVF_TABLE = 64u, OVF_BYTES = 128u, OVF_REDUCE = 256u,
+  // overflows that make the records of this attempt incomplete
+  OVF_RERUN = OVF_POOL | OVF_W | OVF_U | OVF_LONG | OVF_ARENA | OVF_PROBE
 };
 
 // Control block: counters written by the kernels, read back once per run.

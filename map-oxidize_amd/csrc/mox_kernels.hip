@@ -837,6 +837,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
   const int tid = threadIdx.x;
   const uint32_t b = blockIdx.x;
   const uint32_t G = w.map_grid;
+  // an overflowed map or directory means this attempt is rerun with larger
+  // buffers: its records are incomplete (w_sorted may not even be written)
+  if (w.ctl->overflow & OVF_RERUN) {
+    if (tid == 0) w.b_uniq[b] = 0;
+    return;
+  }
   const uint64_t ws0 = w.w_off[b], ws1 = w.w_off[b + 1];
   const uint64_t out0 = w.rec_off[b];
   // prefix over map workgroups of this partition's region sizes
@@ -908,6 +914,10 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
         kk = need;
       } else {
         kk++;
+      }
+      if (kk > 32 - NB_LOG2) {  // > RT2_CAP distinct keys share every hash bit: cannot split
+        if (tid == 0) { atomicOr(&w.ctl->overflow, OVF_REDUCE); w.b_uniq[b] = 0; }
+        return;
       }
       estimated = true;
       sub = 0;
