@@ -30,8 +30,8 @@ using namespace mox;
 extern "C" {
 __global__ void k_map(Corpus c, Work w, uint64_t ntiles);
 __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
-__global__ void k_dict_build(Work w, uint32_t max_words);
-__global__ void k_dict_totals(Work w, uint32_t map_grid);
+__global__ void k_dict_build(Work w, uint32_t max_words, uint32_t npieces);
+__global__ void k_dict_totals(Work w);
 __global__ void k_unicode(Corpus c, Work w, Tables T);
 __global__ void k_hist(Work w);
 __global__ void k_bucket_scan(Work w);
@@ -91,7 +91,7 @@ struct DevBuf {
 struct mox_engine {
   int device = 0;
   hipStream_t stream = nullptr;
-  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 64;
+  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 128;
   int n_cu = 256;
   bool sync_each = false;
   Work w{};
@@ -138,7 +138,7 @@ Caps caps_of(const Work& w) {
 Caps initial_caps(uint64_t n, int map_grid) {
   Caps c;
   // cold records per (workgroup, partition) region: about one per 8 input bytes
-  c.cold_cap = std::max<uint64_t>(64, n / ((uint64_t)map_grid * NB * 8));
+  c.cold_cap = std::max<uint64_t>(64, n / ((uint64_t)map_grid * NB * 12));
   c.spill_cap = std::max<uint64_t>(1024, n / ((uint64_t)map_grid * 64));
   c.w_cap = 65536 + n / 64;
   c.u_cap = 4096 + n / 64;
@@ -213,10 +213,11 @@ int alloc_fixed(mox_engine* e) {
   Work& w = e->w;
   int rc;
   if ((rc = dalloc(e, (void**)&w.ctl, sizeof(Ctl)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.cand_key, CAND_SLOTS * 8 * 3))) return rc;
-  w.cand_cnt = w.cand_key + 2 * CAND_SLOTS;
-  if ((rc = dalloc(e, (void**)&w.dict_img, DICT_SLOTS * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dict_cnt, (size_t)e->n_cu * DICT_SLOTS * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.cand, (size_t)MAX_SAMPLE_PIECES * SAMPLE_OUT * sizeof(WRec)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.cand_n, MAX_SAMPLE_PIECES * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_tag, DICT_SLOTS * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_key, DICT_SLOTS * 16))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_tot, DICT_SLOTS * 8))) return rc;
   w.map_grid = (uint32_t)std::min(e->n_cu, MAX_MAP_GRID);
   if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.spill_n, (size_t)w.map_grid * 4))) return rc;
@@ -251,19 +252,20 @@ int alloc_fixed(mox_engine* e) {
   memset(e->h_ctl_init, 0, sizeof(Ctl));
   e->h_ctl_init->err_utf8 = ~0ull;
   e->h_ctl_init->halo_err = ~0ull;
-  HIPCHK(hipMemset(w.dict_img, 0, DICT_SLOTS * 16));
+  HIPCHK(hipMemset(w.dict_tag, 0, DICT_SLOTS * 4));
   return MOX_OK;
 }
 
-size_t map_lds_bytes() { return DICT_SLOTS * 16 + DICT_SLOTS * 4 + NB * 4 + 16; }
-size_t reduce_lds_bytes() { return 4608 * (8 * 3 + 4) + 4096 * 2 + (MAX_MAP_GRID + 4) * 4 + 32768 / 8 + 64; }
+size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_BUCKETS * 4; }
+size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + MAP_WAVES * (ROWBUF + 2 * TOKMAX); }
+size_t reduce_lds_bytes() { return 2560 * (8 * 3 + 4) + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP (mox_kernels.hip)
 
 // exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)
 int launch_scan(mox_engine* e, const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
                 uint64_t* out) {
   hipLaunchKernelGGL(k_scan_reduce, dim3(SCAN_WGS), dim3(SCAN_THREADS), 0, e->stream, v, n_ptr, n_const, n_cap,
                      e->w.scan_part);
-  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(64), 0, e->stream, e->w.scan_part, SCAN_WGS);
+  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_WGS), 0, e->stream, e->w.scan_part, SCAN_WGS);
   hipLaunchKernelGGL(k_scan_apply, dim3(SCAN_WGS), dim3(SCAN_THREADS), 0, e->stream, v, n_ptr, n_const, n_cap,
                      (const uint64_t*)e->w.scan_part, out);
   return MOX_OK;
@@ -296,10 +298,10 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
   // 1. hot dictionary from a sample
   if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
-    HIPCHK(hipMemsetAsync(w.cand_key, 0, CAND_SLOTS * 24, s));
+    HIPCHK(hipMemsetAsync(w.dict_tot, 0, DICT_SLOTS * 8, s));
     hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
   step("k_sample");
-    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
+    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), dict_lds_bytes(), s, w, e->dict_words, e->sample_pieces);
   step("k_dict_build");
   }
   rec(1);
@@ -313,7 +315,7 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   // 3. lanes
   hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
   step("k_unicode");
-  hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w, (uint32_t)grid);
+  hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w);
   step("k_dict_totals");
   rec(3);
   // 4. shuffle directory + bucket reduce
@@ -327,7 +329,7 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   step("k_reduce");
   rec(4);
   // 5. table
-  hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(64), 0, s, w);
+  hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(NB), 0, s, w);
   step("k_final_scan");
   hipLaunchKernelGGL(k_long_flags, dim3(256), dim3(256), 0, s, w, e->d_lens);
   step("k_long_flags");
@@ -381,8 +383,10 @@ int run_corpus(mox_engine* e, const Corpus& c) {
       need.cold_cap = std::max<uint64_t>(need.cold_cap, h.cold_need + h.cold_need / 8 + 16);
       need.spill_cap = std::max<uint64_t>(need.spill_cap, h.spill_need + h.spill_need / 4 + 1024);
     }
-    if (h.overflow & OVF_W) need.w_cap = std::max<uint64_t>(need.w_cap, h.w_total + h.w_total / 4 + 1024);
-    if (h.overflow & OVF_W) need.w_cap = h.w_n + h.w_n / 4 + 1024;
+    if (h.overflow & OVF_W) {
+      const uint64_t wn = std::max<uint64_t>(h.w_total, h.w_n);
+      need.w_cap = std::max<uint64_t>(need.w_cap, wn + wn / 4 + 1024);
+    }
     if (h.overflow & OVF_U) need.u_cap = h.u_n + h.u_n / 4 + 1024;
     if (h.overflow & OVF_ARENA) need.arena_cap = h.arena_n + h.arena_n / 4 + 65536;
     if (h.overflow & OVF_LONG) need.long_cap = next_pow2(2 * h.long_n + 1024);
@@ -441,7 +445,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     dev = cfg->device;
     e->flags = cfg->flags;
     if (cfg->dict_words) e->dict_words = std::min<uint32_t>(cfg->dict_words, DICT_MAX_WORDS);
-    if (cfg->sample_pieces) e->sample_pieces = std::min<uint32_t>(cfg->sample_pieces, 4096);
+    if (cfg->sample_pieces) e->sample_pieces = std::min<uint32_t>(cfg->sample_pieces, MAX_SAMPLE_PIECES);
   }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
@@ -466,7 +470,8 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
   }
   for (auto& ev : e->ev) (void)hipEventCreate(&ev);
   if (hipFuncSetAttribute((const void*)k_map, hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes()) != hipSuccess) {
+      hipFuncSetAttribute((const void*)k_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes()) != hipSuccess ||
+      hipFuncSetAttribute((const void*)k_dict_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dict_lds_bytes()) != hipSuccess) {
     mox_engine_destroy(e);
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
@@ -490,7 +495,7 @@ void mox_engine_destroy(mox_engine* e) {
   (void)hipDeviceSynchronize();
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
-  void* ptrs[] = {w.ctl, w.cand_key, w.dict_img, w.dict_cnt, w.cold_n, w.spill_n, w.b_recs, w.scan_part, (void*)e->tables.lower_src,
+  void* ptrs[] = {w.ctl, w.cand, w.cand_n, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, w.scan_part, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_lens, e->d_text};
   for (void* p : ptrs) dfree(p);

@@ -9,12 +9,19 @@ namespace mox {
 // ---- geometry ----
 constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
 constexpr int MAX_MAP_GRID = 1024;          // map workgroups (one per CU)
-constexpr int NB_LOG2 = 8;                  // cold-record partitions (hash top bits)
+constexpr int MAP_WAVES = MAP_THREADS / 64;
+constexpr int ROW = 1024;                   // bytes one wave classifies per step (64 lanes x 16 B)
+constexpr int ROWBUF = ROW + 32;            // lowered row + 16 B look-ahead + pad (LDS)
+constexpr int TOKMAX = ROW / 2;             // token starts per row (at most every other byte)
+constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
-constexpr int DICT_SLOTS = 4096;            // LDS hot-dictionary hash slots (16-byte keys)
-constexpr int DICT_MAX_WORDS = 3072;
-constexpr int CAND_SLOTS = 1 << 14;         // dictionary candidate table (global)
-constexpr int SAMPLE_PIECE = 64 * 1024;
+constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
+constexpr int DICT_SLOTS = 4 * DICT_BUCKETS;
+constexpr int DICT_MAX_WORDS = 3584;
+constexpr int CAND_SLOTS = 6144;            // dictionary candidate table (LDS of k_dict_build)
+constexpr int MAX_SAMPLE_PIECES = 256;
+constexpr int SAMPLE_OUT = 1024;            // candidates one sample piece hands to k_dict_build
+constexpr int SAMPLE_PIECE = 16 * 1024;     // one 1024-thread workgroup x 16 B
 constexpr int SAMPLE_SLOTS = 4096;
 constexpr int RED_THREADS = 1024;
 constexpr int SCAN_THREADS = 1024;
@@ -96,10 +103,11 @@ struct Corpus {
 struct Work {  // device buffers of one engine
   Ctl* ctl;
   // dictionary
-  unsigned long long* cand_key;   // 2 * CAND_SLOTS (w0, w1 | 1<<63)
-  unsigned long long* cand_cnt;   // CAND_SLOTS
-  uint4* dict_img;                // DICT_SLOTS 16-byte keys
-  uint32_t* dict_cnt;             // [map_grid][DICT_SLOTS]
+  WRec* cand;                     // MAX_SAMPLE_PIECES x SAMPLE_OUT (word, count in its piece)
+  uint32_t* cand_n;               // MAX_SAMPLE_PIECES
+  uint32_t* dict_tag;             // DICT_SLOTS key hashes (0 = empty), bucket b = slots 4b..4b+3
+  uint4* dict_key;                // DICT_SLOTS lowered 16-byte keys
+  unsigned long long* dict_tot;   // DICT_SLOTS counts summed over map workgroups
   // cold records: region (map workgroup g, partition b) = cold[(g*NB + b)*cold_cap ...]
   uint4* cold;                    // map_grid * NB * cold_cap records of 16 B
   uint32_t* cold_n;               // map_grid * NB records written per region

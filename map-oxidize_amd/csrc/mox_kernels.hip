@@ -52,6 +52,25 @@ __device__ __forceinline__ uint64_t lo_mask(int nbytes) {  // 0 <= nbytes <= 8
   return nbytes >= 8 ? ~0ull : ((1ull << (8 * nbytes)) - 1);
 }
 
+// Exclusive scan of one value per thread over a 1024-thread workgroup.
+__device__ __forceinline__ uint64_t block_exscan(uint64_t x, uint64_t* wsum, uint64_t& total) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint64_t incl = x;
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint64_t y = __shfl_up(incl, off);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) wsum[wv] = incl;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+  for (int k = 0; k < nw; k++) { const uint64_t t = wsum[k]; if (k < wv) pre += t; tot += t; }
+  __syncthreads();
+  total = tot;
+  return pre + incl - x;
+}
+
+// Exclusive scan of v[0..n) (n = *n_ptr) into out[0..n], out[n] = total.
+// Three launches: per-WG totals, one-WG scan of totals, per-WG rescan + offset.
 // Corpus byte with out-of-range bytes reading as ' ' (whitespace).
 __device__ __forceinline__ uint8_t byte_at(const Corpus& c, uint64_t p) {
   if (p < c.lo || p >= c.hi) return 0x20;
@@ -159,8 +178,9 @@ __device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint
 }
 
 // ------------------------------------------------------------------ map kernel
-// 32-bit key hash for short (<= 16 byte) keys: bucket = top 8 bits, LDS slots
-// use the low bits.  Final table order is (h32, key), so it is deterministic.
+// 32-bit key hash for short (<= 16 byte) keys: partition = top 8 bits,
+// dictionary buckets and reduce slots use other bits.  Final table order is
+// (h32, key), so it is deterministic.
 __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   uint32_t h = (uint32_t)w0 * 0x9E3779B1u + (uint32_t)(w0 >> 32) * 0x85EBCA77u + (uint32_t)w1 * 0xC2B2AE3Du +
                (uint32_t)(w1 >> 32) * 0x27D4EB2Fu;
@@ -172,42 +192,76 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   return h;
 }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - NB_LOG2); }
+// the two dictionary buckets of a key (2-choice hashing; the first is preferred)
+__device__ __forceinline__ uint32_t dict_b1(uint32_t h) { return h & (DICT_BUCKETS - 1); }
+__device__ __forceinline__ uint32_t dict_b2(uint32_t h) { return (h >> 10) & (DICT_BUCKETS - 1); }
+
 
 struct MapLds {
-  uint4* dkey;      // DICT_SLOTS 16-byte keys (0 = empty)
+  uint4* dtag4;     // DICT_BUCKETS x 4 tags (0 = empty)
+  uint4* dkey;      // DICT_SLOTS 16-byte keys
   uint32_t* dcnt;   // DICT_SLOTS
   uint32_t* bcnt;   // NB: cold records this workgroup wrote per partition
   uint32_t* misc;   // [0] spills
+  uint8_t* wave;    // MAP_WAVES x (ROWBUF + 2 * TOKMAX): lowered row + token list
 };
 
 struct MapCtx {
   Corpus c;
   Work w;
   MapLds s;
-  uint32_t dict_n, maxprobe;
+  uint32_t dict_n;
 };
 
-// A short word (lowered length <= 16, no NUL byte): exact 16-byte key.
+__device__ __forceinline__ bool key_eq(uint4 k, uint64_t w0, uint64_t w1) {
+  return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && k.w == (uint32_t)(w1 >> 32);
+}
+// slot of bucket b whose tag is h and whose key is (w0, w1), or -1
+__device__ __forceinline__ int bucket_find(const MapLds& s, uint32_t b, uint4 t, uint32_t h, uint64_t w0, uint64_t w1) {
+  if (t.x == h && key_eq(s.dkey[4 * b + 0], w0, w1)) return (int)(4 * b + 0);
+  if (t.y == h && key_eq(s.dkey[4 * b + 1], w0, w1)) return (int)(4 * b + 1);
+  if (t.z == h && key_eq(s.dkey[4 * b + 2], w0, w1)) return (int)(4 * b + 2);
+  if (t.w == h && key_eq(s.dkey[4 * b + 3], w0, w1)) return (int)(4 * b + 3);
+  return -1;
+}
+// Dictionary lookup.  Buckets fill slot 0..3 in order and a word goes to its
+// second bucket only when the first was full, so a first bucket with a free
+// slot ends the search.
+__device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w0, uint64_t w1) {
+  const uint32_t b1 = dict_b1(h);
+  const uint4 t1 = s.dtag4[b1];
+  int slot = bucket_find(s, b1, t1, h, w0, w1);
+  if (slot < 0 && t1.w != 0) {
+    const uint32_t b2 = dict_b2(h);
+    slot = bucket_find(s, b2, s.dtag4[b2], h, w0, w1);
+  }
+  return slot;
+}
+
+__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1);
+
+// A short word (lowered length <= 16, no NUL byte) as an exact 16-byte key.
 // Hot words: LDS dictionary count.  Others: appended to this workgroup's
 // region of the word's partition (the shuffle write), no global atomics.
 __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_t w1) {
   const uint32_t h = key_hash(w0, w1);
   if (m.w.dbg & DBG_NO_EMIT) { asm volatile("" ::"v"(h)); return; }
-  const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   if (m.dict_n && !(m.w.dbg & DBG_NO_DICT)) {
-    uint32_t slot = h & (DICT_SLOTS - 1);
-    for (uint32_t i = 0; i <= m.maxprobe; i++) {
-      const uint4 k = m.s.dkey[slot];
-      if (k.x == key.x && k.y == key.y && k.z == key.z && k.w == key.w) {
-        if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
-        return;
-      }
-      if ((k.x | k.y | k.z | k.w) == 0) break;
-      slot = (slot + 1) & (DICT_SLOTS - 1);
+    const int slot = dict_find(m.s, h, w0, w1);
+    if (slot >= 0) {
+      if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
+      return;
     }
   }
+  cold_word(m, h, w0, w1);
+}
+
+// A word not in the dictionary: appended to this workgroup's region of its
+// hash partition (the shuffle write), no global atomics.
+__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
   const uint32_t b = bucket_of(h);
   if (m.w.dbg & DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
+  const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < m.w.cold_cap) {
     m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
@@ -222,7 +276,7 @@ __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_
 }
 
 // Any token, walked byte by byte from global memory (rare: long tokens, tokens
-// running past the 32-byte window, rows with non-ASCII bytes).
+// running past the look-ahead window, rows with non-ASCII bytes).
 __device__ void generic_token(const MapCtx& m, uint64_t p) {
   const Corpus& c = m.c;
   uint64_t q = p;
@@ -297,6 +351,10 @@ __device__ __forceinline__ uint32_t zero_mask16(uint4 v) {
   const uint64_t l = ((uint64_t)v.y << 32) | v.x, h = ((uint64_t)v.w << 32) | v.z;
   return movemask8(zero_bytes80(l)) | (movemask8(zero_bytes80(h)) << 8);
 }
+__device__ __forceinline__ uint4 lower16(uint4 v) {
+  const uint64_t l = lower_ascii(((uint64_t)v.y << 32) | v.x), h = lower_ascii(((uint64_t)v.w << 32) | v.z);
+  return make_uint4((uint32_t)l, (uint32_t)(l >> 32), (uint32_t)h, (uint32_t)(h >> 32));
+}
 __device__ __forceinline__ uint4 shfl_down1(uint4 v) {
   return make_uint4(__shfl_down(v.x, 1), __shfl_down(v.y, 1), __shfl_down(v.z, 1), __shfl_down(v.w, 1));
 }
@@ -304,61 +362,165 @@ __device__ __forceinline__ uint4 lane0(uint4 v) {
   return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
-
-// Fast path of one row (64 lanes x 16 B, all ASCII): per-lane token extraction
-// from a 32-byte window (own 16 B + the next lane's 16 B).
-__device__ __forceinline__ void row_fast(const MapCtx& m, uint64_t p0, uint4 a, uint4 bn, uint32_t prevws,
-                                         unsigned long long& ntok) {
-  const uint32_t ws32 = ws_mask16(a) | (ws_mask16(bn) << 16);
-  const uint32_t z32 = zero_mask16(a) | (zero_mask16(bn) << 16);
-  uint32_t start = (~ws32) & ((ws32 << 1) | prevws) & 0xFFFFu;
-  if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
-  if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
-  if (m.w.dbg & DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
-  ntok += __popc(start);
-  uint64_t W0 = ((uint64_t)a.y << 32) | a.x, W1 = ((uint64_t)a.w << 32) | a.z;
-  uint64_t W2 = ((uint64_t)bn.y << 32) | bn.x, W3 = ((uint64_t)bn.w << 32) | bn.z;
-  W0 = lower_ascii(W0); W1 = lower_ascii(W1); W2 = lower_ascii(W2); W3 = lower_ascii(W3);
-  while (start) {
-    const int p = __builtin_ctz(start);
-    start &= start - 1;
-    const uint32_t rest = ws32 >> p;
-    const int len = rest ? __builtin_ctz(rest) : 32;
-    const bool odd = rest == 0 || len > 16 || (p0 + p + len >= m.c.hi && !m.c.at_end) ||
-                     ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
-    if (odd) { generic_token(m, p0 + p); continue; }
-    const int k = p >> 3, r = (p & 7) * 8;
-    const uint64_t A = k ? W1 : W0, B = k ? W2 : W1, C = k ? W3 : W2;
-    uint64_t w0 = r ? (A >> r) | (B << (64 - r)) : A;
-    uint64_t w1 = r ? (B >> r) | (C << (64 - r)) : B;
-    if (len <= 8) { w0 &= lo_mask(len); w1 = 0; }
-    else w1 &= lo_mask(len - 8);
-    short_word(m, w0, w1);
-  }
+// compiler + LDS ordering between lanes of one wave (LDS executes a wave's
+// instructions in order; this keeps the compiler from reordering across it)
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Slow path of one row: validate UTF-8, find tokens with Unicode whitespace.
-__device__ void row_slow(const MapCtx& m, uint64_t p0, unsigned long long& ntok) {
+// Token starts of a row with non-ASCII bytes (per lane, its 16 bytes): UTF-8
+// validation and Unicode White_Space.  All of them take the generic walk.
+__device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
+  uint32_t st = 0;
   for (int j = 0; j < 16; j++) {
     const uint64_t p = p0 + j;
     if (p < m.c.own_lo || p >= m.c.own_hi) continue;
     const int v = utf8_check(m.c, p);
     if (v == 1) atomicMin(&m.w.ctl->err_utf8, (unsigned long long)(p - m.c.lo));
     else if (v == 2) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - m.c.lo));
-    if (m.w.dbg & DBG_NO_TOKENS) continue;
     if (in_ws(m.c, p)) continue;
     const bool start = (p == m.c.lo) ? true : in_ws(m.c, p - 1);
-    if (start && (m.c.base[p] & 0xC0) != 0x80) {
-      ntok++;
-      generic_token(m, p);
-    }
+    if (start && (m.c.base[p] & 0xC0) != 0x80) st |= 1u << j;
   }
+  return st;
 }
 
-// Every wave streams its own contiguous range of 1 KiB rows, ROWB rows per
-// batch (one wait per batch; 16 independent waves per CU keep ~64 KiB of loads
-// in flight).  No workgroup barrier inside the loop.
-constexpr int ROWB = 4;
+// One row (64 lanes x 16 B) in two phases:
+//  1. byte phase (lane = 16 B): token-start bit masks (SWAR on ASCII rows, the
+//     Unicode walk on rows with non-ASCII bytes), the lowered row into LDS and a
+//     compacted list of token (start, length) in row order (wave prefix sum of
+//     per-lane start counts from 5 bit-sliced ballots);
+//  2. token phase (lane = token): 64 tokens per step read their key from the
+//     LDS row, hash it and count it in the dictionary or emit it.
+constexpr int TU = 4;  // token batches per lane in flight
+
+__device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, uint4 bn, uint32_t prev,
+                                       unsigned long long& ntok, uint8_t* rowbuf, uint16_t* list) {
+  const int lane = threadIdx.x & 63;
+  const bool slow = __any(nonascii16(a) | nonascii16(bn) | (prev & 0x80u));
+  uint32_t ws32 = 0, z32 = 0, start;
+  if (!slow) {
+    ws32 = ws_mask16(a) | (ws_mask16(bn) << 16);
+    z32 = zero_mask16(a) | (zero_mask16(bn) << 16);
+    start = (~ws32) & ((ws32 << 1) | (is_ascii_ws(prev) ? 1u : 0u)) & 0xFFFFu;
+    if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
+    if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
+  } else {
+    start = slow_starts(m, p0);
+  }
+  if (m.w.dbg & DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
+  const uint32_t cnt = __popc(start);
+  ntok += cnt;
+  // wave-exclusive prefix of cnt (0..16) and the wave total
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t pre = 0, total = 0;
+#pragma unroll
+  for (int bit = 0; bit < 5; bit++) {
+    const uint64_t bm = __ballot((cnt >> bit) & 1u);
+    pre += (uint32_t)__popcll(bm & lt) << bit;
+    total += (uint32_t)__popcll(bm) << bit;
+  }
+  if (total == 0) return;
+  reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
+  if (lane == 63) reinterpret_cast<uint4*>(rowbuf)[64] = lower16(bn);
+  // list entry (u16): start in row (10 bits) | length (5 bits, <= 16) | odd (bit 15)
+  uint32_t k = pre;
+  bool any_odd = false;
+  while (start) {
+    const int p = __builtin_ctz(start);
+    start &= start - 1;
+    const uint32_t rest = ws32 >> p;
+    const int len = rest ? __builtin_ctz(rest) : 32;
+    const bool odd = slow || rest == 0 || len > 16 || (p0 + p + len >= m.c.hi && !m.c.at_end) ||
+                     ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
+    any_odd |= odd;
+    list[k++] = (uint16_t)((uint32_t)(lane * 16 + p) | (odd ? 0x8000u : ((uint32_t)len << 10)));
+  }
+  wave_lds_fence();
+  const uint64_t rowbase = p0 - (uint64_t)lane * 16;
+  if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
+    for (uint32_t j = lane; j < total; j += 64) {
+      const uint32_t e = list[j];
+      if (e & 0x8000u) generic_token(m, rowbase + (e & 1023u));
+    }
+  }
+  if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
+  // fast tokens, TU batches of 64 in flight per lane (independent LDS chains)
+  const uint4* rb4 = reinterpret_cast<const uint4*>(rowbuf);
+  const bool use_dict = m.dict_n && !(m.w.dbg & DBG_NO_DICT);
+  for (uint32_t j0 = 0; j0 < total; j0 += 64 * TU) {
+    uint32_t e[TU];
+#pragma unroll
+    for (int u = 0; u < TU; u++) {
+      const uint32_t j = j0 + u * 64 + lane;
+      e[u] = j < total ? (uint32_t)list[j] : 0x8000u;  // inactive = odd
+    }
+    uint64_t w0[TU], w1[TU];
+    uint32_t h[TU];
+#pragma unroll
+    for (int u = 0; u < TU; u++) {
+      const uint32_t pos = e[u] & 1023u, len = (e[u] >> 10) & 31u;
+      const uint4 x = rb4[pos >> 4], y = rb4[(pos >> 4) + 1];
+      const uint64_t W0 = ((uint64_t)x.y << 32) | x.x, W1 = ((uint64_t)x.w << 32) | x.z;
+      const uint64_t W2 = ((uint64_t)y.y << 32) | y.x, W3 = ((uint64_t)y.w << 32) | y.z;
+      const int kk = (pos >> 3) & 1, r = (pos & 7) * 8;
+      const uint64_t A = kk ? W1 : W0, B = kk ? W2 : W1, C = kk ? W3 : W2;
+      uint64_t a0 = r ? (A >> r) | (B << (64 - r)) : A;
+      uint64_t a1 = r ? (B >> r) | (C << (64 - r)) : B;
+      if (len <= 8) { a0 &= lo_mask((int)len); a1 = 0; }
+      else a1 &= lo_mask((int)len - 8);
+      w0[u] = a0;
+      w1[u] = a1;
+      h[u] = key_hash(a0, a1);
+    }
+    int slot[TU];
+#pragma unroll
+    for (int u = 0; u < TU; u++) {
+      slot[u] = -1;
+      if (use_dict) {
+        const uint32_t b1 = dict_b1(h[u]), b2 = dict_b2(h[u]);
+        const uint4 t1 = m.s.dtag4[b1], t2 = m.s.dtag4[b2];
+        int sl = t2.w == h[u] ? (int)(4 * b2 + 3) : -1;
+        sl = t2.z == h[u] ? (int)(4 * b2 + 2) : sl;
+        sl = t2.y == h[u] ? (int)(4 * b2 + 1) : sl;
+        sl = t2.x == h[u] ? (int)(4 * b2 + 0) : sl;
+        sl = t1.w == h[u] ? (int)(4 * b1 + 3) : sl;
+        sl = t1.z == h[u] ? (int)(4 * b1 + 2) : sl;
+        sl = t1.y == h[u] ? (int)(4 * b1 + 1) : sl;
+        sl = t1.x == h[u] ? (int)(4 * b1 + 0) : sl;
+        slot[u] = sl;
+      }
+    }
+    bool hit[TU];
+#pragma unroll
+    for (int u = 0; u < TU; u++) {
+      const uint4 kq = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
+      hit[u] = slot[u] >= 0 && key_eq(kq, w0[u], w1[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < TU; u++) {
+      if (e[u] & 0x8000u) continue;
+      if (hit[u]) {
+        if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
+        continue;
+      }
+      if (slot[u] >= 0) {  // tag matched another word: full search (rare)
+        const int s2 = dict_find(m.s, h[u], w0[u], w1[u]);
+        if (s2 >= 0) { atomicAdd(&m.s.dcnt[s2], 1u); continue; }
+      }
+      cold_word(m, h[u], w0[u], w1[u]);
+    }
+  }
+  wave_lds_fence();
+}
+
+// Every wave streams its own contiguous range of 1 KiB rows.  Rows rotate
+// through DEPTH register slots: the load of row r + DEPTH is issued before row
+// r is processed, and row r + 1's lane-0 segment is row r's look-ahead.  No
+// workgroup barrier inside the loop.
+constexpr int DEPTH = 4;
 
 extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t nrows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -366,22 +528,28 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   m.c = c;
   m.w = w;
   uint8_t* sp = smem;
+  m.s.dtag4 = (uint4*)sp; sp += DICT_SLOTS * 4;
   m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
   m.s.misc = (uint32_t*)sp; sp += 16;
+  m.s.wave = sp;
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) { m.s.dkey[i] = w.dict_img[i]; m.s.dcnt[i] = 0; }
+  m.dict_n = w.ctl->dict_n;
+  if (m.dict_n) {
+    for (int i = tid; i < DICT_BUCKETS; i += MAP_THREADS) m.s.dtag4[i] = reinterpret_cast<const uint4*>(w.dict_tag)[i];
+    for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) { m.s.dkey[i] = w.dict_key[i]; m.s.dcnt[i] = 0; }
+  }
   for (int i = tid; i < NB; i += MAP_THREADS) m.s.bcnt[i] = 0;
   if (tid == 0) m.s.misc[0] = 0;
-  m.dict_n = w.ctl->dict_n;
-  m.maxprobe = w.ctl->dict_maxprobe;
   __syncthreads();
+  uint8_t* rowbuf = m.s.wave + (tid >> 6) * (ROWBUF + 2 * TOKMAX);
+  uint16_t* list = reinterpret_cast<uint16_t*>(rowbuf + ROWBUF);
   unsigned long long ntok = 0;
 
   const uint64_t base0 = c.own_lo & ~15ull;
-  const uint64_t nwaves = (uint64_t)gridDim.x * (MAP_THREADS / 64);
-  const uint64_t wid = (uint64_t)blockIdx.x * (MAP_THREADS / 64) + (tid >> 6);
+  const uint64_t nwaves = (uint64_t)gridDim.x * MAP_WAVES;
+  const uint64_t wid = (uint64_t)blockIdx.x * MAP_WAVES + (tid >> 6);
   const uint64_t per = nrows / nwaves, rem = nrows % nwaves;
   const uint64_t rb = wid * per + (wid < rem ? wid : rem);
   const uint64_t re = rb + per + (wid < rem ? 1 : 0);
@@ -389,41 +557,40 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
     // the byte before this wave's first row (lane 0's left context)
     uint32_t prev_last;
     {
-      const uint64_t pb = base0 + rb * 1024;
+      const uint64_t pb = base0 + rb * ROW;
       prev_last = (pb > c.lo && pb - 1 < c.hi) ? c.base[pb - 1] : 0x20u;
     }
-    for (uint64_t r = rb; r < re; r += ROWB) {
-      const uint32_t nb = (uint32_t)((re - r) < ROWB ? (re - r) : ROWB);
-      uint4 seg[ROWB];
-#pragma unroll
-      for (int k = 0; k < ROWB; k++) seg[k] = raw16(c, base0 + (r + (k < (int)nb ? k : nb - 1)) * 1024 + lane * 16);
-      uint4 extra = raw16(c, base0 + (r + nb) * 1024);  // lane-0 segment of the following row
-      const uint64_t bstart = base0 + r * 1024, bend = base0 + (r + nb) * 1024 + 16;
-      const bool edge = bstart < c.lo || bend > c.hi;
-      if (edge) {
-#pragma unroll
-        for (int k = 0; k < ROWB; k++) seg[k] = fix16(c, base0 + (r + k) * 1024 + lane * 16, seg[k]);
-        extra = fix16(c, base0 + (r + nb) * 1024, extra);
+    // rows past the corpus read as blanks (raw16 clamps, fix16 blanks them)
+    uint4 s0 = raw16(c, base0 + rb * ROW + lane * 16);
+    uint4 s1 = raw16(c, base0 + (rb + 1) * ROW + lane * 16);
+    uint4 s2 = raw16(c, base0 + (rb + 2) * ROW + lane * 16);
+    uint4 s3 = raw16(c, base0 + (rb + 3) * ROW + lane * 16);
+    for (uint64_t r = rb; r < re; r++) {
+      uint4 a = s0, nx = s1;
+      s0 = s1; s1 = s2; s2 = s3;
+      s3 = raw16(c, base0 + (r + DEPTH) * ROW + lane * 16);
+      const uint64_t p0 = base0 + r * ROW + lane * 16;
+      const uint64_t rs = base0 + r * ROW;
+      if (rs < c.lo || rs + ROW + 16 > c.hi) {
+        a = fix16(c, p0, a);
+        nx = fix16(c, rs + ROW + lane * 16, nx);
       }
-#pragma unroll
-      for (int k = 0; k < ROWB; k++) {
-        if ((uint32_t)k >= nb) break;
-        const uint4 a = seg[k];
-        const uint4 nxt = lane0(k + 1 < (int)nb ? seg[k + 1 < ROWB ? k + 1 : k] : extra);
-        uint4 bn = shfl_down1(a);
-        if (lane == 63) bn = nxt;
-        const uint32_t up = __shfl_up(a.w >> 24, 1);
-        const uint32_t prev = lane == 0 ? prev_last : up;
-        const uint64_t p0 = base0 + (r + k) * 1024 + lane * 16;
-        const bool slow = __any(nonascii16(a) | nonascii16(bn) | (prev & 0x80u));
-        if (slow) row_slow(m, p0, ntok);
-        else row_fast(m, p0, a, bn, is_ascii_ws(prev) ? 1u : 0u, ntok);
-        prev_last = __shfl(a.w >> 24, 63);
-      }
+      uint4 bn = shfl_down1(a);
+      const uint4 nxt = lane0(nx);  // look-ahead: the next row's first 16 bytes
+      if (lane == 63) bn = nxt;
+      const uint32_t up = __shfl_up(a.w >> 24, 1);
+      const uint32_t prev = lane == 0 ? prev_last : up;
+      do_row(m, p0, a, bn, prev, ntok, rowbuf, list);
+      prev_last = __shfl(a.w >> 24, 63);
     }
   }
   __syncthreads();
-  for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) w.dict_cnt[(uint64_t)blockIdx.x * DICT_SLOTS + i] = m.s.dcnt[i];
+  if (m.dict_n) {
+    for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
+      const uint32_t n = m.s.dcnt[i];
+      if (n) atomicAdd(&w.dict_tot[i], (unsigned long long)n);
+    }
+  }
   for (int i = tid; i < NB; i += MAP_THREADS) {
     const uint32_t n = m.s.bcnt[i];
     w.cold_n[(uint64_t)blockIdx.x * NB + i] = n < w.cold_cap ? n : w.cold_cap;
@@ -449,36 +616,44 @@ __device__ __forceinline__ bool claim16(unsigned long long* k0, unsigned long lo
   return o1 == 0 || o1 == t1;
 }
 
-// Sample pieces of the corpus, count short ASCII words per piece in LDS, merge
-// repeated ones into a global candidate table.  Heuristic only: the dictionary
-// decides speed, never counts.
+// Sample pieces of the corpus (one 16 KiB piece per workgroup, staged in LDS)
+// and count their short ASCII words in LDS; words seen at least twice go to
+// this piece's candidate list (plain stores, no global atomics).  Heuristic
+// only: the dictionary decides speed, never counts.
 extern "C" __global__ __launch_bounds__(1024) void k_sample(Corpus c, Work w, uint32_t npieces) {
+  __shared__ __attribute__((aligned(16))) uint8_t buf[SAMPLE_PIECE + 32];
   __shared__ unsigned long long sk0[SAMPLE_SLOTS], sk1[SAMPLE_SLOTS];
   __shared__ uint32_t scnt[SAMPLE_SLOTS];
+  __shared__ uint32_t nout;
   const int tid = threadIdx.x;
   for (int i = tid; i < SAMPLE_SLOTS; i += 1024) { sk0[i] = 0; sk1[i] = 0; scnt[i] = 0; }
-  __syncthreads();
+  if (tid == 0) nout = 0;
   const uint64_t span = c.own_hi - c.own_lo;
   const uint64_t stride = span / npieces;
-  const uint64_t ps = c.own_lo + stride * blockIdx.x;
-  uint64_t pe = ps + SAMPLE_PIECE;
-  if (pe > c.own_hi) pe = c.own_hi;
-  const uint64_t s0 = ps + (uint64_t)tid * (SAMPLE_PIECE / 1024);
-  uint64_t s1 = s0 + SAMPLE_PIECE / 1024;
-  if (s1 > pe) s1 = pe;
-  for (uint64_t p = s0; p < s1; p++) {
-    uint8_t b = c.base[p];
-    if (is_ascii_ws(b) || b >= 0x80) continue;
-    if (p > c.lo && !is_ascii_ws(c.base[p - 1])) continue;
+  const uint64_t ps = (c.own_lo + stride * blockIdx.x) & ~15ull;  // 16-aligned piece start
+  // stage [ps - 16, ps + PIECE + 16) (out-of-range bytes read as spaces)
+  for (int i = tid; i < (SAMPLE_PIECE + 32) / 16; i += 1024) {
+    const uint64_t p = ps - 16 + (uint64_t)i * 16;
+    const bool in = p + 16 > c.lo && p < c.hi;
+    uint4 v = in ? fix16(c, p, raw16(c, p)) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
+    reinterpret_cast<uint4*>(buf)[i] = v;
+  }
+  __syncthreads();
+  // thread t scans piece bytes [16 t, 16 t + 16), i.e. buf[16 + 16 t ...]
+  for (int j = 0; j < 16; j++) {
+    const int q = 16 + tid * 16 + j;
+    const uint8_t b = buf[q];
+    if (is_ascii_ws(b) || b >= 0x80 || !is_ascii_ws(buf[q - 1])) continue;
     uint64_t w0 = 0, w1 = 0;
     int len = 0;
     bool ok = true;
-    for (uint64_t q = p;; q++) {
-      uint8_t x = byte_at(c, q);
-      if (is_ascii_ws(x)) break;
-      if (x >= 0x80 || x == 0 || len == 16) { ok = false; break; }
-      uint64_t lx = ascii_lower(x);
-      if (len < 8) w0 |= lx << (8 * len); else w1 |= lx << (8 * (len - 8));
+    for (int x = q;; x++) {
+      if (x >= SAMPLE_PIECE + 32) { ok = false; break; }
+      const uint8_t y = buf[x];
+      if (is_ascii_ws(y)) break;
+      if (y >= 0x80 || y == 0 || len == 16) { ok = false; break; }
+      const uint64_t ly = ascii_lower(y);
+      if (len < 8) w0 |= ly << (8 * len); else w1 |= ly << (8 * (len - 8));
       len++;
     }
     if (!ok || len == 0) continue;
@@ -489,72 +664,120 @@ extern "C" __global__ __launch_bounds__(1024) void k_sample(Corpus c, Work w, ui
     }
   }
   __syncthreads();
+  WRec* out = w.cand + (uint64_t)blockIdx.x * SAMPLE_OUT;
   for (int i = tid; i < SAMPLE_SLOTS; i += 1024) {
-    const uint64_t w0 = sk0[i], w1 = sk1[i] & ~(1ull << 63);
     const uint32_t n = scnt[i];
-    if (w0 == 0 || sk1[i] == 0 || n < 2) continue;
-    uint32_t slot = (key_hash(w0, w1) >> 8) & (CAND_SLOTS - 1);
-    for (int pr = 0; pr < 128; pr++) {
-      if (claim16(&w.cand_key[2 * slot], &w.cand_key[2 * slot + 1], w0, w1)) {
-        atomicAdd(&w.cand_cnt[slot], (unsigned long long)n);
-        break;
-      }
-      slot = (slot + 1) & (CAND_SLOTS - 1);
-    }
+    if (n < 2 || sk0[i] == 0 || sk1[i] == 0) continue;
+    const uint32_t o = atomicAdd(&nout, 1u);
+    if (o < SAMPLE_OUT) out[o] = WRec{sk0[i], sk1[i] & ~(1ull << 63), n};
   }
+  __syncthreads();
+  if (tid == 0) w.cand_n[blockIdx.x] = nout < SAMPLE_OUT ? nout : SAMPLE_OUT;
 }
 
-// Select the most frequent candidates and lay them out as the LDS hash image
-// (DICT_SLOTS 16-byte keys, linear probing from key_hash & (DICT_SLOTS-1)).
-extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
-  __shared__ uint32_t claim[DICT_SLOTS];
-  __shared__ uint32_t hist[64];
-  __shared__ uint32_t maxprobe, nsel, thresh_log2;
+// Merge the pieces' candidate lists in an LDS table, select the most frequent
+// words (count threshold from a log2 histogram refined by a linear one) and
+// lay them out as the LDS dictionary image: tag = key hash in the first free
+// slot of bucket b1, else of bucket b2, hottest words first.
+extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words, uint32_t npieces) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  unsigned long long* ck0 = (unsigned long long*)smem;
+  unsigned long long* ck1 = ck0 + CAND_SLOTS;
+  uint32_t* ccnt = (uint32_t*)(ck1 + CAND_SLOTS);
+  uint32_t* fill = ccnt + CAND_SLOTS;  // DICT_BUCKETS
+  __shared__ uint32_t hist[64], fine[256];
+  __shared__ uint32_t nsel, thresh_lo, cls;
   const int tid = threadIdx.x;
-  for (int i = tid; i < DICT_SLOTS; i += 1024) { claim[i] = 0; w.dict_img[i] = make_uint4(0, 0, 0, 0); }
+  for (int i = tid; i < CAND_SLOTS; i += 1024) { ck0[i] = 0; ck1[i] = 0; ccnt[i] = 0; }
+  for (int i = tid; i < DICT_BUCKETS; i += 1024) fill[i] = 0;
+  for (int i = tid; i < DICT_SLOTS; i += 1024) { w.dict_tag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
   if (tid < 64) hist[tid] = 0;
-  if (tid == 0) { maxprobe = 0; nsel = 0; }
+  if (tid < 256) fine[tid] = 0;
+  if (tid == 0) nsel = 0;
+  __syncthreads();
+  __shared__ uint32_t pn[MAX_SAMPLE_PIECES];
+  for (uint32_t i = tid; i < npieces; i += 1024) pn[i] = w.cand_n[i];
+  __syncthreads();
+  for (uint32_t x = tid; x < npieces * SAMPLE_OUT; x += 1024) {
+    const uint32_t pc = x / SAMPLE_OUT, i = x % SAMPLE_OUT;
+    {
+      if (i >= pn[pc]) continue;
+      const WRec r = w.cand[x];
+      uint32_t slot = key_hash(r.w0, r.w1) % CAND_SLOTS;
+      for (int pr = 0; pr < 256; pr++) {
+        if (claim16(&ck0[slot], &ck1[slot], r.w0, r.w1)) { atomicAdd(&ccnt[slot], (uint32_t)r.count); break; }
+        slot = slot + 1 == CAND_SLOTS ? 0 : slot + 1;
+      }
+    }
+  }
   __syncthreads();
   for (int i = tid; i < CAND_SLOTS; i += 1024) {
-    const uint64_t cnt = w.cand_cnt[i];
-    if (w.cand_key[2 * i] != 0 && cnt >= 2) atomicAdd(&hist[63 - __clzll(cnt)], 1u);
+    const uint32_t cnt = ccnt[i];
+    if (cnt) atomicAdd(&hist[31 - __clz(cnt)], 1u);
+  }
+  __syncthreads();
+  // class k: all candidates with log2(count) > k fit; k itself may not
+  if (tid == 0) {
+    uint32_t acc = 0, k = 64;
+    for (int b = 63; b >= 0; b--) { if (acc + hist[b] > max_words) { k = b; break; } acc += hist[b]; k = b - 1; }
+    cls = k;       // candidates in class k are split by the fine histogram (k == ~0u: all fit)
+    nsel = acc;    // candidates strictly above class k
+  }
+  __syncthreads();
+  const uint32_t k = cls;
+  // fine histogram of class k: count in [2^k, 2^(k+1)) in 256 linear bins
+  for (int i = tid; i < CAND_SLOTS && k < 32; i += 1024) {
+    const uint64_t cnt = ccnt[i];
+    if (cnt == 0 || (uint32_t)(31 - __clz((uint32_t)cnt)) != k) continue;
+    const uint32_t bin = k >= 8 ? (uint32_t)((cnt - (1ull << k)) >> (k - 8)) : (uint32_t)((cnt - (1ull << k)) << (8 - k));
+    atomicAdd(&fine[bin > 255 ? 255 : bin], 1u);
   }
   __syncthreads();
   if (tid == 0) {
-    uint32_t acc = 0, b = 64;
-    for (int k = 63; k >= 1; k--) { if (acc + hist[k] > max_words) break; acc += hist[k]; b = k; }
-    thresh_log2 = b;
-  }
-  __syncthreads();
-  const uint32_t tb = thresh_log2;
-  for (int i = tid; i < CAND_SLOTS && tb < 64; i += 1024) {
-    const uint64_t w0 = w.cand_key[2 * i], w1t = w.cand_key[2 * i + 1];
-    if (w0 == 0 || w1t == 0 || w.cand_cnt[i] < (1ull << tb)) continue;
-    const uint64_t w1 = w1t & ~(1ull << 63);
-    uint32_t slot = key_hash(w0, w1) & (DICT_SLOTS - 1);
-    for (uint32_t pr = 0; pr < DICT_SLOTS; pr++) {
-      if (atomicCAS(&claim[slot], 0u, 1u) == 0u) {
-        w.dict_img[slot] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-        atomicMax(&maxprobe, pr);
-        atomicAdd(&nsel, 1u);
-        break;
-      }
-      slot = (slot + 1) & (DICT_SLOTS - 1);
+    uint64_t lo = 1;  // select count >= lo
+    if (k < 32) {
+      uint32_t acc = nsel;
+      int b = 255;
+      for (; b >= 0; b--) { if (acc + fine[b] > max_words) break; acc += fine[b]; }
+      const uint32_t fb = (uint32_t)(b + 1);  // bins >= fb fit
+      lo = (1ull << k) + (k >= 8 ? ((uint64_t)fb << (k - 8)) : (((uint64_t)fb + (1ull << (8 - k)) - 1) >> (8 - k)));
+      if (fb >= 256) lo = 1ull << (k + 1);
     }
+    thresh_lo = (uint32_t)(lo > 0xFFFFFFFFull ? 0xFFFFFFFFull : lo);
+    nsel = 0;
   }
   __syncthreads();
-  if (tid == 0) { w.ctl->dict_n = nsel; w.ctl->dict_maxprobe = maxprobe; w.ctl->dict_thresh = tb; }
+  const uint64_t lo = thresh_lo < 1 ? 1 : thresh_lo;
+  // insert by descending log2 count class, so that a word dropped because both
+  // of its buckets are full is never hotter than the words that filled them
+  for (int cl = 31; cl >= 0; cl--) {
+    if (cl < 31 && (2ull << cl) <= lo) break;  // every count in this class is < lo
+    for (int i = tid; i < CAND_SLOTS; i += 1024) {
+      const uint32_t cnt = ccnt[i];
+      if (cnt == 0 || cnt < lo || (31 - __clz(cnt)) != cl) continue;
+      const uint64_t w0 = ck0[i], w1 = ck1[i] & ~(1ull << 63);
+      const uint32_t h = key_hash(w0, w1);
+      if (h == 0) continue;  // tag 0 marks an empty slot
+      uint32_t b = dict_b1(h);
+      uint32_t f = atomicAdd(&fill[b], 1u);
+      if (f >= 4) { b = dict_b2(h); f = atomicAdd(&fill[b], 1u); }
+      if (f >= 4) continue;  // both buckets full: this word stays cold
+      w.dict_tag[4 * b + f] = h;
+      w.dict_key[4 * b + f] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+      atomicAdd(&nsel, 1u);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) { w.ctl->dict_n = nsel; w.ctl->dict_thresh = thresh_lo; }
 }
 
-// Sum the per-workgroup dictionary counts and emit them as weighted records.
-extern "C" __global__ void k_dict_totals(Work w, uint32_t map_grid) {
+// Emit the dictionary totals (summed by k_map's atomics) as weighted records.
+extern "C" __global__ void k_dict_totals(Work w) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= DICT_SLOTS) return;
-  const uint4 k = w.dict_img[s];
-  if ((k.x | k.y | k.z | k.w) == 0) return;
-  uint64_t tot = 0;
-  for (uint32_t g = 0; g < map_grid; g++) tot += w.dict_cnt[(uint64_t)g * DICT_SLOTS + s];
+  if (s >= DICT_SLOTS || w.ctl->dict_n == 0 || w.dict_tag[s] == 0) return;
+  const uint64_t tot = w.dict_tot[s];
   if (tot == 0) return;
+  const uint4 k = w.dict_key[s];
   unsigned long long i = atomicAdd(&w.ctl->w_n, 1ull);
   if (i < w.w_cap) w.w[i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, tot};
   else atomicOr(&w.ctl->overflow, OVF_W);
@@ -709,26 +932,25 @@ extern "C" __global__ void k_hist(Work w) {
   }
 }
 
-extern "C" __global__ void k_bucket_scan(Work w) {  // one workgroup of NB threads
-  __shared__ uint64_t bw[NB], r[NB];
+extern "C" __global__ __launch_bounds__(NB) void k_bucket_scan(Work w) {  // one workgroup of NB threads
+  __shared__ uint64_t wsum[16];
   const int b = threadIdx.x;
-  bw[b] = w.b_w[b];
-  r[b] = w.b_recs[b] + w.b_w[b];
-  __syncthreads();
+  const uint64_t nw = w.b_w[b], nr = w.b_recs[b];
+  uint64_t sw, sr, cold;
+  const uint64_t ow = block_exscan(nw, wsum, sw);
+  const uint64_t orr = block_exscan(nr + nw, wsum, sr);
+  (void)block_exscan(nr, wsum, cold);
+  w.w_off[b] = ow;
+  w.rec_off[b] = orr;
+  w.b_cur[b] = 0;
   if (b == 0) {
-    uint64_t sw = 0, sr = 0, cold = 0;
-    for (int i = 0; i < NB; i++) {
-      w.w_off[i] = sw; w.rec_off[i] = sr;
-      sw += bw[i]; sr += r[i];
-      cold += w.b_recs[i];
-    }
-    w.w_off[NB] = sw; w.rec_off[NB] = sr;
+    w.w_off[NB] = sw;
+    w.rec_off[NB] = sr;
     w.ctl->cold_recs = cold;
     if (sw > w.w_cap) atomicOr(&w.ctl->overflow, OVF_W);
     if (sr > w.uniq_cap) atomicOr(&w.ctl->overflow, OVF_POOL);
     w.ctl->w_total = sw;
   }
-  w.b_cur[b] = 0;
 }
 
 extern "C" __global__ void k_scatter(Work w) {
@@ -754,39 +976,37 @@ extern "C" __global__ void k_scatter(Work w) {
 }
 
 // ------------------------------------------------------------------ bucket reduce
-// One workgroup per partition: group its cold records (count 1, one contiguous
-// region per map workgroup) and weighted records by exact 16-byte key in an LDS
-// hash table, sort the distinct keys by (h32, key) with an LDS bitonic sort and
-// write them out.  A partition with more distinct keys than one table holds is
-// processed in 2^k sub-passes over the next hash bits; k comes from a
-// linear-counting estimate taken during pass 1.
-constexpr int RT2_SLOTS = 4608;
-constexpr int RT2_CAP = 3584;
-constexpr int LC_BITS = 32768;   // linear-counting bitmap
+// One workgroup per partition (2 per CU): group its cold records (count 1, one
+// contiguous region per map workgroup, streamed by one wave per region) and its
+// weighted records by exact 16-byte key in an LDS hash table, sort the distinct
+// keys by (h32, key) with an LDS bitonic sort and write them out.  A partition
+// with more distinct keys than the table holds is redone in 2^k sub-passes over
+// the next hash bits.
+constexpr int RED_SLOTS = 2560;
+constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort width
 constexpr int RED_UNROLL = 4;
 
 struct RedLds {
-  unsigned long long* k0;  // RT2_SLOTS (0 = free)
-  unsigned long long* k1;  // RT2_SLOTS
-  unsigned long long* cnt; // RT2_SLOTS (0 = not yet published)
-  uint32_t* hh;            // RT2_SLOTS key hash
-  uint16_t* idx;           // 4096
-  uint32_t* gpre;          // MAX_MAP_GRID + 1 prefix of region sizes
-  uint32_t* lc;            // LC_BITS / 32
-  uint32_t* misc;          // [0] uniques [1] overflow [2],[3] scratch
+  unsigned long long* k0;  // RED_SLOTS (0 = free)
+  unsigned long long* k1;  // RED_SLOTS
+  unsigned long long* cnt; // RED_SLOTS (0 = not yet published)
+  uint32_t* hh;            // RED_SLOTS key hash
+  uint16_t* idx;           // RED_CAP
+  uint32_t* misc;          // [0] uniques [1] overflow [2] compaction cursor
 };
 
 __device__ __forceinline__ uint32_t red_slot(uint32_t h) {
-  return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * RT2_SLOTS) >> 32);
+  return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * RED_SLOTS) >> 32);
 }
 
 // Exact insert.  A slot is claimed by CAS on k0 (short keys have a non-zero
 // first byte, so w0 != 0); the claimant then stores k1, hh and finally
-// publishes cnt (> 0).  Readers retry a slot whose cnt is still 0 -- no
-// spinning inside divergent code.
+// publishes cnt (> 0).  Readers retry a slot whose cnt is still 0: the
+// claimant's stores run in the same loop iteration, so no lane waits on a
+// lane that cannot make progress.
 __device__ __forceinline__ void red_insert(const RedLds& s, uint32_t h, uint64_t w0, uint64_t w1, uint64_t c) {
   uint32_t slot = red_slot(h);
-  for (uint32_t it = 0; it < (1u << 22); it++) {
+  for (uint32_t it = 0; it < 4 * RED_SLOTS; it++) {
     unsigned long long cur = s.k0[slot];
     if (cur == 0) {
       cur = atomicCAS(&s.k0[slot], 0ull, (unsigned long long)w0);
@@ -796,7 +1016,7 @@ __device__ __forceinline__ void red_insert(const RedLds& s, uint32_t h, uint64_t
         __threadfence_block();
         atomicAdd(&s.cnt[slot], (unsigned long long)c);
         const uint32_t u = atomicAdd(&s.misc[0], 1u);
-        if (u >= RT2_CAP) s.misc[1] = 1;
+        if (u >= RED_CAP) s.misc[1] = 1;
         return;
       }
     }
@@ -805,7 +1025,7 @@ __device__ __forceinline__ void red_insert(const RedLds& s, uint32_t h, uint64_t
       __threadfence_block();
       if (s.k1[slot] == w1) { atomicAdd(&s.cnt[slot], (unsigned long long)c); return; }
     }
-    slot = slot + 1 == RT2_SLOTS ? 0 : slot + 1;
+    slot = slot + 1 == RED_SLOTS ? 0 : slot + 1;
   }
   s.misc[1] = 1;
 }
@@ -822,19 +1042,18 @@ __device__ __forceinline__ bool in_sub(uint32_t h, uint32_t kk, uint32_t sub) {
   return kk == 0 || ((h << NB_LOG2) >> (32 - kk)) == sub;
 }
 
-extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
+extern "C" __global__ __launch_bounds__(RED_THREADS) void k_reduce(Work w) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   RedLds s;
   uint8_t* sp = smem;
-  s.k0 = (unsigned long long*)sp; sp += RT2_SLOTS * 8;
-  s.k1 = (unsigned long long*)sp; sp += RT2_SLOTS * 8;
-  s.cnt = (unsigned long long*)sp; sp += RT2_SLOTS * 8;
-  s.hh = (uint32_t*)sp; sp += RT2_SLOTS * 4;
-  s.idx = (uint16_t*)sp; sp += 4096 * 2;
-  s.gpre = (uint32_t*)sp; sp += (MAX_MAP_GRID + 4) * 4;
-  s.lc = (uint32_t*)sp; sp += LC_BITS / 8;
-  s.misc = (uint32_t*)sp; sp += 64;
-  const int tid = threadIdx.x;
+  s.k0 = (unsigned long long*)sp; sp += RED_SLOTS * 8;
+  s.k1 = (unsigned long long*)sp; sp += RED_SLOTS * 8;
+  s.cnt = (unsigned long long*)sp; sp += RED_SLOTS * 8;
+  s.hh = (uint32_t*)sp; sp += RED_SLOTS * 4;
+  s.idx = (uint16_t*)sp; sp += RED_CAP * 2;
+  s.misc = (uint32_t*)sp; sp += 16;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NWV = RED_THREADS / 64;
   const uint32_t b = blockIdx.x;
   const uint32_t G = w.map_grid;
   // an overflowed map or directory means this attempt is rerun with larger
@@ -845,98 +1064,58 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
   }
   const uint64_t ws0 = w.w_off[b], ws1 = w.w_off[b + 1];
   const uint64_t out0 = w.rec_off[b];
-  // prefix over map workgroups of this partition's region sizes
-  if (tid == 0) {
-    uint32_t acc = 0;
-    for (uint32_t g = 0; g < G; g++) { s.gpre[g] = acc; acc += w.cold_n[(uint64_t)g * NB + b]; }
-    s.gpre[G] = acc;
-  }
-  for (int i = tid; i < LC_BITS / 32; i += RED_THREADS) s.lc[i] = 0;
-  __syncthreads();
-  const uint32_t ncold = s.gpre[G];
   uint32_t kk = 0;
-  bool estimated = false;
   uint64_t written = 0;
   for (uint32_t sub = 0; sub < (1u << kk);) {
-    for (int i = tid; i < RT2_SLOTS; i += RED_THREADS) { s.k0[i] = 0; s.cnt[i] = 0; }
-    if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; }
+    for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { s.k0[i] = 0; s.cnt[i] = 0; }
+    if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
     __syncthreads();
-    const bool first = !estimated;
-    for (uint32_t i0 = 0; i0 < ncold; i0 += RED_THREADS * RED_UNROLL) {
-      uint4 v[RED_UNROLL];
-      bool ok[RED_UNROLL];
+    // cold regions: wave wv streams regions g = wv, wv + NWV, ...
+    for (uint32_t g = wv; g < G; g += NWV) {
+      const uint32_t n = w.cold_n[(uint64_t)g * NB + b];
+      const uint4* reg = w.cold + ((uint64_t)g * NB + b) * w.cold_cap;
+      for (uint32_t i0 = 0; i0 < n; i0 += 64 * RED_UNROLL) {
+        uint4 v[RED_UNROLL];
 #pragma unroll
-      for (int u = 0; u < RED_UNROLL; u++) {
-        const uint32_t i = i0 + u * RED_THREADS + tid;
-        ok[u] = i < ncold;
-        if (ok[u]) {
-          int a = 0, z = (int)G - 1;  // region g with gpre[g] <= i < gpre[g+1]
-          while (a < z) { const int mid = (a + z + 1) >> 1; if (s.gpre[mid] <= i) a = mid; else z = mid - 1; }
-          v[u] = w.cold[((uint64_t)a * NB + b) * w.cold_cap + (i - s.gpre[a])];
+        for (int u = 0; u < RED_UNROLL; u++) {
+          const uint32_t i = i0 + u * 64 + lane;
+          v[u] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
         }
-      }
-      const bool stop = __atomic_load_n(&s.misc[1], __ATOMIC_RELAXED) != 0;
+        if (__atomic_load_n(&s.misc[1], __ATOMIC_RELAXED)) break;  // this pass is redone anyway
 #pragma unroll
-      for (int u = 0; u < RED_UNROLL; u++) {
-        if (!ok[u]) continue;
-        const uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x, w1 = ((uint64_t)v[u].w << 32) | v[u].z;
-        const uint32_t h = key_hash(w0, w1);
-        if (first) { const uint32_t bit = (h * 0x85EBCA6Bu) >> 17; atomicOr(&s.lc[bit >> 5], 1u << (bit & 31)); }
-        if (!stop && in_sub(h, kk, sub)) red_insert(s, h, w0, w1, 1);
-      }
-      if (!first) {  // later passes: stop early on overflow (uniform decision)
-        __syncthreads();
-        const bool ovf = s.misc[1] != 0;
-        __syncthreads();
-        if (ovf) break;
+        for (int u = 0; u < RED_UNROLL; u++) {
+          if ((v[u].x | v[u].y) == 0) continue;
+          const uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x, w1 = ((uint64_t)v[u].w << 32) | v[u].z;
+          const uint32_t h = key_hash(w0, w1);
+          if (in_sub(h, kk, sub)) red_insert(s, h, w0, w1, 1);
+        }
       }
     }
     for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
       const WRec rr = w.w_sorted[i];
       const uint32_t h = key_hash(rr.w0, rr.w1);
-      if (first) { const uint32_t bit = (h * 0x85EBCA6Bu) >> 17; atomicOr(&s.lc[bit >> 5], 1u << (bit & 31)); }
       if (!__atomic_load_n(&s.misc[1], __ATOMIC_RELAXED) && in_sub(h, kk, sub)) red_insert(s, h, rr.w0, rr.w1, rr.count);
     }
     __syncthreads();
-    if (s.misc[1]) {
-      if (first) {  // too many distinct keys for one table: estimate them, then split
-        uint32_t z = 0;
-        for (int i = tid; i < LC_BITS / 32; i += RED_THREADS) z += 32 - __popc(s.lc[i]);
-        __syncthreads();
-        if (tid == 0) s.misc[2] = 0;
-        __syncthreads();
-        atomicAdd(&s.misc[2], z);
-        __syncthreads();
-        const double zf = s.misc[2] ? (double)s.misc[2] / LC_BITS : 0.5 / LC_BITS;
-        const double est = -(double)LC_BITS * log(zf);
-        uint32_t need = 1;
-        while ((double)(1u << need) * RT2_CAP < est * 1.25 && need < 20) need++;
-        kk = need;
-      } else {
-        kk++;
-      }
-      if (kk > 32 - NB_LOG2) {  // > RT2_CAP distinct keys share every hash bit: cannot split
+    if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the partition
+      kk++;
+      if (kk > 32 - NB_LOG2) {  // > RED_CAP distinct keys share every hash bit: cannot split
         if (tid == 0) { atomicOr(&w.ctl->overflow, OVF_REDUCE); w.b_uniq[b] = 0; }
         return;
       }
-      estimated = true;
       sub = 0;
       written = 0;
       __syncthreads();
       continue;
     }
-    estimated = true;
     // compact + bitonic sort by (h32, key) for a deterministic order
     const uint32_t nu = s.misc[0];
+    for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
+      if (s.cnt[i]) { const uint32_t p = atomicAdd(&s.misc[2], 1u); s.idx[p] = (uint16_t)i; }
     __syncthreads();
-    if (tid == 0) s.misc[3] = 0;
-    __syncthreads();
-    for (int i = tid; i < RT2_SLOTS; i += RED_THREADS)
-      if (s.cnt[i]) { const uint32_t p = atomicAdd(&s.misc[3], 1u); s.idx[p] = (uint16_t)i; }
-    __syncthreads();
-    for (int i = nu + tid; i < 4096; i += RED_THREADS) s.idx[i] = 0xFFFF;
     uint32_t N = 1;
     while (N < nu) N <<= 1;
+    for (uint32_t i = nu + tid; i < N; i += RED_THREADS) s.idx[i] = 0xFFFF;
     __syncthreads();
     for (uint32_t size = 2; size <= N; size <<= 1) {
       for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
@@ -966,8 +1145,6 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 1) void k_reduce(Work w) {
 }
 
 // ------------------------------------------------------------------ scans
-// Exclusive scan of v[0..n) (n = *n_ptr) into out[0..n], out[n] = total.
-// Three launches: per-WG totals, one-WG scan of totals, per-WG rescan + offset.
 extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint64_t* v, const unsigned long long* n_ptr,
                                                                       uint64_t n_const, uint64_t n_cap, uint64_t* part) {
   __shared__ uint64_t red[SCAN_THREADS / 64];
@@ -987,11 +1164,12 @@ extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const u
     part[blockIdx.x] = t;
   }
 }
-extern "C" __global__ void k_scan_parts(uint64_t* part, int nparts) {  // one thread is plenty
-  if (threadIdx.x || blockIdx.x) return;
-  uint64_t s = 0;
-  for (int i = 0; i < nparts; i++) { uint64_t x = part[i]; part[i] = s; s += x; }
-  part[nparts] = s;
+extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_parts(uint64_t* part, int nparts) {  // nparts == blockDim
+  __shared__ uint64_t wsum[16];
+  uint64_t tot;
+  const uint64_t ex = block_exscan(threadIdx.x < (unsigned)nparts ? part[threadIdx.x] : 0, wsum, tot);
+  if (threadIdx.x < (unsigned)nparts) part[threadIdx.x] = ex;
+  if (threadIdx.x == 0) part[nparts] = tot;
 }
 extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint64_t* v, const unsigned long long* n_ptr,
                                                                      uint64_t n_const, uint64_t n_cap, const uint64_t* part,
@@ -1040,15 +1218,17 @@ __device__ __forceinline__ uint32_t short_len(uint64_t w0, uint64_t w1) {
 }
 
 // After k_reduce: total short uniques + offsets; n_total = short + long.
-extern "C" __global__ void k_final_scan(Work w) {  // one workgroup of NB threads
+extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {  // one workgroup of NB threads
+  __shared__ uint64_t wsum[16];
+  uint64_t tot;
+  const uint64_t ex = block_exscan(w.b_uniq[threadIdx.x], wsum, tot);
+  w.uniq_off[threadIdx.x] = ex;
   if (threadIdx.x == 0) {
-    uint64_t s = 0;
-    for (int i = 0; i < NB; i++) { w.uniq_off[i] = s; s += w.b_uniq[i]; }
-    w.uniq_off[NB] = s;
-    w.ctl->n_short = s;
-    unsigned long long nl = w.ctl->long_uniq;
-    w.ctl->n_total = s + nl;
-    if (s + nl > w.table_cap) atomicOr(&w.ctl->overflow, OVF_TABLE);
+    w.uniq_off[NB] = tot;
+    w.ctl->n_short = tot;
+    const unsigned long long nl = w.ctl->long_uniq;
+    w.ctl->n_total = tot + nl;
+    if (tot + nl > w.table_cap) atomicOr(&w.ctl->overflow, OVF_TABLE);
   }
 }
 
