@@ -91,9 +91,10 @@ struct DevBuf {
 struct mox_engine {
   int device = 0;
   hipStream_t stream = nullptr;
-  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 128;
+  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 48;
   int n_cu = 256;
   bool sync_each = false;
+  uint64_t next_cold_cap = 0;  // region capacity learnt from spills of an earlier run
   Work w{};
   Tables tables{};
   Ctl* h_ctl = nullptr;       // pinned
@@ -138,7 +139,7 @@ Caps caps_of(const Work& w) {
 Caps initial_caps(uint64_t n, int map_grid) {
   Caps c;
   // cold records per (workgroup, partition) region: about one per 8 input bytes
-  c.cold_cap = std::max<uint64_t>(64, n / ((uint64_t)map_grid * NB * 12));
+  c.cold_cap = std::max<uint64_t>(64, n / ((uint64_t)map_grid * NB * 8));
   c.spill_cap = std::max<uint64_t>(1024, n / ((uint64_t)map_grid * 64));
   c.w_cap = 65536 + n / 64;
   c.u_cap = 4096 + n / 64;
@@ -256,7 +257,7 @@ int alloc_fixed(mox_engine* e) {
   return MOX_OK;
 }
 
-size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_BUCKETS * 4; }
+size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_BUCKETS * 4; }  // k_dict_build
 size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + MAP_WAVES * (ROWBUF + 2 * TOKMAX); }
 size_t reduce_lds_bytes() { return 2560 * (8 * 3 + 4) + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP (mox_kernels.hip)
 
@@ -319,11 +320,11 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   step("k_dict_totals");
   rec(3);
   // 4. shuffle directory + bucket reduce
-  hipLaunchKernelGGL(k_hist, dim3(512), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_hist, dim3(w.map_grid), dim3(1024), 0, s, w);
   step("k_hist");
   hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(NB), 0, s, w);
   step("k_bucket_scan");
-  hipLaunchKernelGGL(k_scatter, dim3(512), dim3(256), 0, s, w);
+  hipLaunchKernelGGL(k_scatter, dim3(w.map_grid), dim3(1024), 0, s, w);
   step("k_scatter");
   hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);
   step("k_reduce");
@@ -361,7 +362,9 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
 int run_corpus(mox_engine* e, const Corpus& c) {
   e->have_result = false;
   uint64_t n = c.own_hi - c.own_lo;
-  int rc = ensure_caps(e, initial_caps(n, e->n_cu));
+  Caps want = initial_caps(n, e->n_cu);
+  want.cold_cap = std::max<uint64_t>(want.cold_cap, e->next_cold_cap);
+  int rc = ensure_caps(e, want);
   if (rc) return rc;
   e->stats.retries = 0;
   for (int attempt = 0;; attempt++) {
@@ -398,6 +401,10 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     if ((rc = ensure_caps(e, need))) return rc;
   }
   const Ctl& h = *e->h_ctl;
+  // spills are correct but slow (atomic scatter): size the regions for the
+  // next run of this engine from what this one needed
+  // (applied at the start of the next run: the buffers hold this run's table)
+  if (h.spill_need) e->next_cold_cap = std::max<uint64_t>(e->next_cold_cap, h.cold_need + h.cold_need / 8 + 16);
   e->stats.bytes = n;
   e->stats.tokens = h.tokens;
   e->stats.uniques = h.n_total;

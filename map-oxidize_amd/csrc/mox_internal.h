@@ -18,7 +18,7 @@ constexpr int NB = 1 << NB_LOG2;
 constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
 constexpr int DICT_SLOTS = 4 * DICT_BUCKETS;
 constexpr int DICT_MAX_WORDS = 3584;
-constexpr int CAND_SLOTS = 6144;            // dictionary candidate table (LDS of k_dict_build)
+constexpr int CAND_SLOTS = 7168;            // dictionary candidate table (LDS of k_dict_build)
 constexpr int MAX_SAMPLE_PIECES = 256;
 constexpr int SAMPLE_OUT = 1024;            // candidates one sample piece hands to k_dict_build
 constexpr int SAMPLE_PIECE = 16 * 1024;     // one 1024-thread workgroup x 16 B

@@ -26,7 +26,11 @@ namespace mox {
 // ------------------------------------------------------------------ helpers
 // per-byte masks, valid only when every byte < 0x80 (ASCII fast path)
 __device__ __forceinline__ uint32_t movemask8(uint64_t m80) {  // m80: 0x80 per selected byte
-  return (uint32_t)((((m80 >> 7) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+  uint64_t m = (m80 >> 7) & 0x0101010101010101ull;  // bit 8i = byte i
+  m |= m >> 7;   // bits 0,1 | 16,17 | 32,33 | 48,49
+  m |= m >> 14;  // bits 0..3 | 32..35
+  m |= m >> 28;  // bits 0..7
+  return (uint32_t)m & 0xFFu;
 }
 __device__ __forceinline__ uint64_t zero_bytes80(uint64_t v) {  // exact: 0x80 where byte == 0
   uint64_t t = (v & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
@@ -387,26 +391,114 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
   return st;
 }
 
+// Token phase for TU batches of 64 tokens (lane = token): key from the LDS row
+// (three 8-byte reads at the 8-aligned start, funnel shift), hash, dictionary
+// tags of both buckets, key check, then LDS count or cold emission.
+template <int TU>
+__device__ __forceinline__ void token_batches(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
+                                              uint32_t total, bool use_dict) {
+  const int lane = threadIdx.x & 63;
+  uint32_t e[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const uint32_t j = j0 + u * 64 + lane;
+    e[u] = j < total ? (uint32_t)list[j] : 0x8000u;  // inactive = odd
+  }
+  uint64_t w0[TU], w1[TU];
+  uint32_t h[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const uint32_t pos = e[u] & 1023u, len = (e[u] >> 10) & 31u;
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(rowbuf + (pos & ~7u));
+    const uint64_t Q0 = q[0], Q1 = q[1], Q2 = q[2];
+    const uint32_t r = (pos & 7u) * 8u;
+    uint64_t a0 = (Q0 >> r) | ((Q1 << 1) << (63u - r));
+    uint64_t a1 = (Q1 >> r) | ((Q2 << 1) << (63u - r));
+    const uint64_t m0 = len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1ull);
+    const uint64_t m1 = len <= 8 ? 0ull : (len >= 16 ? ~0ull : ((1ull << (8 * (len - 8))) - 1ull));
+    a0 &= m0;
+    a1 &= m1;
+    w0[u] = a0;
+    w1[u] = a1;
+    h[u] = key_hash(a0, a1);
+  }
+  int slot[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    slot[u] = -1;
+    if (use_dict) {
+      const uint32_t b1 = dict_b1(h[u]), b2 = dict_b2(h[u]);
+      const uint4 t1 = m.s.dtag4[b1], t2 = m.s.dtag4[b2];
+      int sl = t2.w == h[u] ? (int)(4 * b2 + 3) : -1;
+      sl = t2.z == h[u] ? (int)(4 * b2 + 2) : sl;
+      sl = t2.y == h[u] ? (int)(4 * b2 + 1) : sl;
+      sl = t2.x == h[u] ? (int)(4 * b2 + 0) : sl;
+      sl = t1.w == h[u] ? (int)(4 * b1 + 3) : sl;
+      sl = t1.z == h[u] ? (int)(4 * b1 + 2) : sl;
+      sl = t1.y == h[u] ? (int)(4 * b1 + 1) : sl;
+      sl = t1.x == h[u] ? (int)(4 * b1 + 0) : sl;
+      slot[u] = sl;
+    }
+  }
+  bool hit[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const uint4 kq = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
+    hit[u] = slot[u] >= 0 && key_eq(kq, w0[u], w1[u]);
+  }
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    if (e[u] & 0x8000u) continue;
+    if (hit[u]) {
+      if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
+      continue;
+    }
+    if (slot[u] >= 0) {  // tag matched another word: full search (rare)
+      const int s2 = dict_find(m.s, h[u], w0[u], w1[u]);
+      if (s2 >= 0) { atomicAdd(&m.s.dcnt[s2], 1u); continue; }
+    }
+    cold_word(m, h[u], w0[u], w1[u]);
+  }
+}
+
 // One row (64 lanes x 16 B) in two phases:
 //  1. byte phase (lane = 16 B): token-start bit masks (SWAR on ASCII rows, the
 //     Unicode walk on rows with non-ASCII bytes), the lowered row into LDS and a
 //     compacted list of token (start, length) in row order (wave prefix sum of
 //     per-lane start counts from 5 bit-sliced ballots);
-//  2. token phase (lane = token): 64 tokens per step read their key from the
-//     LDS row, hash it and count it in the dictionary or emit it.
-constexpr int TU = 4;  // token batches per lane in flight
-
-__device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, uint4 bn, uint32_t prev,
+//  2. token phase (lane = token), see token_batches.
+// nxt = the next row's first 16 bytes (wave-uniform), prev_last = the byte
+// before the row (wave-uniform).
+__device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, uint4 nxt, uint32_t prev_last,
                                        unsigned long long& ntok, uint8_t* rowbuf, uint16_t* list) {
   const int lane = threadIdx.x & 63;
-  const bool slow = __any(nonascii16(a) | nonascii16(bn) | (prev & 0x80u));
+  const uint64_t rowbase = p0 - (uint64_t)lane * 16;
+  const bool slow = __any(nonascii16(a) != 0) || nonascii16(nxt) != 0 || (prev_last & 0x80u) != 0;
   uint32_t ws32 = 0, z32 = 0, start;
+  bool chk = false;  // rows with NUL bytes or near a non-final buffer end need the odd checks
+  uint32_t lim = 64;
   if (!slow) {
-    ws32 = ws_mask16(a) | (ws_mask16(bn) << 16);
-    z32 = zero_mask16(a) | (zero_mask16(bn) << 16);
-    start = (~ws32) & ((ws32 << 1) | (is_ascii_ws(prev) ? 1u : 0u)) & 0xFFFFu;
-    if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
-    if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
+    const uint64_t L = ((uint64_t)a.y << 32) | a.x, H = ((uint64_t)a.w << 32) | a.z;
+    const uint32_t ws16 = movemask8(ws_bytes80(L)) | (movemask8(ws_bytes80(H)) << 8);
+    const uint32_t wsn = __shfl_down(ws16, 1);
+    const uint32_t wsp = __shfl_up(ws16, 1);
+    const uint32_t ws_nxt = ws_mask16(nxt);
+    ws32 = ws16 | ((lane == 63 ? ws_nxt : wsn) << 16);
+    const uint32_t prevws = lane == 0 ? (is_ascii_ws(prev_last) ? 1u : 0u) : (wsp >> 15) & 1u;
+    start = (~ws32) & ((ws32 << 1) | prevws) & 0xFFFFu;
+    if (rowbase < m.c.own_lo || rowbase + ROW > m.c.own_hi) {
+      if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
+      if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
+    }
+    const bool anyz = __any((zero_bytes80(L) | zero_bytes80(H)) != 0) || zero_mask16(nxt) != 0;
+    if (anyz) {
+      const uint32_t z16 = zero_mask16(a);
+      const uint32_t zn = __shfl_down(z16, 1);
+      z32 = z16 | ((lane == 63 ? zero_mask16(nxt) : zn) << 16);
+    }
+    const bool near_end = !m.c.at_end && rowbase + ROW + 32 >= m.c.hi;
+    if (near_end) lim = m.c.hi > p0 ? (uint32_t)(m.c.hi - p0 < 64 ? m.c.hi - p0 : 64) : 0u;
+    chk = anyz || near_end;
   } else {
     start = slow_starts(m, p0);
   }
@@ -424,22 +516,21 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, ui
   }
   if (total == 0) return;
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
-  if (lane == 63) reinterpret_cast<uint4*>(rowbuf)[64] = lower16(bn);
+  if (lane == 63) reinterpret_cast<uint4*>(rowbuf)[64] = lower16(nxt);
   // list entry (u16): start in row (10 bits) | length (5 bits, <= 16) | odd (bit 15)
   uint32_t k = pre;
   bool any_odd = false;
   while (start) {
-    const int p = __builtin_ctz(start);
+    const uint32_t p = __builtin_ctz(start);
     start &= start - 1;
     const uint32_t rest = ws32 >> p;
-    const int len = rest ? __builtin_ctz(rest) : 32;
-    const bool odd = slow || rest == 0 || len > 16 || (p0 + p + len >= m.c.hi && !m.c.at_end) ||
-                     ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
+    const uint32_t len = rest ? __builtin_ctz(rest) : 32;
+    bool odd = slow || len > 16;
+    if (chk) odd = odd || p + len >= lim || ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
     any_odd |= odd;
-    list[k++] = (uint16_t)((uint32_t)(lane * 16 + p) | (odd ? 0x8000u : ((uint32_t)len << 10)));
+    list[k++] = (uint16_t)((uint32_t)(lane * 16) + p + (odd ? 0x8000u : (len << 10)));
   }
   wave_lds_fence();
-  const uint64_t rowbase = p0 - (uint64_t)lane * 16;
   if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
     for (uint32_t j = lane; j < total; j += 64) {
       const uint32_t e = list[j];
@@ -447,71 +538,13 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, ui
     }
   }
   if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
-  // fast tokens, TU batches of 64 in flight per lane (independent LDS chains)
-  const uint4* rb4 = reinterpret_cast<const uint4*>(rowbuf);
   const bool use_dict = m.dict_n && !(m.w.dbg & DBG_NO_DICT);
-  for (uint32_t j0 = 0; j0 < total; j0 += 64 * TU) {
-    uint32_t e[TU];
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      const uint32_t j = j0 + u * 64 + lane;
-      e[u] = j < total ? (uint32_t)list[j] : 0x8000u;  // inactive = odd
-    }
-    uint64_t w0[TU], w1[TU];
-    uint32_t h[TU];
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      const uint32_t pos = e[u] & 1023u, len = (e[u] >> 10) & 31u;
-      const uint4 x = rb4[pos >> 4], y = rb4[(pos >> 4) + 1];
-      const uint64_t W0 = ((uint64_t)x.y << 32) | x.x, W1 = ((uint64_t)x.w << 32) | x.z;
-      const uint64_t W2 = ((uint64_t)y.y << 32) | y.x, W3 = ((uint64_t)y.w << 32) | y.z;
-      const int kk = (pos >> 3) & 1, r = (pos & 7) * 8;
-      const uint64_t A = kk ? W1 : W0, B = kk ? W2 : W1, C = kk ? W3 : W2;
-      uint64_t a0 = r ? (A >> r) | (B << (64 - r)) : A;
-      uint64_t a1 = r ? (B >> r) | (C << (64 - r)) : B;
-      if (len <= 8) { a0 &= lo_mask((int)len); a1 = 0; }
-      else a1 &= lo_mask((int)len - 8);
-      w0[u] = a0;
-      w1[u] = a1;
-      h[u] = key_hash(a0, a1);
-    }
-    int slot[TU];
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      slot[u] = -1;
-      if (use_dict) {
-        const uint32_t b1 = dict_b1(h[u]), b2 = dict_b2(h[u]);
-        const uint4 t1 = m.s.dtag4[b1], t2 = m.s.dtag4[b2];
-        int sl = t2.w == h[u] ? (int)(4 * b2 + 3) : -1;
-        sl = t2.z == h[u] ? (int)(4 * b2 + 2) : sl;
-        sl = t2.y == h[u] ? (int)(4 * b2 + 1) : sl;
-        sl = t2.x == h[u] ? (int)(4 * b2 + 0) : sl;
-        sl = t1.w == h[u] ? (int)(4 * b1 + 3) : sl;
-        sl = t1.z == h[u] ? (int)(4 * b1 + 2) : sl;
-        sl = t1.y == h[u] ? (int)(4 * b1 + 1) : sl;
-        sl = t1.x == h[u] ? (int)(4 * b1 + 0) : sl;
-        slot[u] = sl;
-      }
-    }
-    bool hit[TU];
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      const uint4 kq = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
-      hit[u] = slot[u] >= 0 && key_eq(kq, w0[u], w1[u]);
-    }
-#pragma unroll
-    for (int u = 0; u < TU; u++) {
-      if (e[u] & 0x8000u) continue;
-      if (hit[u]) {
-        if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
-        continue;
-      }
-      if (slot[u] >= 0) {  // tag matched another word: full search (rare)
-        const int s2 = dict_find(m.s, h[u], w0[u], w1[u]);
-        if (s2 >= 0) { atomicAdd(&m.s.dcnt[s2], 1u); continue; }
-      }
-      cold_word(m, h[u], w0[u], w1[u]);
-    }
+  for (uint32_t j0 = 0; j0 < total;) {
+    const uint32_t rem = total - j0;
+    if (rem > 192) { token_batches<4>(m, rowbuf, list, j0, total, use_dict); j0 += 256; }
+    else if (rem > 128) { token_batches<3>(m, rowbuf, list, j0, total, use_dict); j0 += 192; }
+    else if (rem > 64) { token_batches<2>(m, rowbuf, list, j0, total, use_dict); j0 += 128; }
+    else { token_batches<1>(m, rowbuf, list, j0, total, use_dict); j0 += 64; }
   }
   wave_lds_fence();
 }
@@ -575,13 +608,9 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
         a = fix16(c, p0, a);
         nx = fix16(c, rs + ROW + lane * 16, nx);
       }
-      uint4 bn = shfl_down1(a);
       const uint4 nxt = lane0(nx);  // look-ahead: the next row's first 16 bytes
-      if (lane == 63) bn = nxt;
-      const uint32_t up = __shfl_up(a.w >> 24, 1);
-      const uint32_t prev = lane == 0 ? prev_last : up;
-      do_row(m, p0, a, bn, prev, ntok, rowbuf, list);
-      prev_last = __shfl(a.w >> 24, 63);
+      do_row(m, p0, a, nxt, prev_last, ntok, rowbuf, list);
+      prev_last = __builtin_amdgcn_readlane(a.w >> 24, 63);
     }
   }
   __syncthreads();
@@ -902,34 +931,30 @@ extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
 // ------------------------------------------------------------------ shuffle directory
 // Records per partition: cold regions (map workgroup x partition) and weighted
 // records (dictionary totals, Unicode-lane words, map spills).
-extern "C" __global__ void k_hist(Work w) {
+// Workgroup g (one per map workgroup) adds map workgroup g's region sizes and
+// spills, and a grid-strided share of the weighted records.
+extern "C" __global__ __launch_bounds__(1024) void k_hist(Work w) {
   __shared__ uint32_t hw[NB];
-  __shared__ unsigned long long hr[NB];
-  for (int i = threadIdx.x; i < NB; i += blockDim.x) { hw[i] = 0; hr[i] = 0; }
+  const uint32_t g = blockIdx.x;
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) hw[i] = 0;
   __syncthreads();
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t ncell = (uint64_t)w.map_grid * NB;
-  for (uint64_t i = gtid; i < ncell; i += stride) {
-    const uint32_t n = w.cold_n[i];
-    if (n) atomicAdd(&hr[i % NB], (unsigned long long)n);
+  for (int i = threadIdx.x; i < NB; i += blockDim.x) {
+    const uint32_t n = w.cold_n[(uint64_t)g * NB + i];
+    if (n) atomicAdd((unsigned long long*)&w.b_recs[i], (unsigned long long)n);
   }
   uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
-  for (uint64_t i = gtid; i < nw; i += stride) {
+  for (uint64_t i = (uint64_t)g * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
     const WRec r = w.w[i];
     atomicAdd(&hw[bucket_of(key_hash(r.w0, r.w1))], 1u);
   }
-  const uint64_t nsp = (uint64_t)w.map_grid * w.spill_cap;
-  for (uint64_t i = gtid; i < nsp; i += stride) {
-    if (i % w.spill_cap >= w.spill_n[i / w.spill_cap]) continue;
-    const uint4 k = w.spill[i];
+  const uint32_t ns = w.spill_n[g];
+  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
+    const uint4 k = w.spill[(uint64_t)g * w.spill_cap + i];
     atomicAdd(&hw[bucket_of(key_hash(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z))], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NB; i += blockDim.x) {
-    if (hr[i]) atomicAdd((unsigned long long*)&w.b_recs[i], hr[i]);
+  for (int i = threadIdx.x; i < NB; i += blockDim.x)
     if (hw[i]) atomicAdd(&w.b_w[i], hw[i]);
-  }
 }
 
 extern "C" __global__ __launch_bounds__(NB) void k_bucket_scan(Work w) {  // one workgroup of NB threads
@@ -953,21 +978,19 @@ extern "C" __global__ __launch_bounds__(NB) void k_bucket_scan(Work w) {  // one
   }
 }
 
-extern "C" __global__ void k_scatter(Work w) {
+extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {  // same mapping as k_hist
   if (w.ctl->w_total > w.w_cap) return;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint64_t gtid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t g = blockIdx.x;
   uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
-  for (uint64_t i = gtid; i < nw; i += stride) {
+  for (uint64_t i = (uint64_t)g * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
     const WRec r = w.w[i];
     const uint32_t b = bucket_of(key_hash(r.w0, r.w1));
     const uint32_t k = atomicAdd(&w.b_cur[b], 1u);
     w.w_sorted[w.w_off[b] + k] = r;
   }
-  const uint64_t nsp = (uint64_t)w.map_grid * w.spill_cap;
-  for (uint64_t i = gtid; i < nsp; i += stride) {
-    if (i % w.spill_cap >= w.spill_n[i / w.spill_cap]) continue;
-    const uint4 k = w.spill[i];
+  const uint32_t ns = w.spill_n[g];
+  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
+    const uint4 k = w.spill[(uint64_t)g * w.spill_cap + i];
     const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
     const uint32_t b = bucket_of(key_hash(w0, w1));
     const uint32_t j = atomicAdd(&w.b_cur[b], 1u);
