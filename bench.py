@@ -31,6 +31,7 @@ import numpy as np  # noqa: E402
 
 import mox  # noqa: E402
 from mox import corpus  # noqa: E402
+from mox import dist as mdist  # noqa: E402
 
 METRIC = "word-count input GB/s end-to-end at 1 and 8 MI355X; % of HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -52,9 +53,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
     ap.add_argument("--bytes-per-gpu", type=int, default=0, help="override the shard size")
-    ap.add_argument("--cpu-sample-mib", type=int, default=512)
+    ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dict", action="store_true")
+    ap.add_argument("--xport", default="rccl", choices=["rccl", "host"],
+                    help="exchange transport for N > 1 (host: gloo-staged, for ranks sharing one GPU)")
+    ap.add_argument("--device", type=int, default=-1, help="override the GPU (default LOCAL_RANK)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_map.json"),
                     help="PMC summary of the map kernel (tools/pmc_traffic.py) to report as roofline.traffic")
     return ap.parse_args()
@@ -104,28 +108,28 @@ def main():
     if a.bytes_per_gpu:
         per_rank = a.bytes_per_gpu
     total = per_rank * world
-    own_b = rank * per_rank
-    own_e = own_b + per_rank
-    lo = max(0, own_b - 64)
-    hi = min(total, own_e + HALO) if world > 1 else own_e
-    at_end = hi == total
+    lo, hi, own_b, own_e, at_end = mdist.shard_range(total, world, rank, per_rank=per_rank, halo=HALO)
 
-    eng = mox.Engine(device=local, flags=mox.MOX_F_TIMING | (mox.MOX_F_NO_DICT if a.no_dict else 0),
+    eng = mox.Engine(device=local if a.device < 0 else a.device, flags=mox.MOX_F_TIMING | (mox.MOX_F_NO_DICT if a.no_dict else 0),
                      reserve_bytes=per_rank)
     host = corpus.fill(kind, seed, lo, hi - lo)
     d_buf = eng.alloc(hi - lo)
     eng.h2d(d_buf, host)
     del host
-    if world > 1:
+    if world > 1 and a.xport == "rccl":
         uid = mox.comm_unique_id() if rank == 0 else b""
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
+    a2a = mdist.gloo_alltoallv() if world > 1 and a.xport == "host" else None
 
     def step():
-        eng.run_range(d_buf, hi - lo, own_b - lo, own_e - lo, at_end)
+        eng.run_range(d_buf, hi - lo, own_b, own_e, at_end)
         if world > 1:
-            eng.exchange()
+            if a2a:
+                eng.exchange_host(world, rank, a2a)
+            else:
+                eng.exchange()
 
     for _ in range(a.warmup):
         step()
@@ -152,8 +156,16 @@ def main():
     last = eng.stats()
     t = eng.fetch()
     counts, _, _ = t.arrays()
-    ok = int(counts.sum()) == t.tokens if world == 1 else True
+    ok = int(counts.sum()) == t.tokens
     t.close()
+    if dist:  # after the exchange every rank owns disjoint words: tokens add up to the whole corpus
+        import torch
+        tk = torch.tensor([last["tokens"], int(ok)], dtype=torch.float64)
+        dist.all_reduce(tk)
+        tokens_all = int(tk[0].item())
+        ok = int(tk[1].item()) == world
+    else:
+        tokens_all = last["tokens"]
 
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
@@ -181,8 +193,9 @@ def main():
             "data": "synthetic: mox_corpus kind=%d seed=%#x (Zipf(1.1) English-like text, host-generated, "
                     "copied to HBM before timing)" % (kind, seed),
             "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
-                       "parallelism": "dp%d byte-range shards%s" % (world, " + RCCL all-to-all" if world > 1 else "")},
-            "words_per_s": round(last["tokens"] * world / (elapsed / a.steps), 1),
+                       "parallelism": "dp%d byte-range shards%s" % (
+                           world, (" + %s all-to-all" % ("RCCL" if a.xport == "rccl" else "host/gloo")) if world > 1 else "")},
+            "words_per_s": round(tokens_all / (elapsed / a.steps), 1),
             "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * world), 2),
             "roofline": {
                 "kernel": "k_map",

@@ -142,6 +142,14 @@ int mox_comm_init(mox_engine* e, int nranks, int rank, const uint8_t id[MOX_UNIQ
  * it with one RCCL all-to-all, and reduce the received partials.  Afterwards
  * this rank owns the final counts of its hash range (disjoint across ranks). */
 int mox_exchange(mox_engine* e);
+/* Host-staged transport for the same exchange (several ranks sharing one GPU,
+ * or no RCCL): the library calls fn once per all-to-all with pinned host
+ * buffers; send holds nranks consecutive blocks of send_bytes[d] bytes for
+ * rank d, recv must receive nranks consecutive blocks of recv_bytes[s] bytes
+ * from rank s.  Return 0 on success. */
+typedef int (*mox_alltoallv_fn)(void* user, const void* send, const uint64_t* send_bytes, void* recv,
+                                const uint64_t* recv_bytes);
+int mox_exchange_host(mox_engine* e, int nranks, int rank, mox_alltoallv_fn fn, void* user);
 
 /* ---- output layer (reference L5: main.rs:170-192) ---- */
 /* final_result.txt: one "{word} {count}\n" line per word.  Truncates on open

@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -47,6 +48,10 @@ __global__ void k_final_scan(Work w);
 __global__ void k_mat_counts(Work w, uint64_t* lens);
 __global__ void k_mat_long(Work w, uint64_t* lens);
 __global__ void k_mat_bytes(Work w, Corpus c);
+__global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
+__global__ void k_xpack_short(Work w, WRec* out);
+__global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob);
+__global__ void k_xingest(Work w, XDir dir, uint64_t n_short);
 }
 
 namespace {
@@ -112,6 +117,12 @@ struct mox_engine {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  XCnt* d_xcnt = nullptr;                 // [0, MAX_RANKS) sent, [MAX_RANKS, 2 MAX_RANKS) received
+  XCnt* h_xcnt = nullptr;                 // pinned mirror
+  unsigned long long* d_xcur = nullptr;   // 2 MAX_RANKS pack cursors
+  DevBuf x_send_short, x_send_blob, x_recv_short, x_recv_blob;  // device
+  DevBuf hx_send, hx_recv;                // pinned host staging (host transport)
+  Ctl* h_ctl_x = nullptr;                 // pinned control block of an exchange pass
   std::vector<DevBuf> owned;  // allocations to free
 };
 
@@ -278,77 +289,62 @@ float ev_ms(mox_engine* e, int a, int b) {
   return ms;
 }
 
-// One attempt of the whole device pipeline.  Returns MOX_OK after the control
-// block has been read back into e->h_ctl (caller inspects overflow / errors).
-int pipeline_once(mox_engine* e, const Corpus& c) {
-  Work& w = e->w;
-  hipStream_t s = e->stream;
-  const bool timing = (e->flags & MOX_F_TIMING) != 0;
-  auto rec = [&](int i) {
+// Launch sequencing helpers: HIP-event timestamps (MOX_F_TIMING) and, with
+// MOX_SYNC_EACH=1, a synchronisation + name after every launch (hang / fault
+// triage).
+struct Seq {
+  mox_engine* e;
+  hipStream_t s;
+  bool timing, sync_each;
+  void rec(int i) const {
     if (timing) (void)hipEventRecord(e->ev[i], s);
-  };
-  // MOX_SYNC_EACH=1: synchronise after every launch and name it (hang / fault triage)
-  auto step = [&](const char* name) {
-    if (!e->sync_each) return;
+  }
+  void step(const char* name) const {
+    if (!sync_each) return;
     hipError_t er = hipStreamSynchronize(s);
     fprintf(stderr, "[mox] %s done: %s\n", name, hipGetErrorString(er));
-  };
-  rec(0);
-  HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_init, sizeof(Ctl), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
-  HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
-  // 1. hot dictionary from a sample
-  if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
-    HIPCHK(hipMemsetAsync(w.dict_tot, 0, DICT_SLOTS * 8, s));
-    hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
-  step("k_sample");
-    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), dict_lds_bytes(), s, w, e->dict_words, e->sample_pieces);
-  step("k_dict_build");
   }
-  rec(1);
-  // 2. map: one streaming pass over the corpus
-  const uint64_t row0 = c.own_lo & ~15ull;
-  const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + 1023) / 1024 : 0;
-  const int grid = (int)w.map_grid;
-  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows);
-  step("k_map");
-  rec(2);
-  // 3. lanes
-  hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
-  step("k_unicode");
-  hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w);
-  step("k_dict_totals");
-  rec(3);
-  // 4. shuffle directory + bucket reduce
+};
+
+Seq seq_of(mox_engine* e) { return Seq{e, e->stream, (e->flags & MOX_F_TIMING) != 0, e->sync_each}; }
+
+// Stages 4-5 of a pass (shared by the corpus pass and the exchange pass):
+// shuffle directory + bucket reduce, then the dense table.
+void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
+  Work& w = e->w;
+  hipStream_t s = e->stream;
   hipLaunchKernelGGL(k_hist, dim3(w.map_grid), dim3(1024), 0, s, w);
-  step("k_hist");
+  q.step("k_hist");
   hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(NB), 0, s, w);
-  step("k_bucket_scan");
+  q.step("k_bucket_scan");
   hipLaunchKernelGGL(k_scatter, dim3(w.map_grid), dim3(1024), 0, s, w);
-  step("k_scatter");
+  q.step("k_scatter");
   hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);
-  step("k_reduce");
-  rec(4);
-  // 5. table
+  q.step("k_reduce");
+  q.rec(4);
   hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(NB), 0, s, w);
-  step("k_final_scan");
+  q.step("k_final_scan");
   hipLaunchKernelGGL(k_long_flags, dim3(256), dim3(256), 0, s, w, e->d_lens);
-  step("k_long_flags");
+  q.step("k_long_flags");
   launch_scan(e, e->d_lens, nullptr, w.long_cap, w.long_cap, w.lpos);
-  step("scan_long");
+  q.step("scan_long");
   hipLaunchKernelGGL(k_mat_counts, dim3(1024), dim3(256), 0, s, w, e->d_lens);
-  step("k_mat_counts");
+  q.step("k_mat_counts");
   hipLaunchKernelGGL(k_mat_long, dim3(256), dim3(256), 0, s, w, e->d_lens);
-  step("k_mat_long");
+  q.step("k_mat_long");
   launch_scan(e, e->d_lens, &w.ctl->n_total, 0, w.table_cap, w.t_offs);
-  step("scan_offs");
+  q.step("scan_offs");
   hipLaunchKernelGGL(k_mat_bytes, dim3(1024), dim3(256), 0, s, w, c);
-  step("k_mat_bytes");
-  rec(5);
+  q.step("k_mat_bytes");
+  q.rec(5);
+}
+
+// Read the control block back and collect the phase timings.
+int finish_pass(mox_engine* e, const Seq& q) {
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(e->h_ctl, w.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
-  if (timing) {
+  HIPCHK(hipMemcpyAsync(e->h_ctl, e->w.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (q.timing) {
     e->stats.ms_dict = ev_ms(e, 0, 1);
     e->stats.ms_map = ev_ms(e, 1, 2);
     e->stats.ms_lanes = ev_ms(e, 2, 3);
@@ -357,6 +353,64 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
     e->stats.ms_run = ev_ms(e, 0, 5);
   }
   return MOX_OK;
+}
+
+// One attempt of the whole device pipeline.  Returns MOX_OK after the control
+// block has been read back into e->h_ctl (caller inspects overflow / errors).
+int pipeline_once(mox_engine* e, const Corpus& c) {
+  Work& w = e->w;
+  hipStream_t s = e->stream;
+  const Seq q = seq_of(e);
+  q.rec(0);
+  HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_init, sizeof(Ctl), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
+  HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
+  // 1. hot dictionary from a sample
+  if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
+    HIPCHK(hipMemsetAsync(w.dict_tot, 0, DICT_SLOTS * 8, s));
+    hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
+    q.step("k_sample");
+    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), dict_lds_bytes(), s, w, e->dict_words, e->sample_pieces);
+    q.step("k_dict_build");
+  }
+  q.rec(1);
+  // 2. map: one streaming pass over the corpus
+  const uint64_t row0 = c.own_lo & ~15ull;
+  const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + 1023) / 1024 : 0;
+  const int grid = (int)w.map_grid;
+  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows);
+  q.step("k_map");
+  q.rec(2);
+  // 3. lanes
+  hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
+  q.step("k_unicode");
+  hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w);
+  q.step("k_dict_totals");
+  q.rec(3);
+  // 4-5. shuffle directory + bucket reduce, table
+  launch_reduce_tail(e, c, q);
+  return finish_pass(e, q);
+}
+
+// Capacities that cover what an overflowed attempt asked for.
+Caps grow_for(mox_engine* e, const Ctl& h) {
+  Caps need = caps_of(e->w);
+  if (h.overflow & OVF_POOL) {
+    need.cold_cap = std::max<uint64_t>(need.cold_cap, h.cold_need + h.cold_need / 8 + 16);
+    need.spill_cap = std::max<uint64_t>(need.spill_cap, h.spill_need + h.spill_need / 4 + 1024);
+  }
+  if (h.overflow & OVF_W) {
+    const uint64_t wn = std::max<uint64_t>(h.w_total, h.w_n);
+    need.w_cap = std::max<uint64_t>(need.w_cap, wn + wn / 4 + 1024);
+  }
+  if (h.overflow & OVF_U) need.u_cap = h.u_n + h.u_n / 4 + 1024;
+  if (h.overflow & OVF_ARENA) need.arena_cap = h.arena_n + h.arena_n / 4 + 65536;
+  if (h.overflow & OVF_LONG) need.long_cap = next_pow2(2 * h.long_n + 1024);
+  if (h.overflow & OVF_TABLE) need.table_cap = h.n_total + h.n_total / 4 + 1024;
+  if (h.overflow & OVF_BYTES) need.bytes_cap = h.bytes_total + h.bytes_total / 4 + 65536;
+  // a table overflow also means the byte estimate is stale
+  if (h.overflow & OVF_TABLE) need.bytes_cap = std::max(need.bytes_cap, need.table_cap * 16);
+  return need;
 }
 
 int run_corpus(mox_engine* e, const Corpus& c) {
@@ -381,22 +435,7 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     if (h.overflow & OVF_REDUCE)
       return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
     if (attempt >= 4) return fail(MOX_ENOMEM, "buffer growth did not converge (overflow mask 0x%x)", h.overflow);
-    Caps need = caps_of(e->w);
-    if (h.overflow & OVF_POOL) {
-      need.cold_cap = std::max<uint64_t>(need.cold_cap, h.cold_need + h.cold_need / 8 + 16);
-      need.spill_cap = std::max<uint64_t>(need.spill_cap, h.spill_need + h.spill_need / 4 + 1024);
-    }
-    if (h.overflow & OVF_W) {
-      const uint64_t wn = std::max<uint64_t>(h.w_total, h.w_n);
-      need.w_cap = std::max<uint64_t>(need.w_cap, wn + wn / 4 + 1024);
-    }
-    if (h.overflow & OVF_U) need.u_cap = h.u_n + h.u_n / 4 + 1024;
-    if (h.overflow & OVF_ARENA) need.arena_cap = h.arena_n + h.arena_n / 4 + 65536;
-    if (h.overflow & OVF_LONG) need.long_cap = next_pow2(2 * h.long_n + 1024);
-    if (h.overflow & OVF_TABLE) need.table_cap = h.n_total + h.n_total / 4 + 1024;
-    if (h.overflow & OVF_BYTES) need.bytes_cap = h.bytes_total + h.bytes_total / 4 + 65536;
-    // a table overflow also means the byte estimate is stale
-    if (h.overflow & OVF_TABLE) need.bytes_cap = std::max(need.bytes_cap, need.table_cap * 16);
+    Caps need = grow_for(e, h);
     e->stats.retries++;
     if ((rc = ensure_caps(e, need))) return rc;
   }
@@ -432,6 +471,234 @@ Corpus make_corpus(const void* d_buf, size_t buf_len, size_t own_begin, size_t o
   c.ctx_lo = mis;
   c.at_end = at_end ? 1 : 0;
   return c;
+}
+
+
+// ============================================================== multi-GPU exchange
+//   After a local pass every rank holds a dense table of its
+// byte range.  Each table row goes to the owner of its hash (short words:
+// partition ranges, already contiguous per owner in the dense order; long
+// words: FNV hash ranges, packed per owner).  The exchange is three
+// all-to-alls (per-peer counts, short records, long blobs) over a transport,
+// then one reduce-only pass over the received partials produces this rank's
+// final table.  Ranks own disjoint word sets.
+
+int grow_dev(DevBuf& b, size_t bytes) {
+  if (b.cap >= bytes && b.p) return MOX_OK;
+  dfree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+  hipError_t err = hipMalloc(&b.p, want);
+  if (err != hipSuccess) return fail(MOX_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(err));
+  b.cap = want;
+  return MOX_OK;
+}
+int grow_pinned(DevBuf& b, size_t bytes) {
+  if (b.cap >= bytes && b.p) return MOX_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
+  hipError_t err = hipHostMalloc(&b.p, want, hipHostMallocDefault);
+  if (err != hipSuccess) return fail(MOX_ENOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(err));
+  b.cap = want;
+  return MOX_OK;
+}
+
+// Moves per-peer byte ranges between ranks.  send/recv are device buffers;
+// off/len are per-peer byte offsets and sizes (len identical on both sides of
+// every pair by construction).
+struct Transport {
+  virtual ~Transport() = default;
+  // per-peer count rows: h_send[d] -> peer d; fills h_recv[s] from peer s.
+  // d_send / d_recv are device mirrors (d_send already holds h_send).
+  virtual int counts(const XCnt* d_send, XCnt* d_recv, const XCnt* h_send, XCnt* h_recv) = 0;
+  virtual int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
+                        const uint64_t* rlen) = 0;
+};
+
+struct RcclTransport : Transport {
+  mox_engine* e;
+  explicit RcclTransport(mox_engine* e_) : e(e_) {}
+  int counts(const XCnt* d_send, XCnt* d_recv, const XCnt*, XCnt* h_recv) override {
+    const int P = e->nranks;
+    RCCLCHK(ncclGroupStart());
+    for (int p = 0; p < P; p++) {
+      RCCLCHK(ncclSend(d_send + p, sizeof(XCnt), ncclUint8, p, e->comm, e->stream));
+      RCCLCHK(ncclRecv(d_recv + p, sizeof(XCnt), ncclUint8, p, e->comm, e->stream));
+    }
+    RCCLCHK(ncclGroupEnd());
+    HIPCHK(hipMemcpyAsync(h_recv, d_recv, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    return MOX_OK;
+  }
+  int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
+                const uint64_t* rlen) override {
+    const int P = e->nranks, me = e->rank;
+    if (slen[me]) HIPCHK(hipMemcpyAsync(recv + roff[me], send + soff[me], slen[me], hipMemcpyDeviceToDevice, e->stream));
+    RCCLCHK(ncclGroupStart());
+    for (int p = 0; p < P; p++) {
+      if (p == me) continue;
+      if (slen[p]) RCCLCHK(ncclSend(send + soff[p], slen[p], ncclUint8, p, e->comm, e->stream));
+      if (rlen[p]) RCCLCHK(ncclRecv(recv + roff[p], rlen[p], ncclUint8, p, e->comm, e->stream));
+    }
+    RCCLCHK(ncclGroupEnd());
+    return MOX_OK;
+  }
+};
+
+// Host-staged transport: device -> pinned host, caller's all-to-all callback
+// (e.g. torch.distributed over gloo), pinned host -> device.  Used where RCCL
+// cannot run (several ranks sharing one GPU in tests).
+struct HostTransport : Transport {
+  mox_engine* e;
+  int P;
+  mox_alltoallv_fn fn;
+  void* user;
+  HostTransport(mox_engine* e_, int P_, mox_alltoallv_fn f, void* u) : e(e_), P(P_), fn(f), user(u) {}
+  int counts(const XCnt*, XCnt*, const XCnt* h_send, XCnt* h_recv) override {
+    uint64_t len[MAX_RANKS];
+    for (int p = 0; p < P; p++) len[p] = sizeof(XCnt);
+    if (fn(user, h_send, len, h_recv, len) != 0) return fail(MOX_EIO, "host all-to-all callback failed (counts)");
+    return MOX_OK;
+  }
+  int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
+                const uint64_t* rlen) override {
+    const uint64_t stot = soff[P - 1] + slen[P - 1], rtot = roff[P - 1] + rlen[P - 1];
+    int rc;
+    if ((rc = grow_pinned(e->hx_send, stot + 8)) || (rc = grow_pinned(e->hx_recv, rtot + 8))) return rc;
+    if (stot) HIPCHK(hipMemcpyAsync(e->hx_send.p, send, stot, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if (fn(user, e->hx_send.p, slen, e->hx_recv.p, rlen) != 0) return fail(MOX_EIO, "host all-to-all callback failed");
+    if (rtot) HIPCHK(hipMemcpyAsync(recv, e->hx_recv.p, rtot, hipMemcpyHostToDevice, e->stream));
+    return MOX_OK;
+  }
+};
+
+// One attempt of the reduce-only pass over the received partials.
+int exchange_pass_once(mox_engine* e, uint64_t r_short, uint64_t blob_bytes, const XDir& rdir) {
+  Work& w = e->w;
+  hipStream_t s = e->stream;
+  const Seq q = seq_of(e);
+  q.rec(0);
+  *e->h_ctl_x = *e->h_ctl_init;
+  e->h_ctl_x->w_n = r_short;
+  HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_x, sizeof(Ctl), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
+  HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
+  HIPCHK(hipMemsetAsync(w.cold_n, 0, (size_t)w.map_grid * NB * 4, s));
+  HIPCHK(hipMemsetAsync(w.spill_n, 0, (size_t)w.map_grid * 4, s));
+  if (r_short) HIPCHK(hipMemcpyAsync(w.w, e->x_recv_short.p, r_short * sizeof(WRec), hipMemcpyDeviceToDevice, s));
+  if (blob_bytes) HIPCHK(hipMemcpyAsync(w.arena, e->x_recv_blob.p, blob_bytes, hipMemcpyDeviceToDevice, s));
+  q.rec(1);
+  q.rec(2);
+  hipLaunchKernelGGL(k_xingest, dim3(1024), dim3(256), 0, s, w, rdir, r_short);
+  q.step("k_xingest");
+  q.rec(3);
+  Corpus none{};
+  none.base = (const uint8_t*)w.ctl;  // long refs are all arena refs in this pass
+  launch_reduce_tail(e, none, q);
+  return finish_pass(e, q);
+}
+
+int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
+  if (!e->have_result) return fail(MOX_ESTATE, "no local result: mox_run_range first");
+  if (P > MAX_RANKS) return fail(MOX_EINVAL, "at most %d ranks", MAX_RANKS);
+  HIPCHK(hipSetDevice(e->device));
+  Work& w = e->w;
+  hipStream_t s = e->stream;
+  int rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  const mox_stats local = e->stats;  // the exchange pass reuses the phase events
+  if (!e->d_xcnt) {
+    if ((rc = dalloc(e, (void**)&e->d_xcnt, 2 * MAX_RANKS * sizeof(XCnt)))) return rc;
+    if ((rc = dalloc(e, (void**)&e->d_xcur, 2 * MAX_RANKS * 8))) return rc;
+    HIPCHK(hipHostMalloc((void**)&e->h_xcnt, 2 * MAX_RANKS * sizeof(XCnt), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&e->h_ctl_x, sizeof(Ctl), hipHostMallocDefault));
+  }
+  XCnt* d_send = e->d_xcnt;
+  XCnt* d_recv = e->d_xcnt + MAX_RANKS;
+  XCnt* h_send = e->h_xcnt;
+  XCnt* h_recv = e->h_xcnt + MAX_RANKS;
+  // 1. per-destination counts
+  HIPCHK(hipMemsetAsync(d_send, 0, P * sizeof(XCnt), s));
+  hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, s, w, (uint32_t)P, d_send);
+  HIPCHK(hipMemcpyAsync(h_send, d_send, P * sizeof(XCnt), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if ((rc = T.counts(d_send, d_recv, h_send, h_recv))) return rc;
+  // 2. send layout + pack
+  uint64_t s_short_off[MAX_RANKS], s_short_len[MAX_RANKS], s_blob_off[MAX_RANKS], s_blob_len[MAX_RANKS];
+  uint64_t r_short_off[MAX_RANKS], r_short_len[MAX_RANKS], r_blob_off[MAX_RANKS], r_blob_len[MAX_RANKS];
+  uint64_t ns = 0, sb = 0, rs = 0, rb = 0, r_long = 0;
+  XDir sdir{}, rdir{};
+  sdir.P = rdir.P = (uint32_t)P;
+  for (int d = 0; d < P; d++) {
+    s_short_off[d] = ns * sizeof(WRec);
+    s_short_len[d] = h_send[d].n_short * sizeof(WRec);
+    ns += h_send[d].n_short;
+    sdir.blob[d] = s_blob_off[d] = sb;
+    sdir.nlong[d] = h_send[d].n_long;
+    s_blob_len[d] = h_send[d].n_long * sizeof(XHdr) + h_send[d].long_bytes;
+    sb += s_blob_len[d];
+    r_short_off[d] = rs * sizeof(WRec);
+    r_short_len[d] = h_recv[d].n_short * sizeof(WRec);
+    rs += h_recv[d].n_short;
+    rdir.blob[d] = r_blob_off[d] = rb;
+    rdir.nlong[d] = h_recv[d].n_long;
+    rdir.hpre[d] = r_long;
+    r_long += h_recv[d].n_long;
+    r_blob_len[d] = h_recv[d].n_long * sizeof(XHdr) + h_recv[d].long_bytes;
+    rb += r_blob_len[d];
+  }
+  sdir.blob[P] = sb;
+  rdir.blob[P] = rb;
+  rdir.hpre[P] = r_long;
+  if ((rc = grow_dev(e->x_send_short, ns * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_send_blob, sb + 64)) ||
+      (rc = grow_dev(e->x_recv_short, rs * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_recv_blob, rb + 64)))
+    return rc;
+  hipLaunchKernelGGL(k_xpack_short, dim3(1024), dim3(256), 0, s, w, (WRec*)e->x_send_short.p);
+  HIPCHK(hipMemsetAsync(e->d_xcur, 0, 2 * MAX_RANKS * 8, s));
+  hipLaunchKernelGGL(k_xpack_long, dim3(256), dim3(256), 0, s, w, sdir, e->d_xcur, (uint8_t*)e->x_send_blob.p);
+  HIPCHK(hipGetLastError());
+  (void)me;
+  // 3. payload all-to-alls
+  if ((rc = T.alltoallv((const uint8_t*)e->x_send_short.p, s_short_off, s_short_len, (uint8_t*)e->x_recv_short.p, r_short_off,
+                        r_short_len)))
+    return rc;
+  if ((rc = T.alltoallv((const uint8_t*)e->x_send_blob.p, s_blob_off, s_blob_len, (uint8_t*)e->x_recv_blob.p, r_blob_off, r_blob_len)))
+    return rc;
+  // 4. reduce-only pass over the received partials (the local table is no
+  //    longer needed: buffers may be regrown)
+  Caps need = caps_of(w);
+  need.w_cap = std::max<uint64_t>(need.w_cap, rs + rs / 8 + 1024);
+  need.table_cap = std::max<uint64_t>(need.table_cap, rs + r_long + 1024);
+  need.bytes_cap = std::max<uint64_t>(need.bytes_cap, rs * 16 + rb + 65536);
+  need.long_cap = std::max<uint64_t>(need.long_cap, next_pow2(2 * r_long + 1024));
+  need.arena_cap = std::max<uint64_t>(need.arena_cap, rb + 65536);
+  HIPCHK(hipStreamSynchronize(s));
+  e->have_result = false;
+  if ((rc = ensure_caps(e, need))) return rc;
+  for (int attempt = 0;; attempt++) {
+    if ((rc = exchange_pass_once(e, rs, rb, rdir))) return rc;
+    const Ctl& h = *e->h_ctl;
+    if (!h.overflow) break;
+    if (h.overflow & OVF_REDUCE) return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
+    if (attempt >= 4) return fail(MOX_ENOMEM, "exchange buffer growth did not converge (overflow mask 0x%x)", h.overflow);
+    e->stats.retries++;
+    if ((rc = ensure_caps(e, grow_for(e, h)))) return rc;
+  }
+  const Ctl& h = *e->h_ctl;
+  const uint32_t retries = e->stats.retries;
+  e->stats = local;
+  e->stats.retries = retries;
+  e->stats.tokens = h.tokens;
+  e->stats.uniques = h.n_total;
+  e->stats.ms_exchange = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  e->last_corpus = Corpus{};
+  e->last_corpus.base = (const uint8_t*)w.ctl;
+  e->have_result = true;
+  return MOX_OK;
 }
 
 }  // namespace
@@ -506,6 +773,12 @@ void mox_engine_destroy(mox_engine* e) {
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_lens, e->d_text};
   for (void* p : ptrs) dfree(p);
+  for (DevBuf* b : {&e->x_send_short, &e->x_send_blob, &e->x_recv_short, &e->x_recv_blob}) dfree(b->p);
+  for (DevBuf* b : {&e->hx_send, &e->hx_recv}) if (b->p) (void)hipHostFree(b->p);
+  dfree(e->d_xcnt);
+  dfree(e->d_xcur);
+  if (e->h_xcnt) (void)hipHostFree(e->h_xcnt);
+  if (e->h_ctl_x) (void)hipHostFree(e->h_ctl_x);
   if (e->h_ctl) (void)hipHostFree(e->h_ctl);
   if (e->h_ctl_init) (void)hipHostFree(e->h_ctl_init);
   for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
@@ -715,7 +988,15 @@ int mox_comm_init(mox_engine* e, int nranks, int rank, const uint8_t id[MOX_UNIQ
 int mox_exchange(mox_engine* e) {
   if (!e) return fail(MOX_EINVAL, "engine is NULL");
   if (!e->comm) return fail(MOX_ESTATE, "mox_comm_init first");
-  return fail(MOX_ESTATE, "mox_exchange: not implemented yet");
+  RcclTransport t(e);
+  return exchange_impl(e, e->nranks, e->rank, t);
+}
+
+int mox_exchange_host(mox_engine* e, int nranks, int rank, mox_alltoallv_fn fn, void* user) {
+  if (!e || !fn) return fail(MOX_EINVAL, "NULL argument");
+  if (nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad rank %d of %d", rank, nranks);
+  HostTransport t(e, nranks, fn, user);
+  return exchange_impl(e, nranks, rank, t);
 }
 
 }  // extern "C"

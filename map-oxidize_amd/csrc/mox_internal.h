@@ -82,6 +82,36 @@ struct LSlot {
   unsigned long long count;
 };
 
+// ---- multi-GPU exchange ----
+constexpr int MAX_RANKS = 64;
+// Owner rank of a short key's partition b: ranks own contiguous partition
+// ranges, so the dense table (partition order) is already in owner order.
+__host__ __device__ __forceinline__ uint32_t part_owner(uint32_t b, uint32_t P) { return (uint32_t)(((uint64_t)b * P) >> NB_LOG2); }
+// First partition of rank d (d may be P: returns NB).
+__host__ __device__ __forceinline__ uint32_t owner_first_part(uint32_t d, uint32_t P) { return (uint32_t)(((uint64_t)d * NB + P - 1) / P); }
+// Owner rank of a long word (FNV-1a-64 hash h).
+__host__ __device__ __forceinline__ uint32_t long_owner(uint64_t h, uint32_t P) { return (uint32_t)(((h >> 32) * P) >> 32); }
+// Long-word record header on the wire; off = byte offset of the word inside
+// this (source, destination) blob's byte area, which follows the headers.
+struct XHdr {
+  uint64_t h, len, count, off;
+};
+// Per-destination counts one rank sends (one 32-byte row per peer).
+struct XCnt {
+  unsigned long long n_short;     // WRec records
+  unsigned long long n_long;      // XHdr records
+  unsigned long long long_bytes;  // word bytes, each word padded to 8
+  unsigned long long pad;
+};
+// Kernel argument: per-peer offsets (send side: blob bases; receive side:
+// blob bases + header prefix).
+struct XDir {
+  uint32_t P;
+  uint64_t blob[MAX_RANKS + 1];   // byte offset of peer d's long blob
+  uint64_t nlong[MAX_RANKS];      // headers in peer d's blob
+  uint64_t hpre[MAX_RANKS + 1];   // prefix of nlong (receive side)
+};
+
 struct Tables {  // Unicode case data in device memory
   const uint32_t* lower_src;
   const uint32_t* lower_dst;

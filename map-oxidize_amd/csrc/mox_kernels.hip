@@ -1321,4 +1321,86 @@ extern "C" __global__ void k_mat_bytes(Work w, Corpus c) {
   }
 }
 
+// ------------------------------------------------------------------ multi-GPU exchange
+//   Input: this rank's dense table after a local run.  Short
+// words travel as WRec (key, count) in dense order, which is partition order
+// and therefore owner order (part_owner); long words as XHdr + bytes, grouped
+// per owner by long_owner(FNV hash).
+
+// xcnt[d] for every destination d (xcnt zeroed by the host).
+extern "C" __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt) {
+  if (blockIdx.x == 0 && threadIdx.x < P) {
+    const uint32_t d = threadIdx.x;
+    xcnt[d].n_short = w.uniq_off[owner_first_part(d + 1, P)] - w.uniq_off[owner_first_part(d, P)];
+  }
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
+    const LSlot e = w.ltab[s];
+    if (!e.h) continue;
+    const uint32_t d = long_owner(e.h, P);
+    atomicAdd(&xcnt[d].n_long, 1ull);
+    atomicAdd(&xcnt[d].long_bytes, (unsigned long long)((e.len + 7) & ~7ull));
+  }
+}
+
+// Short words in dense order as WRec (same source mapping as k_mat_counts).
+extern "C" __global__ void k_xpack_short(Work w, WRec* out) {
+  __shared__ uint64_t uoff[NB + 1];
+  __shared__ uint64_t roff[NB + 1];
+  for (int i = threadIdx.x; i <= NB; i += blockDim.x) { uoff[i] = w.uniq_off[i]; roff[i] = w.rec_off[i]; }
+  __syncthreads();
+  const uint64_t ns = w.ctl->n_short;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    int a = 0, b = NB - 1;
+    while (a < b) { int m = (a + b + 1) >> 1; if (uoff[m] <= i) a = m; else b = m - 1; }
+    const uint64_t src = roff[a] + (i - uoff[a]);
+    const uint4 k = w.uk[src];
+    out[i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, w.uc[src]};
+  }
+}
+
+// Long words into per-destination blobs [XHdr x n_long][bytes]; cur = 2P
+// zeroed cursors (headers, bytes).  Bytes come from the materialised table.
+extern "C" __global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob) {
+  const uint64_t ns = w.ctl->n_short;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
+    const LSlot e = w.ltab[s];
+    if (!e.h) continue;
+    const uint32_t d = long_owner(e.h, dir.P);
+    const uint64_t k = atomicAdd(&cur[d], 1ull);
+    const uint64_t bo = atomicAdd(&cur[dir.P + d], (unsigned long long)((e.len + 7) & ~7ull));
+    const uint64_t i = ns + w.lpos[s];
+    uint8_t* base = blob + dir.blob[d];
+    reinterpret_cast<XHdr*>(base)[k] = XHdr{e.h, e.len, w.t_counts[i], bo};
+    uint8_t* o = base + dir.nlong[d] * sizeof(XHdr) + bo;
+    const uint8_t* src = w.t_bytes + w.t_offs[i];
+    for (uint64_t j = 0; j < e.len; j++) o[j] = src[j];
+  }
+}
+
+// Received partials -> reduce input.  Short WRecs are already in w.w (count in
+// ctl->w_n); long words are inserted into the long table with arena refs (the
+// received blob area was copied to the arena).  Sums all counts into
+// ctl->tokens.
+extern "C" __global__ void k_xingest(Work w, XDir dir, uint64_t n_short) {
+  const uint64_t nlong = dir.hpre[dir.P];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  unsigned long long tok = 0;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n_short; t += stride) tok += w.w[t].count;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nlong; t += stride) {
+    uint32_t a = 0, b = dir.P - 1;  // source s with hpre[s] <= t < hpre[s+1]
+    while (a < b) { const uint32_t m = (a + b + 1) >> 1; if (dir.hpre[m] <= t) a = m; else b = m - 1; }
+    const uint64_t base = dir.blob[a];
+    const XHdr hd = reinterpret_cast<const XHdr*>(w.arena + base)[t - dir.hpre[a]];
+    const uint64_t ref = base + dir.nlong[a] * sizeof(XHdr) + hd.off;
+    long_insert(w, nullptr, hd.h, ARENA_BIT | ref, hd.len, hd.count);
+    atomicAdd(&w.ctl->long_n, 1ull);
+    tok += hd.count;
+  }
+  for (int off = 32; off > 0; off >>= 1) tok += __shfl_down(tok, off);
+  if ((threadIdx.x & 63) == 0 && tok) atomicAdd(&w.ctl->tokens, tok);
+}
+
 }  // namespace mox

@@ -93,6 +93,10 @@ class Stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+# int (*)(void* user, const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes)
+_A2A_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                           ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
+
 _lib = None
 
 
@@ -125,6 +129,7 @@ def lib():
             "mox_comm_unique_id": ([ctypes.c_char_p], I),
             "mox_comm_init": ([VP, I, I, ctypes.c_char_p], I),
             "mox_exchange": ([VP], I),
+            "mox_exchange_host": ([VP, I, I, _A2A_FN, VP], I),
             "mox_write_final_result": ([P(_Table), ctypes.c_char_p], I),
             "mox_print_top_words": ([P(_Table), sz], I),
         }
@@ -260,7 +265,36 @@ class Engine:
         _check(lib().mox_comm_init(self._h, nranks, rank, uid))
 
     def exchange(self):
+        """RCCL all-to-all exchange + final reduce (after run_range on every rank)."""
         _check(lib().mox_exchange(self._h))
+
+    def exchange_host(self, nranks, rank, alltoallv):
+        """The same exchange over a host transport.  ``alltoallv(send, send_sizes,
+        recv_sizes)`` gets the send bytes (memoryview, blocks for ranks 0..n-1)
+        and must return the received bytes (blocks from ranks 0..n-1)."""
+        err = []
+
+        def cb(_user, send, send_bytes, recv, recv_bytes):
+            try:
+                ss = [int(send_bytes[i]) for i in range(nranks)]
+                rs = [int(recv_bytes[i]) for i in range(nranks)]
+                buf = (ctypes.c_uint8 * sum(ss)).from_address(send) if sum(ss) else bytearray()
+                out = alltoallv(memoryview(buf), ss, rs)
+                out = bytes(out)
+                if len(out) != sum(rs):
+                    raise ValueError("alltoallv returned %d bytes, expected %d" % (len(out), sum(rs)))
+                if out:
+                    ctypes.memmove(recv, out, len(out))
+                return 0
+            except Exception as ex:  # reported after the call returns
+                err.append(ex)
+                return 1
+
+        fn = _A2A_FN(cb)
+        rc = lib().mox_exchange_host(self._h, nranks, rank, fn, None)
+        if err:
+            raise err[0]
+        _check(rc)
 
     def close(self):
         if getattr(self, "_h", None):

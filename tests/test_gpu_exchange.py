@@ -1,0 +1,119 @@
+"""GPU: the multi-GPU exchange -- byte-range shards, local
+passes, all-to-all of the partial tables, final per-owner reduce -- checked
+bit-exactly against the oracle on the whole corpus.
+
+One GPU box has one GPU, so several ranks share device 0: the RCCL transport is
+exercised at world size 1 (self send/recv through RCCL), the multi-rank data
+path through the host-staged transport (threads in one process, and separate
+processes over gloo).  Both transports move the same packed buffers; only the
+copy differs."""
+import json
+import os
+import subprocess
+import sys
+import threading
+
+import pytest
+
+import coracle
+import mox
+from mox import corpus
+from mox import dist as mdist
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+def mixed_corpus(n, seed):
+    """Zipf text with Unicode tokens and long (> 16 byte) words mixed in."""
+    z = corpus.fill(corpus.ZIPF, seed, 0, n).tobytes()
+    u = corpus.fill(corpus.UNICODE, seed + 1, 0, n // 8).tobytes()
+    extra = b" ".join(b"Supercalifragilistic%dexpialidocious" % (i % 97) for i in range(3000))
+    return z[: n // 2] + b" " + u + b"\n" + extra + b" " + z[n // 2:]
+
+
+def run_ranks(data, world, use_threads=True):
+    """Each rank: engine on device 0, its shard, exchange over ThreadAlltoall."""
+    x = mdist.ThreadAlltoall(world)
+    out, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            lo, hi, ob, oe, at_end = mdist.shard_range(len(data), world, r)
+            e = mox.Engine(device=0)
+            try:
+                buf = data[lo:hi]
+                d = e.alloc(max(1, len(buf)))
+                try:
+                    if buf:
+                        e.h2d(d, buf)
+                    e.run_range(d, len(buf), ob, oe, at_end)
+                    e.exchange_host(world, r, x.fn(r))
+                    t = e.fetch()
+                    out[r] = (t.sorted_items(), t.tokens)
+                    t.close()
+                finally:
+                    e.free(d)
+            finally:
+                e.close()
+        except BaseException as ex:  # noqa: BLE001
+            errs.append(ex)
+            x.barrier.abort()
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(300) for t in ts]
+    if errs:
+        raise errs[0]
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_exchange_threads(world):
+    data = mixed_corpus(6 << 20, 40 + world)
+    out = run_ranks(data, world)
+    merged = mdist.merge_tables([items for items, _ in out])  # also asserts disjoint owners
+    want, wtok = coracle.count(data)
+    assert sum(tok for _, tok in out) == wtok
+    for items, tok in out:
+        assert sum(c for _, c in items) == tok
+    assert merged == want
+
+
+def test_host_exchange_empty_and_tiny_shards():
+    for data in (b"", b"a", b"a b", b"x " * 5 + b"Y" * 40):
+        out = run_ranks(data, 3)
+        assert mdist.merge_tables([items for items, _ in out]) == coracle.count(data)[0]
+
+
+def test_rccl_transport_world1():
+    data = mixed_corpus(3 << 20, 9)
+    e = mox.Engine(device=0)
+    try:
+        e.comm_init(1, 0, mox.comm_unique_id())
+        d = e.alloc(len(data))
+        try:
+            e.h2d(d, data)
+            e.run_range(d, len(data), 0, len(data), True)
+            e.exchange()
+            t = e.fetch()
+            got = t.sorted_items()
+            t.close()
+        finally:
+            e.free(d)
+    finally:
+        e.close()
+    assert got == coracle.count(data)[0]
+
+
+def test_host_exchange_gloo_processes(tmp_path):
+    """Two processes (torch.distributed gloo) share the GPU; rank 0 gathers."""
+    out = tmp_path / "merged.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29561",
+           os.path.join(ROOT, "tests", "dist_worker.py"), str(out)]
+    r = subprocess.run(cmd, capture_output=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(out.read_text())
+    data = mixed_corpus(4 << 20, 77)
+    assert [(bytes.fromhex(w), c) for w, c in res] == coracle.count(data)[0]

@@ -2,9 +2,9 @@
 # GPU parity tests then a short bench (each step under its own time limit).
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "not slow" > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu.log
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "not slow" ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -25 gpurun_out/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 200 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench.log 2>&1
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.log | tail -3
 exit $rc
