@@ -269,7 +269,7 @@ int alloc_fixed(mox_engine* e) {
 }
 
 size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_BUCKETS * 4; }  // k_dict_build
-size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + MAP_WAVES * (ROWBUF + 2 * TOKMAX); }
+size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
 size_t reduce_lds_bytes() { return 2560 * (8 * 3 + 4) + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP (mox_kernels.hip)
 
 // exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)
@@ -376,7 +376,7 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   q.rec(1);
   // 2. map: one streaming pass over the corpus
   const uint64_t row0 = c.own_lo & ~15ull;
-  const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + 1023) / 1024 : 0;
+  const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + PAY - 1) / PAY : 0;
   const int grid = (int)w.map_grid;
   hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows);
   q.step("k_map");
@@ -459,9 +459,13 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   return MOX_OK;
 }
 
+// Internal coordinates: c.base is the buffer address rounded down to 16 B,
+// minus 16, so that every valid byte sits at >= 16 and a row's context lane
+// (16 bytes before its payload) never underflows.  Loads clamp to
+// [lo, hi), so nothing below the buffer is ever read.
 Corpus make_corpus(const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end, int at_end) {
   uintptr_t addr = (uintptr_t)d_buf;
-  uint64_t mis = addr & 15;
+  uint64_t mis = (addr & 15) + 16;
   Corpus c{};
   c.base = (const uint8_t*)(addr - mis);
   c.lo = mis;

@@ -461,19 +461,21 @@ __device__ __forceinline__ void token_batches(const MapCtx& m, const uint8_t* ro
   }
 }
 
-// One row (64 lanes x 16 B) in two phases:
+// One ring slot (64 lanes x 16 B = corpus bytes [sbase, sbase + 1024)) in two
+// phases.  Lanes 1..62 hold the row's 992 payload bytes; lane 0 (the 16 bytes
+// before) and lane 63 (the 16 bytes after) are context only: they give the
+// previous-byte and look-ahead bits and start no token.
 //  1. byte phase (lane = 16 B): token-start bit masks (SWAR on ASCII rows, the
-//     Unicode walk on rows with non-ASCII bytes), the lowered row into LDS and a
-//     compacted list of token (start, length) in row order (wave prefix sum of
-//     per-lane start counts from 5 bit-sliced ballots);
+//     Unicode walk on rows with non-ASCII bytes), the lowered slot back into LDS
+//     and a compacted list of token (slot offset, length) in row order (wave
+//     prefix sum of per-lane start counts from 5 bit-sliced ballots);
 //  2. token phase (lane = token), see token_batches.
-// nxt = the next row's first 16 bytes (wave-uniform), prev_last = the byte
-// before the row (wave-uniform).
-__device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, uint4 nxt, uint32_t prev_last,
-                                       unsigned long long& ntok, uint8_t* rowbuf, uint16_t* list) {
+__device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
+                                       uint16_t* list) {
   const int lane = threadIdx.x & 63;
-  const uint64_t rowbase = p0 - (uint64_t)lane * 16;
-  const bool slow = __any(nonascii16(a) != 0) || nonascii16(nxt) != 0 || (prev_last & 0x80u) != 0;
+  const uint64_t p0 = sbase + (uint64_t)lane * 16;
+  const bool ctx = lane == 0 || lane == 63;
+  const bool slow = __any(nonascii16(a) != 0);
   uint32_t ws32 = 0, z32 = 0, start;
   bool chk = false;  // rows with NUL bytes or near a non-final buffer end need the odd checks
   uint32_t lim = 64;
@@ -482,25 +484,23 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, ui
     const uint32_t ws16 = movemask8(ws_bytes80(L)) | (movemask8(ws_bytes80(H)) << 8);
     const uint32_t wsn = __shfl_down(ws16, 1);
     const uint32_t wsp = __shfl_up(ws16, 1);
-    const uint32_t ws_nxt = ws_mask16(nxt);
-    ws32 = ws16 | ((lane == 63 ? ws_nxt : wsn) << 16);
-    const uint32_t prevws = lane == 0 ? (is_ascii_ws(prev_last) ? 1u : 0u) : (wsp >> 15) & 1u;
-    start = (~ws32) & ((ws32 << 1) | prevws) & 0xFFFFu;
-    if (rowbase < m.c.own_lo || rowbase + ROW > m.c.own_hi) {
+    ws32 = ws16 | (wsn << 16);
+    start = (~ws32) & ((ws32 << 1) | ((wsp >> 15) & 1u)) & 0xFFFFu;
+    if (ctx) start = 0;
+    if (sbase + 16 < m.c.own_lo || sbase + ROW - 16 > m.c.own_hi) {
       if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
       if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
     }
-    const bool anyz = __any((zero_bytes80(L) | zero_bytes80(H)) != 0) || zero_mask16(nxt) != 0;
+    const bool anyz = __any((zero_bytes80(L) | zero_bytes80(H)) != 0);
     if (anyz) {
       const uint32_t z16 = zero_mask16(a);
-      const uint32_t zn = __shfl_down(z16, 1);
-      z32 = z16 | ((lane == 63 ? zero_mask16(nxt) : zn) << 16);
+      z32 = z16 | (__shfl_down(z16, 1) << 16);
     }
-    const bool near_end = !m.c.at_end && rowbase + ROW + 32 >= m.c.hi;
+    const bool near_end = !m.c.at_end && sbase + ROW + 32 >= m.c.hi;
     if (near_end) lim = m.c.hi > p0 ? (uint32_t)(m.c.hi - p0 < 64 ? m.c.hi - p0 : 64) : 0u;
     chk = anyz || near_end;
   } else {
-    start = slow_starts(m, p0);
+    start = ctx ? 0u : slow_starts(m, p0);
   }
   if (m.w.dbg & DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
   const uint32_t cnt = __popc(start);
@@ -516,8 +516,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, ui
   }
   if (total == 0) return;
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
-  if (lane == 63) reinterpret_cast<uint4*>(rowbuf)[64] = lower16(nxt);
-  // list entry (u16): start in row (10 bits) | length (5 bits, <= 16) | odd (bit 15)
+  // list entry (u16): slot offset (10 bits) | length (5 bits, <= 16) | odd (bit 15)
   uint32_t k = pre;
   bool any_odd = false;
   while (start) {
@@ -534,7 +533,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, ui
   if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
     for (uint32_t j = lane; j < total; j += 64) {
       const uint32_t e = list[j];
-      if (e & 0x8000u) generic_token(m, rowbase + (e & 1023u));
+      if (e & 0x8000u) generic_token(m, sbase + (e & 1023u));
     }
   }
   if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
@@ -549,12 +548,17 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t p0, uint4 a, ui
   wave_lds_fence();
 }
 
-// Every wave streams its own contiguous range of 1 KiB rows.  Rows rotate
-// through DEPTH register slots: the load of row r + DEPTH is issued before row
-// r is processed, and row r + 1's lane-0 segment is row r's look-ahead.  No
-// workgroup barrier inside the loop.
-constexpr int DEPTH = 4;
-
+// Map kernel.  One persistent 1024-thread workgroup per CU owns a contiguous
+// range of rows (992 payload bytes each).
+//  * wave 0 = loader: streams each row's slot (payload +16 B either side) with
+//    16 B/lane loads into registers, LD_GROUPS groups of LD_GROUP rows in
+//    flight, and copies each into a free ring slot with ds_write, then
+//    publishes the slot (flag written after the data by the same wave, so DS
+//    ordering makes the hand-off safe).  It issues no stores to memory, so its
+//    vmcnt waits are exact.
+//  * waves 1..15 = consumers: take rows in order by ticket (dynamic load
+//    balance), process them from LDS (do_row) and release the slot.  Their
+//    cold-record stores are never waited for inside the loop.
 extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t nrows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   MapCtx m;
@@ -565,65 +569,96 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
-  m.s.misc = (uint32_t*)sp; sp += 16;
-  m.s.wave = sp;
-  const int tid = threadIdx.x, lane = tid & 63;
+  m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
+  uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
+  uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
+  uint8_t* ring = sp; sp += RING * SLOT;
+  uint16_t* lists = (uint16_t*)sp;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.ctl->dict_n;
   if (m.dict_n) {
     for (int i = tid; i < DICT_BUCKETS; i += MAP_THREADS) m.s.dtag4[i] = reinterpret_cast<const uint4*>(w.dict_tag)[i];
     for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) { m.s.dkey[i] = w.dict_key[i]; m.s.dcnt[i] = 0; }
   }
   for (int i = tid; i < NB; i += MAP_THREADS) m.s.bcnt[i] = 0;
-  if (tid == 0) m.s.misc[0] = 0;
+  if (tid < 4) m.s.misc[tid] = 0;
+  if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
   __syncthreads();
-  uint8_t* rowbuf = m.s.wave + (tid >> 6) * (ROWBUF + 2 * TOKMAX);
-  uint16_t* list = reinterpret_cast<uint16_t*>(rowbuf + ROWBUF);
   unsigned long long ntok = 0;
 
   const uint64_t base0 = c.own_lo & ~15ull;
-  const uint64_t nwaves = (uint64_t)gridDim.x * MAP_WAVES;
-  const uint64_t wid = (uint64_t)blockIdx.x * MAP_WAVES + (tid >> 6);
-  const uint64_t per = nrows / nwaves, rem = nrows % nwaves;
-  const uint64_t rb = wid * per + (wid < rem ? wid : rem);
-  const uint64_t re = rb + per + (wid < rem ? 1 : 0);
-  if (rb < re) {
-    // the byte before this wave's first row (lane 0's left context)
-    uint32_t prev_last;
-    {
-      const uint64_t pb = base0 + rb * ROW;
-      prev_last = (pb > c.lo && pb - 1 < c.hi) ? c.base[pb - 1] : 0x20u;
-    }
-    // rows past the corpus read as blanks (raw16 clamps, fix16 blanks them)
-    uint4 s0 = raw16(c, base0 + rb * ROW + lane * 16);
-    uint4 s1 = raw16(c, base0 + (rb + 1) * ROW + lane * 16);
-    uint4 s2 = raw16(c, base0 + (rb + 2) * ROW + lane * 16);
-    uint4 s3 = raw16(c, base0 + (rb + 3) * ROW + lane * 16);
-    for (uint64_t r = rb; r < re; r++) {
-      uint4 a = s0, nx = s1;
-      s0 = s1; s1 = s2; s2 = s3;
-      s3 = raw16(c, base0 + (r + DEPTH) * ROW + lane * 16);
-      const uint64_t p0 = base0 + r * ROW + lane * 16;
-      const uint64_t rs = base0 + r * ROW;
-      if (rs < c.lo || rs + ROW + 16 > c.hi) {
-        a = fix16(c, p0, a);
-        nx = fix16(c, rs + ROW + lane * 16, nx);
+  const uint64_t G = gridDim.x;
+  const uint64_t per = nrows / G, rem = nrows % G;
+  const uint64_t rb = blockIdx.x * per + (blockIdx.x < rem ? blockIdx.x : rem);
+  const uint32_t n = (uint32_t)(per + (blockIdx.x < rem ? 1 : 0));
+
+  if (wv == 0) {
+    // ---------------- loader
+    uint4 buf[LD_GROUPS][LD_GROUP];
+    auto issue = [&](uint4 (&b)[LD_GROUP], uint32_t t0) {
+#pragma unroll
+      for (int i = 0; i < LD_GROUP; i++) {  // rows past n load a clamped block: uniform vmcnt counts
+        const uint64_t sb = base0 + (rb + t0 + i) * PAY - 16;
+        b[i] = raw16(c, sb + 16 * (uint64_t)lane);
       }
-      const uint4 nxt = lane0(nx);  // look-ahead: the next row's first 16 bytes
-      do_row(m, p0, a, nxt, prev_last, ntok, rowbuf, list);
-      prev_last = __builtin_amdgcn_readlane(a.w >> 24, 63);
+    };
+    auto retire = [&](const uint4 (&b)[LD_GROUP], uint32_t t0) {
+#pragma unroll
+      for (int i = 0; i < LD_GROUP; i++) {
+        const uint32_t t = t0 + i;
+        if (t >= n) break;
+        const uint32_t slot = t % RING;
+        if (t >= RING) {
+          while (__hip_atomic_load(&sfree[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t - RING + 1)
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        reinterpret_cast<uint4*>(ring + slot * SLOT)[lane] = b[i];
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        if (lane == 0) __hip_atomic_store(&sready[slot], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    };
+#pragma unroll
+    for (int g = 0; g < LD_GROUPS - 1; g++) issue(buf[g], g * LD_GROUP);
+    for (uint32_t t0 = 0; t0 < n; t0 += LD_GROUPS * LD_GROUP) {
+#pragma unroll
+      for (int g = 0; g < LD_GROUPS; g++) {
+        issue(buf[(g + LD_GROUPS - 1) % LD_GROUPS], t0 + (g + LD_GROUPS - 1) * LD_GROUP);
+        retire(buf[g], t0 + g * LD_GROUP);
+      }
+    }
+  } else {
+    // ---------------- consumers
+    uint16_t* list = lists + (wv - 1) * TOKMAX;
+    for (;;) {
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
+      u = __builtin_amdgcn_readfirstlane(u);
+      if (u >= n) break;
+      const uint32_t slot = u % RING;
+      while (__hip_atomic_load(&sready[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != u + 1)
+        __builtin_amdgcn_s_sleep(1);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      uint8_t* sl = ring + slot * SLOT;
+      const uint64_t sbase = base0 + (rb + u) * PAY - 16;
+      uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
+      if (sbase < c.lo || sbase + SLOT > c.hi) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
+      do_row(m, sbase, a, ntok, sl, list);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
   __syncthreads();
   if (m.dict_n) {
     for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
-      const uint32_t n = m.s.dcnt[i];
-      if (n) atomicAdd(&w.dict_tot[i], (unsigned long long)n);
+      const uint32_t cnt = m.s.dcnt[i];
+      if (cnt) atomicAdd(&w.dict_tot[i], (unsigned long long)cnt);
     }
   }
   for (int i = tid; i < NB; i += MAP_THREADS) {
-    const uint32_t n = m.s.bcnt[i];
-    w.cold_n[(uint64_t)blockIdx.x * NB + i] = n < w.cold_cap ? n : w.cold_cap;
-    if (n) atomicMax(&w.ctl->cold_need, n);
+    const uint32_t cnt = m.s.bcnt[i];
+    w.cold_n[(uint64_t)blockIdx.x * NB + i] = cnt < w.cold_cap ? cnt : w.cold_cap;
+    if (cnt) atomicMax(&w.ctl->cold_need, cnt);
   }
   if (tid == 0) {
     const uint32_t sn = m.s.misc[0];
