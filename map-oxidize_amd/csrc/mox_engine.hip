@@ -268,8 +268,8 @@ int alloc_fixed(mox_engine* e) {
   return MOX_OK;
 }
 
-size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_BUCKETS * 4; }  // k_dict_build
-size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
+size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_SLOTS * 4; }  // k_dict_build
+size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
 size_t reduce_lds_bytes() { return 2560 * (8 * 3 + 4) + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP (mox_kernels.hip)
 
 // exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)

@@ -15,12 +15,13 @@ constexpr int ROWBUF = ROW + 32;            // lowered row + 16 B look-ahead + p
 constexpr int TOKMAX = ROW / 2;             // token starts per row (at most every other byte)
 // k_map row ring (LDS): one loader wave streams rows, the other waves consume
 // them.  Slot = 64 lanes x 16 B = [16 B before | PAY payload bytes | 16 B after].
-constexpr int RING = 40;
+constexpr int RING = 32;                    // power of two
 constexpr int SLOT = ROW;
 constexpr int PAY = ROW - 32;               // 992 payload bytes per row
 constexpr int LD_GROUP = 6;                 // loader: rows per register group
 constexpr int LD_GROUPS = 4;                // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
-constexpr int MAP_CONSUMERS = MAP_WAVES - 1;
+constexpr int MAP_LOADERS = 2;              // loader waves (alternate row groups)
+constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
 constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots

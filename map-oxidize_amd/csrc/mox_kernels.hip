@@ -182,32 +182,39 @@ __device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint
 }
 
 // ------------------------------------------------------------------ map kernel
-// 32-bit key hash for short (<= 16 byte) keys: partition = top 8 bits,
-// dictionary buckets and reduce slots use other bits.  Final table order is
-// (h32, key), so it is deterministic.
+// 32-bit key hash of a short (<= 16 byte) key given as 4 little-endian dwords:
+// a rotate/xor fold then a two-round multiply-xorshift finaliser.  Bit use:
+// partition = top NB_LOG2 bits, dictionary home slot = low 12 bits, second
+// dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
+// bits.  Final table order is (h32, key), so it is deterministic.
+__device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t a = k0 ^ __builtin_rotateleft32(k1, 11) ^ __builtin_rotateleft32(k2, 21) ^ __builtin_rotateleft32(k3, 6);
+  a *= 0x9E3779B1u;
+  a ^= a >> 15;
+  a *= 0x85EBCA6Bu;
+  a ^= a >> 13;
+  return a;
+}
 __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
-  uint32_t h = (uint32_t)w0 * 0x9E3779B1u + (uint32_t)(w0 >> 32) * 0x85EBCA77u + (uint32_t)w1 * 0xC2B2AE3Du +
-               (uint32_t)(w1 >> 32) * 0x27D4EB2Fu;
-  h ^= h >> 16;
-  h *= 0x85EBCA6Bu;
-  h ^= h >> 13;
-  h *= 0xC2B2AE35u;
-  h ^= h >> 16;
-  return h;
+  return hash32((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
 }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - NB_LOG2); }
-// the two dictionary buckets of a key (2-choice hashing; the first is preferred)
-__device__ __forceinline__ uint32_t dict_b1(uint32_t h) { return h & (DICT_BUCKETS - 1); }
-__device__ __forceinline__ uint32_t dict_b2(uint32_t h) { return (h >> 10) & (DICT_BUCKETS - 1); }
-
+// Dictionary: DICT_SLOTS slots in groups of 4.  A word sits in its home slot
+// (h mod DICT_SLOTS) when that was free at build time (words are placed
+// hottest first), else in a free slot of its home group, else of its second
+// group.  The token phase checks the home slot first and the two groups only
+// for the tokens that miss there.
+__device__ __forceinline__ uint32_t dict_home(uint32_t h) { return h & (DICT_SLOTS - 1); }
+__device__ __forceinline__ uint32_t dict_g1(uint32_t h) { return (h & (DICT_SLOTS - 1)) >> 2; }
+__device__ __forceinline__ uint32_t dict_g2(uint32_t h) { return (h >> 12) & (DICT_BUCKETS - 1); }
 
 struct MapLds {
   uint4* dtag4;     // DICT_BUCKETS x 4 tags (0 = empty)
   uint4* dkey;      // DICT_SLOTS 16-byte keys
   uint32_t* dcnt;   // DICT_SLOTS
   uint32_t* bcnt;   // NB: cold records this workgroup wrote per partition
-  uint32_t* misc;   // [0] spills
-  uint8_t* wave;    // MAP_WAVES x (ROWBUF + 2 * TOKMAX): lowered row + token list
+  uint32_t* misc;   // [0] spills [1] row ticket
+  uint4* masktab;   // [17]: byte masks keeping the first len bytes of a 16-byte key
 };
 
 struct MapCtx {
@@ -228,17 +235,11 @@ __device__ __forceinline__ int bucket_find(const MapLds& s, uint32_t b, uint4 t,
   if (t.w == h && key_eq(s.dkey[4 * b + 3], w0, w1)) return (int)(4 * b + 3);
   return -1;
 }
-// Dictionary lookup.  Buckets fill slot 0..3 in order and a word goes to its
-// second bucket only when the first was full, so a first bucket with a free
-// slot ends the search.
+// Exact dictionary lookup over both groups of the key.
 __device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w0, uint64_t w1) {
-  const uint32_t b1 = dict_b1(h);
-  const uint4 t1 = s.dtag4[b1];
-  int slot = bucket_find(s, b1, t1, h, w0, w1);
-  if (slot < 0 && t1.w != 0) {
-    const uint32_t b2 = dict_b2(h);
-    slot = bucket_find(s, b2, s.dtag4[b2], h, w0, w1);
-  }
+  const uint32_t g1 = dict_g1(h), g2 = dict_g2(h);
+  int slot = bucket_find(s, g1, s.dtag4[g1], h, w0, w1);
+  if (slot < 0) slot = bucket_find(s, g2, s.dtag4[g2], h, w0, w1);
   return slot;
 }
 
@@ -262,6 +263,14 @@ __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_
 
 // A word not in the dictionary: appended to this workgroup's region of its
 // hash partition (the shuffle write), no global atomics.
+__device__ __forceinline__ void cold_spill(const MapCtx& m, uint4 key) {
+  const uint32_t sp = atomicAdd(&m.s.misc[0], 1u);
+  if (sp < m.w.spill_cap) {
+    m.w.spill[(uint64_t)blockIdx.x * m.w.spill_cap + sp] = key;
+    return;
+  }
+  atomicOr(&m.w.ctl->overflow, OVF_POOL);
+}
 __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
   const uint32_t b = bucket_of(h);
   if (m.w.dbg & DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
@@ -271,12 +280,7 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
     m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
     return;
   }
-  const uint32_t sp = atomicAdd(&m.s.misc[0], 1u);
-  if (sp < m.w.spill_cap) {
-    m.w.spill[(uint64_t)blockIdx.x * m.w.spill_cap + sp] = key;
-    return;
-  }
-  atomicOr(&m.w.ctl->overflow, OVF_POOL);
+  cold_spill(m, key);
 }
 
 // Any token, walked byte by byte from global memory (rare: long tokens, tokens
@@ -391,43 +395,85 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
   return st;
 }
 
-// Token phase for TU batches of 64 tokens (lane = token): key from the LDS row
-// (three 8-byte reads at the 8-aligned start, funnel shift), hash, dictionary
-// tags of both buckets, key check, then LDS count or cold emission.
+// Key of list entry e from the lowered slot: 24 bytes read at the 8-aligned
+// start, byte-aligned with v_alignbyte, masked to len bytes.
+__device__ __forceinline__ void key_at(const MapLds& s, const uint8_t* rowbuf, uint32_t e, uint32_t (&K)[4]) {
+  const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
+  const uint2* q = reinterpret_cast<const uint2*>(rowbuf + (pos & ~7u));
+  const uint2 A = q[0], B = q[1], C = q[2];
+  const uint4 M = s.masktab[len];
+  const bool o = (pos & 4u) != 0;
+  const uint32_t E0 = o ? A.y : A.x, E1 = o ? B.x : A.y, E2 = o ? B.y : B.x, E3 = o ? C.x : B.y, E4 = o ? C.y : C.x;
+  const uint32_t sh = pos & 3u;
+  K[0] = __builtin_amdgcn_alignbyte(E1, E0, sh) & M.x;
+  K[1] = __builtin_amdgcn_alignbyte(E2, E1, sh) & M.y;
+  K[2] = __builtin_amdgcn_alignbyte(E3, E2, sh) & M.z;
+  K[3] = __builtin_amdgcn_alignbyte(E4, E3, sh) & M.w;
+}
+__device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
+  return ((k.x ^ K[0]) | (k.y ^ K[1]) | (k.z ^ K[2]) | (k.w ^ K[3])) == 0;
+}
+
+// Token pass A over TU batches of 64 list entries (lane = token): key, hash,
+// one LDS read of the home slot.  Hits count in LDS; misses are compacted in
+// place to the front of the list (entry index <= read index, and every read of
+// this call precedes its writes).  Returns the new miss count.
 template <int TU>
-__device__ __forceinline__ void token_batches(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                              uint32_t total, bool use_dict) {
+__device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbuf, uint16_t* list, uint32_t j0,
+                                           uint32_t total, uint32_t nmiss, bool use_dict) {
   const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t e[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
     e[u] = j < total ? (uint32_t)list[j] : 0x8000u;  // inactive = odd
   }
-  uint64_t w0[TU], w1[TU];
-  uint32_t h[TU];
+  bool hit[TU];
+  uint32_t home[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    const uint32_t pos = e[u] & 1023u, len = (e[u] >> 10) & 31u;
-    const uint64_t* q = reinterpret_cast<const uint64_t*>(rowbuf + (pos & ~7u));
-    const uint64_t Q0 = q[0], Q1 = q[1], Q2 = q[2];
-    const uint32_t r = (pos & 7u) * 8u;
-    uint64_t a0 = (Q0 >> r) | ((Q1 << 1) << (63u - r));
-    uint64_t a1 = (Q1 >> r) | ((Q2 << 1) << (63u - r));
-    const uint64_t m0 = len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1ull);
-    const uint64_t m1 = len <= 8 ? 0ull : (len >= 16 ? ~0ull : ((1ull << (8 * (len - 8))) - 1ull));
-    a0 &= m0;
-    a1 &= m1;
-    w0[u] = a0;
-    w1[u] = a1;
-    h[u] = key_hash(a0, a1);
+    uint32_t K[4];
+    key_at(m.s, rowbuf, e[u], K);
+    const uint32_t h = hash32(K[0], K[1], K[2], K[3]);
+    home[u] = dict_home(h);
+    hit[u] = use_dict && key_eq4(m.s.dkey[home[u]], K);
   }
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const bool valid = !(e[u] & 0x8000u);
+    if (valid && hit[u] && !(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[home[u]], 1u);
+    const bool miss = valid && !hit[u];
+    const uint64_t bm = __ballot(miss);
+    if (miss) list[nmiss + (uint32_t)__popcll(bm & lt)] = (uint16_t)e[u];
+    nmiss += (uint32_t)__popcll(bm);
+  }
+  return nmiss;
+}
+
+// Token pass B over TU batches of 64 compacted misses: both dictionary groups
+// (8 tags), key check, then an LDS count or the cold store.
+template <int TU>
+__device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
+                                       uint32_t nmiss, bool use_dict) {
+  const int lane = threadIdx.x & 63;
+  uint32_t e[TU];
+  bool valid[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const uint32_t j = j0 + u * 64 + lane;
+    valid[u] = j < nmiss;
+    e[u] = valid[u] ? (uint32_t)list[j] : 0u;
+  }
+  uint32_t K[TU][4], h[TU];
   int slot[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
+    key_at(m.s, rowbuf, e[u], K[u]);
+    h[u] = hash32(K[u][0], K[u][1], K[u][2], K[u][3]);
     slot[u] = -1;
     if (use_dict) {
-      const uint32_t b1 = dict_b1(h[u]), b2 = dict_b2(h[u]);
+      const uint32_t b1 = dict_g1(h[u]), b2 = dict_g2(h[u]);
       const uint4 t1 = m.s.dtag4[b1], t2 = m.s.dtag4[b2];
       int sl = t2.w == h[u] ? (int)(4 * b2 + 3) : -1;
       sl = t2.z == h[u] ? (int)(4 * b2 + 2) : sl;
@@ -442,22 +488,20 @@ __device__ __forceinline__ void token_batches(const MapCtx& m, const uint8_t* ro
   }
   bool hit[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) {
-    const uint4 kq = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
-    hit[u] = slot[u] >= 0 && key_eq(kq, w0[u], w1[u]);
-  }
+  for (int u = 0; u < TU; u++) hit[u] = slot[u] >= 0 && key_eq4(m.s.dkey[slot[u] < 0 ? 0 : slot[u]], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    if (e[u] & 0x8000u) continue;
+    if (!valid[u]) continue;
+    const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
     if (hit[u]) {
       if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
       continue;
     }
     if (slot[u] >= 0) {  // tag matched another word: full search (rare)
-      const int s2 = dict_find(m.s, h[u], w0[u], w1[u]);
+      const int s2 = dict_find(m.s, h[u], w0, w1);
       if (s2 >= 0) { atomicAdd(&m.s.dcnt[s2], 1u); continue; }
     }
-    cold_word(m, h[u], w0[u], w1[u]);
+    cold_word(m, h[u], w0, w1);
   }
 }
 
@@ -469,7 +513,7 @@ __device__ __forceinline__ void token_batches(const MapCtx& m, const uint8_t* ro
 //     Unicode walk on rows with non-ASCII bytes), the lowered slot back into LDS
 //     and a compacted list of token (slot offset, length) in row order (wave
 //     prefix sum of per-lane start counts from 5 bit-sliced ballots);
-//  2. token phase (lane = token), see token_batches.
+//  2. token phase (lane = token): pass_a over all tokens, pass_b over its misses.
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
                                        uint16_t* list) {
   const int lane = threadIdx.x & 63;
@@ -538,25 +582,30 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   }
   if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
   const bool use_dict = m.dict_n && !(m.w.dbg & DBG_NO_DICT);
+  uint32_t nmiss = 0;
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
-    if (rem > 192) { token_batches<4>(m, rowbuf, list, j0, total, use_dict); j0 += 256; }
-    else if (rem > 128) { token_batches<3>(m, rowbuf, list, j0, total, use_dict); j0 += 192; }
-    else if (rem > 64) { token_batches<2>(m, rowbuf, list, j0, total, use_dict); j0 += 128; }
-    else { token_batches<1>(m, rowbuf, list, j0, total, use_dict); j0 += 64; }
+    if (rem > 128) { nmiss = pass_a<3>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 192; }
+    else if (rem > 64) { nmiss = pass_a<2>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 128; }
+    else { nmiss = pass_a<1>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 64; }
+  }
+  wave_lds_fence();
+  for (uint32_t j0 = 0; j0 < nmiss;) {
+    if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 128; }
+    else { pass_b<1>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 64; }
   }
   wave_lds_fence();
 }
 
 // Map kernel.  One persistent 1024-thread workgroup per CU owns a contiguous
 // range of rows (992 payload bytes each).
-//  * wave 0 = loader: streams each row's slot (payload +16 B either side) with
+//  * waves 0..MAP_LOADERS-1 = loaders (alternate row groups): stream each row's slot (payload +16 B either side) with
 //    16 B/lane loads into registers, LD_GROUPS groups of LD_GROUP rows in
 //    flight, and copies each into a free ring slot with ds_write, then
 //    publishes the slot (flag written after the data by the same wave, so DS
 //    ordering makes the hand-off safe).  It issues no stores to memory, so its
 //    vmcnt waits are exact.
-//  * waves 1..15 = consumers: take rows in order by ticket (dynamic load
+//  * the other waves = consumers: take rows in order by ticket (dynamic load
 //    balance), process them from LDS (do_row) and release the slot.  Their
 //    cold-record stores are never waited for inside the loop.
 extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t nrows) {
@@ -570,6 +619,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
   m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
+  m.s.masktab = (uint4*)sp; sp += 17 * 16;
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
@@ -583,6 +633,15 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   for (int i = tid; i < NB; i += MAP_THREADS) m.s.bcnt[i] = 0;
   if (tid < 4) m.s.misc[tid] = 0;
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
+  if (tid < 17) {
+    uint32_t mk[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int c = tid - 4 * i;  // bytes kept in dword i
+      mk[i] = c <= 0 ? 0u : (c >= 4 ? ~0u : ((1u << (8 * c)) - 1u));
+    }
+    m.s.masktab[tid] = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+  }
   __syncthreads();
   unsigned long long ntok = 0;
 
@@ -592,8 +651,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   const uint64_t rb = blockIdx.x * per + (blockIdx.x < rem ? blockIdx.x : rem);
   const uint32_t n = (uint32_t)(per + (blockIdx.x < rem ? 1 : 0));
 
-  if (wv == 0) {
-    // ---------------- loader
+  if (wv < MAP_LOADERS) {
+    // ---------------- loaders: loader wv owns row groups wv, wv + MAP_LOADERS, ...
     uint4 buf[LD_GROUPS][LD_GROUP];
     auto issue = [&](uint4 (&b)[LD_GROUP], uint32_t t0) {
 #pragma unroll
@@ -603,33 +662,44 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
       }
     };
     auto retire = [&](const uint4 (&b)[LD_GROUP], uint32_t t0) {
+      // wait until every slot of the group is free (one batch of LDS reads per poll)
+      for (;;) {
+        bool ok = true;
 #pragma unroll
-      for (int i = 0; i < LD_GROUP; i++) {
-        const uint32_t t = t0 + i;
-        if (t >= n) break;
-        const uint32_t slot = t % RING;
-        if (t >= RING) {
-          while (__hip_atomic_load(&sfree[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t - RING + 1)
-            __builtin_amdgcn_s_sleep(1);
+        for (int i = 0; i < LD_GROUP; i++) {
+          const uint32_t t = t0 + i;
+          if (t >= RING && t < n)
+            ok &= __hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == t - RING + 1;
         }
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        reinterpret_cast<uint4*>(ring + slot * SLOT)[lane] = b[i];
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0) __hip_atomic_store(&sready[slot], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (ok) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+      for (int i = 0; i < LD_GROUP; i++)
+        if (t0 + i < n) reinterpret_cast<uint4*>(ring + ((t0 + i) % RING) * SLOT)[lane] = b[i];
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (lane == 0) {
+#pragma unroll
+        for (int i = 0; i < LD_GROUP; i++)
+          if (t0 + i < n) __hip_atomic_store(&sready[(t0 + i) % RING], t0 + i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     };
+    __builtin_amdgcn_s_setprio(3);  // the loader feeds 15 consumers: never let it lose issue arbitration
+    constexpr uint32_t STRIDE = MAP_LOADERS * LD_GROUP;  // rows between this loader's consecutive groups
+    const uint32_t first = wv * LD_GROUP;
 #pragma unroll
-    for (int g = 0; g < LD_GROUPS - 1; g++) issue(buf[g], g * LD_GROUP);
-    for (uint32_t t0 = 0; t0 < n; t0 += LD_GROUPS * LD_GROUP) {
+    for (int g = 0; g < LD_GROUPS - 1; g++) issue(buf[g], first + g * STRIDE);
+    for (uint32_t t0 = first; t0 < n; t0 += LD_GROUPS * STRIDE) {
 #pragma unroll
       for (int g = 0; g < LD_GROUPS; g++) {
-        issue(buf[(g + LD_GROUPS - 1) % LD_GROUPS], t0 + (g + LD_GROUPS - 1) * LD_GROUP);
-        retire(buf[g], t0 + g * LD_GROUP);
+        issue(buf[(g + LD_GROUPS - 1) % LD_GROUPS], t0 + (g + LD_GROUPS - 1) * STRIDE);
+        retire(buf[g], t0 + g * STRIDE);
       }
     }
   } else {
     // ---------------- consumers
-    uint16_t* list = lists + (wv - 1) * TOKMAX;
+    uint16_t* list = lists + (wv - MAP_LOADERS) * TOKMAX;
     for (;;) {
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
@@ -748,13 +818,12 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
   unsigned long long* ck0 = (unsigned long long*)smem;
   unsigned long long* ck1 = ck0 + CAND_SLOTS;
   uint32_t* ccnt = (uint32_t*)(ck1 + CAND_SLOTS);
-  uint32_t* fill = ccnt + CAND_SLOTS;  // DICT_BUCKETS
+  uint32_t* ltag = ccnt + CAND_SLOTS;  // DICT_SLOTS tags being placed
   __shared__ uint32_t hist[64], fine[256];
   __shared__ uint32_t nsel, thresh_lo, cls;
   const int tid = threadIdx.x;
   for (int i = tid; i < CAND_SLOTS; i += 1024) { ck0[i] = 0; ck1[i] = 0; ccnt[i] = 0; }
-  for (int i = tid; i < DICT_BUCKETS; i += 1024) fill[i] = 0;
-  for (int i = tid; i < DICT_SLOTS; i += 1024) { w.dict_tag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
+  for (int i = tid; i < DICT_SLOTS; i += 1024) { ltag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
   if (tid < 64) hist[tid] = 0;
   if (tid < 256) fine[tid] = 0;
   if (tid == 0) nsel = 0;
@@ -822,16 +891,24 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
       const uint64_t w0 = ck0[i], w1 = ck1[i] & ~(1ull << 63);
       const uint32_t h = key_hash(w0, w1);
       if (h == 0) continue;  // tag 0 marks an empty slot
-      uint32_t b = dict_b1(h);
-      uint32_t f = atomicAdd(&fill[b], 1u);
-      if (f >= 4) { b = dict_b2(h); f = atomicAdd(&fill[b], 1u); }
-      if (f >= 4) continue;  // both buckets full: this word stays cold
-      w.dict_tag[4 * b + f] = h;
-      w.dict_key[4 * b + f] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+      // home slot, else a free slot of the home group, else of the second group
+      int slot = -1;
+      if (atomicCAS(&ltag[dict_home(h)], 0u, h) == 0u) slot = (int)dict_home(h);
+      for (int i = 0; i < 4 && slot < 0; i++) {
+        const uint32_t s1 = 4 * dict_g1(h) + i;
+        if (atomicCAS(&ltag[s1], 0u, h) == 0u) slot = (int)s1;
+      }
+      for (int i = 0; i < 4 && slot < 0; i++) {
+        const uint32_t s2 = 4 * dict_g2(h) + i;
+        if (atomicCAS(&ltag[s2], 0u, h) == 0u) slot = (int)s2;
+      }
+      if (slot < 0) continue;  // both groups full: this word stays cold
+      w.dict_key[slot] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
       atomicAdd(&nsel, 1u);
     }
     __syncthreads();
   }
+  for (int i = tid; i < DICT_SLOTS; i += 1024) w.dict_tag[i] = ltag[i];
   if (tid == 0) { w.ctl->dict_n = nsel; w.ctl->dict_thresh = thresh_lo; }
 }
 
