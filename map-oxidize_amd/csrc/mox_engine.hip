@@ -270,7 +270,7 @@ int alloc_fixed(mox_engine* e) {
 
 size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_SLOTS * 4; }  // k_dict_build
 size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
-size_t reduce_lds_bytes() { return 2560 * (8 * 3 + 4) + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP (mox_kernels.hip)
+size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
 
 // exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)
 int launch_scan(mox_engine* e, const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
@@ -428,6 +428,18 @@ int run_corpus(mox_engine* e, const Corpus& c) {
       fprintf(stderr, "[mox] attempt %d: overflow 0x%x cold_need %llu spill_need %llu w_total %llu u_n %llu n_total %llu caps cold %u spill %u w %llu run %.3f ms\n",
               attempt, h.overflow, h.cold_need, h.spill_need, h.w_total, h.u_n, h.n_total, e->w.cold_cap, e->w.spill_cap,
               (unsigned long long)e->w.w_cap, e->stats.ms_run);
+    if ((e->w.dbg & DBG_STAMP) && e->w.stamps) {
+      std::vector<unsigned long long> st(8 * NB);
+      (void)hipMemcpy(st.data(), e->w.stamps, st.size() * 8, hipMemcpyDeviceToHost);
+      FILE* f = fopen("gpurun_out/stamps.csv", "w");
+      if (f) {
+        for (int i = 0; i < NB; i++)
+          fprintf(f, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, st[8 * i], st[8 * i + 1], st[8 * i + 2], st[8 * i + 3], st[8 * i + 4], st[8 * i + 5], st[8 * i + 6]);
+        fclose(f);
+      }
+    }
+    if (getenv("MOX_VERBOSE"))
+      fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu\n", h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3]);
     if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
     if (h.halo_err != ~0ull)
       return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
@@ -754,6 +766,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
   if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
+  if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096);
   e->sync_each = getenv("MOX_SYNC_EACH") != nullptr;
   int rc = alloc_fixed(e);
   if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));

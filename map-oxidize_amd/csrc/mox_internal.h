@@ -40,7 +40,8 @@ constexpr uint64_t LONG_TAG = 0xFF00000000000000ull;   // w1 marker of a hashed 
 constexpr uint64_t LONG_LEN_MASK = 0x0000FFFFFFFFFFFFull;
 constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points into the arena
 
-enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u };
+enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u,
+                  DBG_RED_NOSORT = 32u, DBG_RED_NOINSERT = 64u, DBG_RED_NOSLOW = 128u, DBG_COUNT = 256u, DBG_RED_PLAINADD = 512u, DBG_STAMP = 1024u };
 enum : uint32_t {
   OVF_POOL = 1u, OVF_W = 2u, OVF_U = 4u, OVF_LONG = 8u, OVF_ARENA = 16u, OVF_PROBE = 32u,
   OVF_TABLE = 64u, OVF_BYTES = 128u, OVF_REDUCE = 256u,
@@ -71,6 +72,7 @@ struct Ctl {
   unsigned long long cold_need;   // max records any (workgroup, partition) region asked for
   unsigned long long spill_need;  // max spill records of any map workgroup
   unsigned long long w_total;     // weighted + spilled records
+  unsigned long long dbg_cnt[4];  // MOX_DBG & DBG_COUNT instrumentation
 };
 
 // Weighted record: a key with a count (dictionary totals, spills, Unicode-lane
@@ -189,6 +191,7 @@ struct Work {  // device buffers of one engine
   // scan scratch
   uint64_t* scan_part;            // SCAN_WGS + 1
   uint32_t dbg;                   // ablation switches (MOX_DBG env), 0 in production
+  unsigned long long* stamps;     // DBG_STAMP: per-workgroup phase timestamps (8 per workgroup)
 };
 
 }  // namespace mox

@@ -1113,84 +1113,144 @@ extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {  // same 
 // ------------------------------------------------------------------ bucket reduce
 // One workgroup per partition (2 per CU): group its cold records (count 1, one
 // contiguous region per map workgroup, streamed by one wave per region) and its
-// weighted records by exact 16-byte key in an LDS hash table, sort the distinct
-// keys by (h32, key) with an LDS bitonic sort and write them out.  A partition
-// with more distinct keys than the table holds is redone in 2^k sub-passes over
-// the next hash bits.
-constexpr int RED_SLOTS = 2560;
+// weighted records by exact 16-byte key in an LDS hash table of RED_BK buckets
+// x 4 slots (one ds_read_b128 of tags resolves a probe), sort the distinct keys
+// by (h32, key) with an LDS bitonic sort and write them out.  A partition with
+// more distinct keys than RED_CAP is redone in 2^k sub-passes over the next
+// hash bits.
+constexpr int RED_BK = 608;    // 2 workgroups per CU: table + sort scratch <= 80 KiB
+constexpr int RED_SLOTS = 4 * RED_BK;
 constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort width
-constexpr int RED_UNROLL = 4;
+constexpr int RED_UNROLL = 2;
+constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
 
 struct RedLds {
-  unsigned long long* k0;  // RED_SLOTS (0 = free)
-  unsigned long long* k1;  // RED_SLOTS
-  unsigned long long* cnt; // RED_SLOTS (0 = not yet published)
-  uint32_t* hh;            // RED_SLOTS key hash
-  uint16_t* idx;           // RED_CAP
+  uint4* tag4;             // RED_BK x 4 key hashes (0 = free)
+  uint4* key;              // RED_SLOTS
+  unsigned long long* cnt; // RED_SLOTS (0 = claimed, not yet published)
+  uint16_t* idx;           // RED_CAP: slots in output order
+  uint16_t* bin;           // RED_SORTB + 1: bin counts, then bin starts (exclusive scan)
+  uint16_t* fill;          // RED_SORTB: bin fill cursors
   uint32_t* misc;          // [0] uniques [1] overflow [2] compaction cursor
+  uint32_t* dbg;           // DBG_COUNT: [0] slow inserts [1] slow iterations [2] publication retries
+  bool plain;
 };
 
-__device__ __forceinline__ uint32_t red_slot(uint32_t h) {
-  return (uint32_t)(((uint64_t)(h * 0x9E3779B1u) * RED_SLOTS) >> 32);
+// hash bits used: partition = top NB_LOG2 bits, sub-pass = the next kk bits,
+// bucket = a multiplicative hash of the low bits
+__device__ __forceinline__ uint32_t red_bucket(uint32_t h) {
+  return (uint32_t)(((uint64_t)((h * 0x9E3779B1u) >> 8) * RED_BK) >> 24);
 }
+__device__ __forceinline__ bool key_eq16(uint4 a, uint4 b) { return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) == 0; }
 
-// Exact insert.  A slot is claimed by CAS on k0 (short keys have a non-zero
-// first byte, so w0 != 0); the claimant then stores k1, hh and finally
-// publishes cnt (> 0).  Readers retry a slot whose cnt is still 0: the
-// claimant's stores run in the same loop iteration, so no lane waits on a
-// lane that cannot make progress.
-__device__ __forceinline__ void red_insert(const RedLds& s, uint32_t h, uint64_t w0, uint64_t w1, uint64_t c) {
-  uint32_t slot = red_slot(h);
-  for (uint32_t it = 0; it < 4 * RED_SLOTS; it++) {
-    unsigned long long cur = s.k0[slot];
-    if (cur == 0) {
-      cur = atomicCAS(&s.k0[slot], 0ull, (unsigned long long)w0);
-      if (cur == 0) {
-        s.k1[slot] = w1;
-        s.hh[slot] = h;
-        __threadfence_block();
-        atomicAdd(&s.cnt[slot], (unsigned long long)c);
+// Exact insert (slow path).  A slot is claimed by CAS on its tag (keys with tag
+// h fill the first free slot of the first bucket with room, so every insert of
+// one key walks the same buckets); the claimant then stores the key and
+// publishes cnt (> 0).  Readers retry a matching slot whose cnt is still 0.
+__device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
+  uint32_t b = red_bucket(h);
+  if (s.dbg) atomicAdd(&s.dbg[0], 1u);
+  const uint32_t* tags = reinterpret_cast<const uint32_t*>(s.tag4);
+  for (uint32_t it = 0; it < 64u * RED_BK;) {
+    const uint4 t = s.tag4[b];
+    const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
+    bool retry = false;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (tv[i] != h) continue;
+      const uint32_t sl = 4 * b + i;
+      if (__hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) { retry = true; break; }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (key_eq16(s.key[sl], k)) { atomicAdd(&s.cnt[sl], (unsigned long long)c); return; }
+    }
+    if (s.dbg) atomicAdd(&s.dbg[1], 1u);
+    if (retry) { if (s.dbg) atomicAdd(&s.dbg[2], 1u); it++; continue; }
+    int e = -1;
+#pragma unroll
+    for (int i = 3; i >= 0; i--) if (tv[i] == 0) e = i;
+    if (e >= 0) {
+      const uint32_t sl = 4 * b + e;
+      if (atomicCAS(const_cast<uint32_t*>(&tags[sl]), 0u, h) == 0u) {
+        s.key[sl] = k;
+        __atomic_signal_fence(__ATOMIC_SEQ_CST);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        atomicAdd(&s.cnt[sl], (unsigned long long)c);
         const uint32_t u = atomicAdd(&s.misc[0], 1u);
         if (u >= RED_CAP) s.misc[1] = 1;
         return;
       }
+      it++;
+      continue;  // lost the slot: re-read this bucket
     }
-    if (cur == w0) {
-      if (__atomic_load_n(&s.cnt[slot], __ATOMIC_RELAXED) == 0) continue;  // claimant still publishing
-      __threadfence_block();
-      if (s.k1[slot] == w1) { atomicAdd(&s.cnt[slot], (unsigned long long)c); return; }
-    }
-    slot = slot + 1 == RED_SLOTS ? 0 : slot + 1;
+    b = b + 1 == RED_BK ? 0 : b + 1;
+    it++;
   }
   s.misc[1] = 1;
+}
+
+// Fast path for records whose key is already published in its home bucket or
+// the next one (keys overflow at most one bucket at this table load): two tag
+// reads issued together, one key read, one add.  Returns false when the slow
+// path is needed (new key, further bucket, publication pending).
+__device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
+  const uint32_t b = red_bucket(h), b2 = b + 1 == RED_BK ? 0 : b + 1;
+  const uint4 t = s.tag4[b], t2 = s.tag4[b2];
+  int sl = t2.w == h ? (int)(4 * b2 + 3) : -1;
+  sl = t2.z == h ? (int)(4 * b2 + 2) : sl;
+  sl = t2.y == h ? (int)(4 * b2 + 1) : sl;
+  sl = t2.x == h ? (int)(4 * b2 + 0) : sl;
+  sl = t.w == h ? (int)(4 * b + 3) : sl;
+  sl = t.z == h ? (int)(4 * b + 2) : sl;
+  sl = t.y == h ? (int)(4 * b + 1) : sl;
+  sl = t.x == h ? (int)(4 * b + 0) : sl;
+  if (sl < 0) return false;
+  const uint4 kk = s.key[sl];
+  const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (cv == 0 || !key_eq16(kk, k)) return false;
+  if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
+  else atomicAdd(&s.cnt[sl], (unsigned long long)c);
+  return true;
 }
 
 __device__ __forceinline__ bool red_less(const RedLds& s, uint16_t a, uint16_t b) {
   if (a == 0xFFFF) return false;
   if (b == 0xFFFF) return true;
-  if (s.hh[a] != s.hh[b]) return s.hh[a] < s.hh[b];
-  if (s.k0[a] != s.k0[b]) return s.k0[a] < s.k0[b];
-  return s.k1[a] < s.k1[b];
+  const uint32_t* tags = reinterpret_cast<const uint32_t*>(s.tag4);
+  if (tags[a] != tags[b]) return tags[a] < tags[b];
+  const uint4 ka = s.key[a], kb = s.key[b];
+  const uint64_t a0 = ((uint64_t)ka.y << 32) | ka.x, b0 = ((uint64_t)kb.y << 32) | kb.x;
+  if (a0 != b0) return a0 < b0;
+  return (((uint64_t)ka.w << 32) | ka.z) < (((uint64_t)kb.w << 32) | kb.z);
 }
 
 __device__ __forceinline__ bool in_sub(uint32_t h, uint32_t kk, uint32_t sub) {
   return kk == 0 || ((h << NB_LOG2) >> (32 - kk)) == sub;
 }
 
-extern "C" __global__ __launch_bounds__(RED_THREADS) void k_reduce(Work w) {
+// sort bin of a key hash: the RED_SORTB-way split of the bits right below the
+// partition bits (ascending bin = ascending hash within the partition)
+__device__ __forceinline__ uint32_t red_bin(uint32_t h) { return (h << NB_LOG2) >> (32 - 11); }
+
+extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) {  // 8 waves per SIMD: 2 workgroups per CU
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   RedLds s;
   uint8_t* sp = smem;
-  s.k0 = (unsigned long long*)sp; sp += RED_SLOTS * 8;
-  s.k1 = (unsigned long long*)sp; sp += RED_SLOTS * 8;
+  s.tag4 = (uint4*)sp; sp += RED_SLOTS * 4;
+  s.key = (uint4*)sp; sp += RED_SLOTS * 16;
   s.cnt = (unsigned long long*)sp; sp += RED_SLOTS * 8;
-  s.hh = (uint32_t*)sp; sp += RED_SLOTS * 4;
   s.idx = (uint16_t*)sp; sp += RED_CAP * 2;
+  s.bin = (uint16_t*)sp; sp += (RED_SORTB + 8) * 2;
+  s.fill = (uint16_t*)sp; sp += RED_SORTB * 2;
   s.misc = (uint32_t*)sp; sp += 16;
+  __shared__ uint32_t dbgc[4];
+  s.dbg = (w.dbg & DBG_COUNT) ? dbgc : nullptr;
+  s.plain = (w.dbg & DBG_RED_PLAINADD) != 0;
+  if (threadIdx.x < 4) dbgc[threadIdx.x] = 0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NWV = RED_THREADS / 64;
   const uint32_t b = blockIdx.x;
   const uint32_t G = w.map_grid;
+  uint32_t* tags = reinterpret_cast<uint32_t*>(s.tag4);
   // an overflowed map or directory means this attempt is rerun with larger
   // buffers: its records are incomplete (w_sorted may not even be written)
   if (w.ctl->overflow & OVF_RERUN) {
@@ -1199,37 +1259,74 @@ extern "C" __global__ __launch_bounds__(RED_THREADS) void k_reduce(Work w) {
   }
   const uint64_t ws0 = w.w_off[b], ws1 = w.w_off[b + 1];
   const uint64_t out0 = w.rec_off[b];
+  const bool stamp = (w.dbg & DBG_STAMP) && tid == 0;
+  if (stamp) w.stamps[b * 8 + 0] = __builtin_amdgcn_s_memrealtime();
   uint32_t kk = 0;
   uint64_t written = 0;
   for (uint32_t sub = 0; sub < (1u << kk);) {
-    for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { s.k0[i] = 0; s.cnt[i] = 0; }
+    for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
     if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
     __syncthreads();
-    // cold regions: wave wv streams regions g = wv, wv + NWV, ...
-    for (uint32_t g = wv; g < G; g += NWV) {
-      const uint32_t n = w.cold_n[(uint64_t)g * NB + b];
-      const uint4* reg = w.cold + ((uint64_t)g * NB + b) * w.cold_cap;
-      for (uint32_t i0 = 0; i0 < n; i0 += 64 * RED_UNROLL) {
-        uint4 v[RED_UNROLL];
+    // cold regions: wave wv streams regions g = wv, wv + NWV, ... in chunks of
+    // 64 x RED_UNROLL records, the next chunk's loads in flight while the
+    // current one is inserted.  Lane k holds the size of the wave's k-th region.
+    {
+      const uint32_t nreg = G > (uint32_t)wv ? (G - wv + NWV - 1) / NWV : 0;  // <= 64 (G <= MAX_MAP_GRID)
+      const uint32_t myn = lane < (int)nreg ? w.cold_n[(uint64_t)(wv + lane * NWV) * NB + b] : 0u;
+      const uint64_t nonempty = __ballot(myn != 0);
+      auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
+        const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
+        return m ? (uint32_t)__builtin_ctzll(m) : nreg;
+      };
+      auto load = [&](uint32_t k, uint32_t i0, uint4 (&v)[RED_UNROLL]) {
+        const uint32_t n = __builtin_amdgcn_readlane(myn, k);
+        const uint4* reg = w.cold + ((uint64_t)(wv + k * NWV) * NB + b) * w.cold_cap;
 #pragma unroll
         for (int u = 0; u < RED_UNROLL; u++) {
           const uint32_t i = i0 + u * 64 + lane;
           v[u] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
         }
-        if (__atomic_load_n(&s.misc[1], __ATOMIC_RELAXED)) break;  // this pass is redone anyway
+      };
+      uint32_t k = next_region(0), i0 = 0;
+      uint4 cur[RED_UNROLL], nxt[RED_UNROLL];
+      if (k < nreg) load(k, 0, cur);
+      while (k < nreg) {
+        uint32_t k2 = k, i2 = i0 + 64 * RED_UNROLL;
+        if (i2 >= __builtin_amdgcn_readlane(myn, k)) { k2 = next_region(k + 1); i2 = 0; }
+        if (k2 < nreg) load(k2, i2, nxt);
+        if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // else: redone anyway
+          uint32_t h[RED_UNROLL];
+          bool todo[RED_UNROLL];
 #pragma unroll
-        for (int u = 0; u < RED_UNROLL; u++) {
-          if ((v[u].x | v[u].y) == 0) continue;
-          const uint64_t w0 = ((uint64_t)v[u].y << 32) | v[u].x, w1 = ((uint64_t)v[u].w << 32) | v[u].z;
-          const uint32_t h = key_hash(w0, w1);
-          if (in_sub(h, kk, sub)) red_insert(s, h, w0, w1, 1);
+          for (int u = 0; u < RED_UNROLL; u++) {
+            h[u] = hash32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
+            todo[u] = (cur[u].x | cur[u].y) != 0 && in_sub(h[u], kk, sub);
+          }
+          if (!(w.dbg & DBG_RED_NOINSERT)) {
+#pragma unroll
+            for (int u = 0; u < RED_UNROLL; u++)
+              if (todo[u]) todo[u] = !red_try(s, h[u], cur[u], 1);
+#pragma unroll
+            for (int u = 0; u < RED_UNROLL; u++)
+              if (todo[u] && !(w.dbg & DBG_RED_NOSLOW)) red_insert(s, h[u], cur[u], 1);
+          } else {
+            asm volatile("" ::"v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
+          }
         }
+#pragma unroll
+        for (int u = 0; u < RED_UNROLL; u++) cur[u] = nxt[u];
+        k = k2;
+        i0 = i2;
       }
     }
+    if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
     for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
       const WRec rr = w.w_sorted[i];
-      const uint32_t h = key_hash(rr.w0, rr.w1);
-      if (!__atomic_load_n(&s.misc[1], __ATOMIC_RELAXED) && in_sub(h, kk, sub)) red_insert(s, h, rr.w0, rr.w1, rr.count);
+      const uint4 k = make_uint4((uint32_t)rr.w0, (uint32_t)(rr.w0 >> 32), (uint32_t)rr.w1, (uint32_t)(rr.w1 >> 32));
+      const uint32_t h = hash32(k.x, k.y, k.z, k.w);
+      if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && in_sub(h, kk, sub) &&
+          !red_try(s, h, k, rr.count))
+        red_insert(s, h, k, rr.count);
     }
     __syncthreads();
     if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the partition
@@ -1243,39 +1340,66 @@ extern "C" __global__ __launch_bounds__(RED_THREADS) void k_reduce(Work w) {
       __syncthreads();
       continue;
     }
-    // compact + bitonic sort by (h32, key) for a deterministic order
+    // deterministic order (h32, key): bucket sort by the hash bits below the
+    // partition bits, then (h32, key) insertion sort inside each bin (~0.7 keys)
+    if (stamp) w.stamps[b * 8 + 2] = __builtin_amdgcn_s_memrealtime();  // all waves done inserting
     const uint32_t nu = s.misc[0];
+    for (int i = tid; i < RED_SORTB; i += RED_THREADS) { s.bin[i] = 0; s.fill[i] = 0; }
+    __syncthreads();
     for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
-      if (s.cnt[i]) { const uint32_t p = atomicAdd(&s.misc[2], 1u); s.idx[p] = (uint16_t)i; }
+      if (tags[i]) atomicAdd(reinterpret_cast<uint32_t*>(s.bin) + (red_bin(tags[i]) >> 1), 1u << (16 * (red_bin(tags[i]) & 1)));
     __syncthreads();
-    uint32_t N = 1;
-    while (N < nu) N <<= 1;
-    for (uint32_t i = nu + tid; i < N; i += RED_THREADS) s.idx[i] = 0xFFFF;
+    {  // exclusive scan of the RED_SORTB bin counts (2 per thread)
+      __shared__ uint64_t wsum[RED_THREADS / 64];
+      uint64_t tot;
+      const uint32_t c0 = s.bin[2 * tid], c1 = s.bin[2 * tid + 1];
+      const uint64_t ex = block_exscan(c0 + c1, wsum, tot);
+      s.bin[2 * tid] = (uint16_t)ex;
+      s.bin[2 * tid + 1] = (uint16_t)(ex + c0);
+      if (tid == 0) s.bin[RED_SORTB] = (uint16_t)tot;
+    }
     __syncthreads();
-    for (uint32_t size = 2; size <= N; size <<= 1) {
-      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-        for (uint32_t i = tid; i < N / 2; i += RED_THREADS) {
-          const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
-          const bool up = (lo & size) == 0;
-          const uint16_t a = s.idx[lo], c2 = s.idx[hi];
-          if (up ? red_less(s, c2, a) : red_less(s, a, c2)) { s.idx[lo] = c2; s.idx[hi] = a; }
+    for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
+      if (tags[i]) {
+        const uint32_t bn = red_bin(tags[i]);
+        const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(s.fill) + (bn >> 1), 1u << (16 * (bn & 1)));
+        const uint32_t p = s.bin[bn] + ((old >> (16 * (bn & 1))) & 0xFFFFu);
+        s.idx[p] = (uint16_t)i;
+      }
+    __syncthreads();
+    if (!(w.dbg & DBG_RED_NOSORT)) {
+      for (int bn = tid; bn < RED_SORTB; bn += RED_THREADS) {
+        const uint32_t lo = s.bin[bn], hi = s.bin[bn + 1];
+        for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort of a tiny bin
+          const uint16_t x = s.idx[i];
+          uint32_t j = i;
+          while (j > lo && red_less(s, x, s.idx[j - 1])) { s.idx[j] = s.idx[j - 1]; j--; }
+          s.idx[j] = x;
         }
-        __syncthreads();
       }
     }
+    __syncthreads();
+    if (stamp) w.stamps[b * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // sorted
     for (uint32_t i = tid; i < nu; i += RED_THREADS) {
       const uint16_t sl = s.idx[i];
-      w.uk[out0 + written + i] = make_uint4((uint32_t)s.k0[sl], (uint32_t)(s.k0[sl] >> 32), (uint32_t)s.k1[sl],
-                                            (uint32_t)(s.k1[sl] >> 32));
+      w.uk[out0 + written + i] = s.key[sl];
       w.uc[out0 + written + i] = s.cnt[sl];
     }
     written += nu;
     sub++;
     __syncthreads();
   }
+  if (stamp) {
+    w.stamps[b * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    w.stamps[b * 8 + 5] = hw;
+    w.stamps[b * 8 + 6] = s.misc[0];
+  }
   if (tid == 0) {
     w.b_uniq[b] = written;
     if (kk) atomicMax(&w.ctl->max_sub, 1u << kk);
+    if (s.dbg) for (int i = 0; i < 3; i++) atomicAdd(&w.ctl->dbg_cnt[i], (unsigned long long)dbgc[i]);
   }
 }
 
