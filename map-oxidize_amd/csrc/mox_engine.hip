@@ -431,6 +431,14 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     if ((e->w.dbg & DBG_STAMP) && e->w.stamps) {
       std::vector<unsigned long long> st(8 * NB);
       (void)hipMemcpy(st.data(), e->w.stamps, st.size() * 8, hipMemcpyDeviceToHost);
+      std::vector<unsigned long long> mc(8 * 1024 * MAP_WAVES);
+      (void)hipMemcpy(mc.data(), e->w.stamps + 8 * 4096, mc.size() * 8, hipMemcpyDeviceToHost);
+      FILE* g = fopen("gpurun_out/mapcyc.csv", "w");
+      if (g) {
+        for (uint32_t i = 0; i < e->w.map_grid * MAP_WAVES; i++)
+          fprintf(g, "%u,%llu,%llu,%llu,%llu,%llu,%llu\n", i, mc[8 * i], mc[8 * i + 1], mc[8 * i + 2], mc[8 * i + 3], mc[8 * i + 4], mc[8 * i + 5]);
+        fclose(g);
+      }
       FILE* f = fopen("gpurun_out/stamps.csv", "w");
       if (f) {
         for (int i = 0; i < NB; i++)
@@ -766,7 +774,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
   if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
-  if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096);
+  if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096 + 8 * 8 * 1024 * MAP_WAVES);
   e->sync_each = getenv("MOX_SYNC_EACH") != nullptr;
   int rc = alloc_fixed(e);
   if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));

@@ -19,7 +19,7 @@ constexpr int RING = 32;                    // power of two
 constexpr int SLOT = ROW;
 constexpr int PAY = ROW - 32;               // 992 payload bytes per row
 constexpr int LD_GROUP = 6;                 // loader: rows per register group
-constexpr int LD_GROUPS = 4;                // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
+constexpr int LD_GROUPS = 3;                // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_LOADERS = 2;              // loader waves (alternate row groups)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)

@@ -363,6 +363,15 @@ __device__ __forceinline__ uint4 lower16(uint4 v) {
   const uint64_t l = lower_ascii(((uint64_t)v.y << 32) | v.x), h = lower_ascii(((uint64_t)v.w << 32) | v.z);
   return make_uint4((uint32_t)l, (uint32_t)(l >> 32), (uint32_t)h, (uint32_t)(h >> 32));
 }
+// Whole-wave lane shifts by one on the VALU (DPP wave_shl:1 / wave_shr:1; gfx9
+// family), instead of ds_bpermute through the LDS crossbar.  Lane 63 (next) and
+// lane 0 (prev) get 0.
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
 __device__ __forceinline__ uint4 shfl_down1(uint4 v) {
   return make_uint4(__shfl_down(v.x, 1), __shfl_down(v.y, 1), __shfl_down(v.z, 1), __shfl_down(v.w, 1));
 }
@@ -515,7 +524,7 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
 //     prefix sum of per-lane start counts from 5 bit-sliced ballots);
 //  2. token phase (lane = token): pass_a over all tokens, pass_b over its misses.
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
-                                       uint16_t* list) {
+                                       uint16_t* list, uint64_t* cyc) {
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
   const bool ctx = lane == 0 || lane == 63;
@@ -526,8 +535,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   if (!slow) {
     const uint64_t L = ((uint64_t)a.y << 32) | a.x, H = ((uint64_t)a.w << 32) | a.z;
     const uint32_t ws16 = movemask8(ws_bytes80(L)) | (movemask8(ws_bytes80(H)) << 8);
-    const uint32_t wsn = __shfl_down(ws16, 1);
-    const uint32_t wsp = __shfl_up(ws16, 1);
+    const uint32_t wsn = from_next_lane(ws16);
+    const uint32_t wsp = from_prev_lane(ws16);
     ws32 = ws16 | (wsn << 16);
     start = (~ws32) & ((ws32 << 1) | ((wsp >> 15) & 1u)) & 0xFFFFu;
     if (ctx) start = 0;
@@ -538,7 +547,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     const bool anyz = __any((zero_bytes80(L) | zero_bytes80(H)) != 0);
     if (anyz) {
       const uint32_t z16 = zero_mask16(a);
-      z32 = z16 | (__shfl_down(z16, 1) << 16);
+      z32 = z16 | (from_next_lane(z16) << 16);
     }
     const bool near_end = !m.c.at_end && sbase + ROW + 32 >= m.c.hi;
     if (near_end) lim = m.c.hi > p0 ? (uint32_t)(m.c.hi - p0 < 64 ? m.c.hi - p0 : 64) : 0u;
@@ -582,6 +591,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   }
   if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
   const bool use_dict = m.dict_n && !(m.w.dbg & DBG_NO_DICT);
+  uint64_t t1 = 0;
+  if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc[1] += t1; }
   uint32_t nmiss = 0;
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
@@ -590,10 +601,13 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     else { nmiss = pass_a<1>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 64; }
   }
   wave_lds_fence();
+  uint64_t t2 = 0;
+  if (cyc) { t2 = __builtin_amdgcn_s_memtime(); cyc[2] += t2 - t1; }
   for (uint32_t j0 = 0; j0 < nmiss;) {
     if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 128; }
     else { pass_b<1>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 64; }
   }
+  if (cyc) { cyc[3] += __builtin_amdgcn_s_memtime() - t2; cyc[4] += nmiss; }
   wave_lds_fence();
 }
 
@@ -700,7 +714,14 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   } else {
     // ---------------- consumers
     uint16_t* list = lists + (wv - MAP_LOADERS) * TOKMAX;
+#ifdef MOX_STAMP
+    uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};  // [0] wait [1] byte phase [2] pass A [3] pass B [4] misses [5] rows
+    uint64_t* cp = (w.dbg & DBG_STAMP) ? cyc : nullptr;
+#else
+    uint64_t* cp = nullptr;  // per-phase cycle accounting: build with -DMOX_STAMP
+#endif
     for (;;) {
+      const uint64_t tw = cp ? __builtin_amdgcn_s_memtime() : 0;
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
       u = __builtin_amdgcn_readfirstlane(u);
@@ -713,10 +734,16 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
       const uint64_t sbase = base0 + (rb + u) * PAY - 16;
       uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
       if (sbase < c.lo || sbase + SLOT > c.hi) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
-      do_row(m, sbase, a, ntok, sl, list);
+      if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp[0] += t0 - tw; cp[1] -= t0; cp[5]++; }
+      do_row(m, sbase, a, ntok, sl, list, cp);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+#ifdef MOX_STAMP
+    if (cp && lane == 0) {
+      for (int i = 0; i < 6; i++) w.stamps[8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8 + i] = cyc[i];
+    }
+#endif
   }
   __syncthreads();
   if (m.dict_n) {
