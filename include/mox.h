@@ -56,8 +56,8 @@ extern "C" {
 typedef struct mox_config {
   int device;             /* HIP device ordinal; -1 = current device */
   uint32_t flags;         /* MOX_F_* */
-  uint32_t dict_words;    /* hot dictionary capacity; 0 = default (3072) */
-  uint32_t sample_pieces; /* 64 KiB pieces sampled to build the dictionary; 0 = default (64) */
+  uint32_t dict_words;    /* hot dictionary capacity; 0 = default (3584, also the maximum) */
+  uint32_t sample_pieces; /* 4 KiB pieces sampled to build the dictionary; 0 = default (192), max 1024 */
   uint64_t reserve_bytes; /* pre-size device buffers for corpora of this size; 0 = grow on demand */
   uint32_t reserved[8];
 } mox_config;

@@ -31,7 +31,9 @@ using namespace mox;
 extern "C" {
 __global__ void k_map(Corpus c, Work w, uint64_t ntiles);
 __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
-__global__ void k_dict_build(Work w, uint32_t max_words, uint32_t npieces);
+__global__ void k_dict_hist(Work w);
+__global__ void k_dict_pick(Work w, uint32_t max_words);
+__global__ void k_dict_build(Work w, uint32_t max_words);
 __global__ void k_dict_totals(Work w);
 __global__ void k_unicode(Corpus c, Work w, Tables T);
 __global__ void k_hist(Work w);
@@ -96,7 +98,7 @@ struct DevBuf {
 struct mox_engine {
   int device = 0;
   hipStream_t stream = nullptr;
-  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 48;
+  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 192;
   int n_cu = 256;
   bool sync_each = false;
   uint64_t next_cold_cap = 0;  // region capacity learnt from spills of an earlier run
@@ -225,8 +227,9 @@ int alloc_fixed(mox_engine* e) {
   Work& w = e->w;
   int rc;
   if ((rc = dalloc(e, (void**)&w.ctl, sizeof(Ctl)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.cand, (size_t)MAX_SAMPLE_PIECES * SAMPLE_OUT * sizeof(WRec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.cand_n, MAX_SAMPLE_PIECES * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.cand, (size_t)GC_SLOTS * sizeof(WRec)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_hist, 257 * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_list, (size_t)DICT_MAX_WORDS * sizeof(WRec)))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_tag, DICT_SLOTS * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_key, DICT_SLOTS * 16))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_tot, DICT_SLOTS * 8))) return rc;
@@ -268,7 +271,6 @@ int alloc_fixed(mox_engine* e) {
   return MOX_OK;
 }
 
-size_t dict_lds_bytes() { return CAND_SLOTS * 20 + DICT_SLOTS * 4; }  // k_dict_build
 size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
 size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
 
@@ -368,9 +370,15 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   // 1. hot dictionary from a sample
   if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
     HIPCHK(hipMemsetAsync(w.dict_tot, 0, DICT_SLOTS * 8, s));
-    hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(1024), 0, s, c, w, e->sample_pieces);
+    HIPCHK(hipMemsetAsync(w.cand, 0, (size_t)GC_SLOTS * sizeof(WRec), s));
+    HIPCHK(hipMemsetAsync(w.dict_hist, 0, 257 * 4, s));
+    hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(256), 0, s, c, w, e->sample_pieces);
     q.step("k_sample");
-    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), dict_lds_bytes(), s, w, e->dict_words, e->sample_pieces);
+    hipLaunchKernelGGL(k_dict_hist, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w);
+    q.step("k_dict_hist");
+    hipLaunchKernelGGL(k_dict_pick, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w, e->dict_words);
+    q.step("k_dict_pick");
+    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
     q.step("k_dict_build");
   }
   q.rec(1);
@@ -444,6 +452,47 @@ int run_corpus(mox_engine* e, const Corpus& c) {
         for (int i = 0; i < NB; i++)
           fprintf(f, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, st[8 * i], st[8 * i + 1], st[8 * i + 2], st[8 * i + 3], st[8 * i + 4], st[8 * i + 5], st[8 * i + 6]);
         fclose(f);
+      }
+    }
+    if (getenv("MOX_DUMP_DICT")) {
+      std::vector<uint4> dk(DICT_SLOTS);
+      std::vector<uint32_t> dt(DICT_SLOTS);
+      std::vector<unsigned long long> tot(DICT_SLOTS);
+      (void)hipMemcpy(dk.data(), e->w.dict_key, DICT_SLOTS * 16, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(dt.data(), e->w.dict_tag, DICT_SLOTS * 4, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(tot.data(), e->w.dict_tot, DICT_SLOTS * 8, hipMemcpyDeviceToHost);
+      std::vector<int> order;
+      unsigned long long sum = 0;
+      for (int i = 0; i < DICT_SLOTS; i++) if (dt[i]) { order.push_back(i); sum += tot[i]; }
+      std::sort(order.begin(), order.end(), [&](int a, int b) { return tot[a] > tot[b]; });
+      fprintf(stderr, "[mox] dict words %zu, hits %llu of %llu tokens\n", order.size(), sum, (unsigned long long)h.tokens);
+      {
+        std::vector<WRec> cand(GC_SLOTS), lst(DICT_MAX_WORDS);
+        std::vector<uint32_t> hist(257);
+        (void)hipMemcpy(cand.data(), e->w.cand, GC_SLOTS * sizeof(WRec), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(lst.data(), e->w.dict_list, DICT_MAX_WORDS * sizeof(WRec), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(hist.data(), e->w.dict_hist, 257 * 4, hipMemcpyDeviceToHost);
+        size_t nc = 0, ns = 0;
+        uint64_t best = 0;
+        for (auto& r : cand) if (r.count) { nc++; if ((r.w1 & ~(1ull << 63)) == 0) { ns++; best = std::max(best, (uint64_t)r.count); } }
+        fprintf(stderr, "[mox] cand: %zu used, %zu with w1==0 (max count %llu); picked %u, thresh %u, hist[255]=%u hist[2]=%u\n", nc, ns,
+                (unsigned long long)best, hist[256], h.dict_thresh, hist[255], hist[2]);
+        int k = 0;
+        for (uint32_t i = 0; i < std::min<uint32_t>(hist[256], DICT_MAX_WORDS) && k < 5; i++)
+          if (lst[i].w1 == 0) { char b[9] = {0}; memcpy(b, &lst[i].w0, 8); fprintf(stderr, "[mox]   list short '%s' count %llu\n", b, (unsigned long long)lst[i].count); k++; }
+      }
+      int nshort = 0;
+      for (size_t j = 0; j < order.size(); j++) {
+        const int i = order[j];
+        char wbuf[17] = {0};
+        memcpy(wbuf, &dk[i], 16);
+        if (strlen(wbuf) <= 4 && nshort < 6) { fprintf(stderr, "[mox]   short slot %d total %llu key '%s' tag %08x\n", i, tot[i], wbuf, dt[i]); nshort++; }
+      }
+      for (size_t j = 0; j < order.size() && j < 8; j++) {
+        const int i = order[j];
+        char wbuf[17] = {0};
+        memcpy(wbuf, &dk[i], 16);
+        fprintf(stderr, "[mox]   slot %d home %d total %llu key '%s'\n", i, (int)(dt[i] & (DICT_SLOTS - 1)), tot[i], wbuf);
       }
     }
     if (getenv("MOX_VERBOSE"))
@@ -768,8 +817,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
   }
   for (auto& ev : e->ev) (void)hipEventCreate(&ev);
   if (hipFuncSetAttribute((const void*)k_map, hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes()) != hipSuccess ||
-      hipFuncSetAttribute((const void*)k_dict_build, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dict_lds_bytes()) != hipSuccess) {
+      hipFuncSetAttribute((const void*)k_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes()) != hipSuccess) {
     mox_engine_destroy(e);
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
@@ -794,7 +842,7 @@ void mox_engine_destroy(mox_engine* e) {
   (void)hipDeviceSynchronize();
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
-  void* ptrs[] = {w.ctl, w.cand, w.cand_n, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, w.scan_part, (void*)e->tables.lower_src,
+  void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, w.scan_part, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_lens, e->d_text};
   for (void* p : ptrs) dfree(p);

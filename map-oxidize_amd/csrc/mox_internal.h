@@ -27,11 +27,10 @@ constexpr int NB = 1 << NB_LOG2;
 constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
 constexpr int DICT_SLOTS = 4 * DICT_BUCKETS;
 constexpr int DICT_MAX_WORDS = 3584;
-constexpr int CAND_SLOTS = 7168;            // dictionary candidate table (LDS of k_dict_build)
-constexpr int MAX_SAMPLE_PIECES = 256;
-constexpr int SAMPLE_OUT = 1024;            // candidates one sample piece hands to k_dict_build
-constexpr int SAMPLE_PIECE = 16 * 1024;     // one 1024-thread workgroup x 16 B
-constexpr int SAMPLE_SLOTS = 4096;
+constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
+constexpr int MAX_SAMPLE_PIECES = 1024;
+constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B
+constexpr int SAMPLE_SLOTS = 2048;
 constexpr int RED_THREADS = 1024;
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_WGS = 1024;
@@ -144,8 +143,9 @@ struct Corpus {
 struct Work {  // device buffers of one engine
   Ctl* ctl;
   // dictionary
-  WRec* cand;                     // MAX_SAMPLE_PIECES x SAMPLE_OUT (word, count in its piece)
-  uint32_t* cand_n;               // MAX_SAMPLE_PIECES
+  WRec* cand;                     // GC_SLOTS candidates (key claimed with claim16, count)
+  uint32_t* dict_hist;            // [256] candidate count histogram, [256] picked words
+  WRec* dict_list;                // DICT_MAX_WORDS picked words
   uint32_t* dict_tag;             // DICT_SLOTS key hashes (0 = empty), bucket b = slots 4b..4b+3
   uint4* dict_key;                // DICT_SLOTS lowered 16-byte keys
   unsigned long long* dict_tot;   // DICT_SLOTS counts summed over map workgroups

@@ -514,6 +514,11 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
   }
 }
 
+// per-phase cycle accounting of a map consumer wave (-DMOX_STAMP builds only)
+struct Cyc {
+  uint64_t wait, byte, pa, pb, miss, rows;
+};
+
 // One ring slot (64 lanes x 16 B = corpus bytes [sbase, sbase + 1024)) in two
 // phases.  Lanes 1..62 hold the row's 992 payload bytes; lane 0 (the 16 bytes
 // before) and lane 63 (the 16 bytes after) are context only: they give the
@@ -524,7 +529,7 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
 //     prefix sum of per-lane start counts from 5 bit-sliced ballots);
 //  2. token phase (lane = token): pass_a over all tokens, pass_b over its misses.
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
-                                       uint16_t* list, uint64_t* cyc) {
+                                       uint16_t* list, struct Cyc* cyc) {
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
   const bool ctx = lane == 0 || lane == 63;
@@ -592,7 +597,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
   const bool use_dict = m.dict_n && !(m.w.dbg & DBG_NO_DICT);
   uint64_t t1 = 0;
-  if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc[1] += t1; }
+  if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
   uint32_t nmiss = 0;
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
@@ -602,12 +607,12 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   }
   wave_lds_fence();
   uint64_t t2 = 0;
-  if (cyc) { t2 = __builtin_amdgcn_s_memtime(); cyc[2] += t2 - t1; }
+  if (cyc) { t2 = __builtin_amdgcn_s_memtime(); cyc->pa += t2 - t1; }
   for (uint32_t j0 = 0; j0 < nmiss;) {
     if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 128; }
     else { pass_b<1>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 64; }
   }
-  if (cyc) { cyc[3] += __builtin_amdgcn_s_memtime() - t2; cyc[4] += nmiss; }
+  if (cyc) { cyc->pb += __builtin_amdgcn_s_memtime() - t2; cyc->miss += nmiss; }
   wave_lds_fence();
 }
 
@@ -715,10 +720,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
     // ---------------- consumers
     uint16_t* list = lists + (wv - MAP_LOADERS) * TOKMAX;
 #ifdef MOX_STAMP
-    uint64_t cyc[6] = {0, 0, 0, 0, 0, 0};  // [0] wait [1] byte phase [2] pass A [3] pass B [4] misses [5] rows
-    uint64_t* cp = (w.dbg & DBG_STAMP) ? cyc : nullptr;
+    Cyc cyc{0, 0, 0, 0, 0, 0};
+    Cyc* cp = &cyc;
 #else
-    uint64_t* cp = nullptr;  // per-phase cycle accounting: build with -DMOX_STAMP
+    Cyc* cp = nullptr;  // per-phase cycle accounting: build with -DMOX_STAMP
 #endif
     for (;;) {
       const uint64_t tw = cp ? __builtin_amdgcn_s_memtime() : 0;
@@ -734,14 +739,15 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
       const uint64_t sbase = base0 + (rb + u) * PAY - 16;
       uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
       if (sbase < c.lo || sbase + SLOT > c.hi) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
-      if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp[0] += t0 - tw; cp[1] -= t0; cp[5]++; }
+      if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
       do_row(m, sbase, a, ntok, sl, list, cp);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 #ifdef MOX_STAMP
-    if (cp && lane == 0) {
-      for (int i = 0; i < 6; i++) w.stamps[8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8 + i] = cyc[i];
+    if (lane == 0 && w.stamps) {
+      unsigned long long* o = w.stamps + 8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8;
+      o[0] = cyc.wait; o[1] = cyc.byte; o[2] = cyc.pa; o[3] = cyc.pb; o[4] = cyc.miss; o[5] = cyc.rows;
     }
 #endif
   }
@@ -777,166 +783,167 @@ __device__ __forceinline__ bool claim16(unsigned long long* k0, unsigned long lo
   return o1 == 0 || o1 == t1;
 }
 
-// Sample pieces of the corpus (one 16 KiB piece per workgroup, staged in LDS)
-// and count their short ASCII words in LDS; words seen at least twice go to
-// this piece's candidate list (plain stores, no global atomics).  Heuristic
-// only: the dictionary decides speed, never counts.
-extern "C" __global__ __launch_bounds__(1024) void k_sample(Corpus c, Work w, uint32_t npieces) {
-  __shared__ __attribute__((aligned(16))) uint8_t buf[SAMPLE_PIECE + 32];
+// ---- hot-word dictionary (heuristic: it decides speed, never counts) ----
+// 1. k_sample: npieces workgroups each count the short ASCII words of one
+//    SAMPLE_PIECE of the corpus (pieces spread evenly) in an LDS table and add
+//    every local word into the global candidate table (cand[GC_SLOTS], claim16
+//    + atomic count; one insert per distinct local word).
+// 2. k_dict_hist: histogram of candidate counts (bins 0..255, 255 = >= 255).
+// 3. k_dict_pick: threshold T = smallest count >= 2 with #(count >= T) <=
+//    max_words; compacts those candidates into dict_list.
+// 4. k_dict_build: places them hottest class first (home slot, else home
+//    group, else second group) as the LDS dictionary image.
+__device__ __forceinline__ uint32_t lower32(uint32_t x) {  // ASCII bytes only
+  const uint32_t ge_a = x + 0x3F3F3F3Fu, gt_z = x + 0x25252525u;
+  return x | (((ge_a & ~gt_z) & 0x80808080u) >> 2);
+}
+
+extern "C" __global__ __launch_bounds__(256) void k_sample(Corpus c, Work w, uint32_t npieces) {
+  constexpr int BUF = SAMPLE_PIECE + 48;  // [ps - 16, ps + PIECE + 32)
+  __shared__ __attribute__((aligned(16))) uint8_t buf[BUF];
   __shared__ unsigned long long sk0[SAMPLE_SLOTS], sk1[SAMPLE_SLOTS];
   __shared__ uint32_t scnt[SAMPLE_SLOTS];
-  __shared__ uint32_t nout;
+  __shared__ uint4 mtab[17];
   const int tid = threadIdx.x;
-  for (int i = tid; i < SAMPLE_SLOTS; i += 1024) { sk0[i] = 0; sk1[i] = 0; scnt[i] = 0; }
-  if (tid == 0) nout = 0;
+  for (int i = tid; i < SAMPLE_SLOTS; i += 256) { sk0[i] = 0; sk1[i] = 0; scnt[i] = 0; }
+  if (tid < 17) {
+    uint32_t mk[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const int cc = tid - 4 * i;
+      mk[i] = cc <= 0 ? 0u : (cc >= 4 ? ~0u : ((1u << (8 * cc)) - 1u));
+    }
+    mtab[tid] = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+  }
   const uint64_t span = c.own_hi - c.own_lo;
   const uint64_t stride = span / npieces;
   const uint64_t ps = (c.own_lo + stride * blockIdx.x) & ~15ull;  // 16-aligned piece start
-  // stage [ps - 16, ps + PIECE + 16) (out-of-range bytes read as spaces)
-  for (int i = tid; i < (SAMPLE_PIECE + 32) / 16; i += 1024) {
+  for (int i = tid; i < BUF / 16; i += 256) {
     const uint64_t p = ps - 16 + (uint64_t)i * 16;
     const bool in = p + 16 > c.lo && p < c.hi;
-    uint4 v = in ? fix16(c, p, raw16(c, p)) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
-    reinterpret_cast<uint4*>(buf)[i] = v;
+    reinterpret_cast<uint4*>(buf)[i] = in ? fix16(c, p, raw16(c, p)) : make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
   }
   __syncthreads();
-  // thread t scans piece bytes [16 t, 16 t + 16), i.e. buf[16 + 16 t ...]
-  for (int j = 0; j < 16; j++) {
-    const int q = 16 + tid * 16 + j;
-    const uint8_t b = buf[q];
-    if (is_ascii_ws(b) || b >= 0x80 || !is_ascii_ws(buf[q - 1])) continue;
-    uint64_t w0 = 0, w1 = 0;
-    int len = 0;
-    bool ok = true;
-    for (int x = q;; x++) {
-      if (x >= SAMPLE_PIECE + 32) { ok = false; break; }
-      const uint8_t y = buf[x];
-      if (is_ascii_ws(y)) break;
-      if (y >= 0x80 || y == 0 || len == 16) { ok = false; break; }
-      const uint64_t ly = ascii_lower(y);
-      if (len < 8) w0 |= ly << (8 * len); else w1 |= ly << (8 * (len - 8));
-      len++;
-    }
-    if (!ok || len == 0) continue;
-    uint32_t slot = key_hash(w0, w1) & (SAMPLE_SLOTS - 1);
+  // thread t: token starts in piece bytes [16 t, 16 t + 16) = buf[16 + 16 t ...]
+  const uint4 own = reinterpret_cast<const uint4*>(buf)[1 + tid], nxt = reinterpret_cast<const uint4*>(buf)[2 + tid];
+  const uint32_t prevb = buf[15 + 16 * tid];
+  const uint32_t ws32 = ws_mask16(own) | (ws_mask16(nxt) << 16);
+  uint32_t start = (~ws32) & ((ws32 << 1) | (is_ascii_ws(prevb) ? 1u : 0u)) & 0xFFFFu;
+  while (start) {
+    const uint32_t p = __builtin_ctz(start);
+    start &= start - 1;
+    const uint32_t rest = ws32 >> p;
+    const uint32_t len = rest ? __builtin_ctz(rest) : 32;
+    if (len > 16) continue;
+    const uint32_t pos = 16 + 16 * tid + p;
+    const uint2* q = reinterpret_cast<const uint2*>(buf + (pos & ~7u));
+    const uint2 A = q[0], B = q[1], C = q[2];
+    const uint4 M = mtab[len];
+    const bool o = (pos & 4u) != 0;
+    const uint32_t E0 = o ? A.y : A.x, E1 = o ? B.x : A.y, E2 = o ? B.y : B.x, E3 = o ? C.x : B.y, E4 = o ? C.y : C.x;
+    const uint32_t sh = pos & 3u;
+    uint32_t K[4] = {__builtin_amdgcn_alignbyte(E1, E0, sh) & M.x, __builtin_amdgcn_alignbyte(E2, E1, sh) & M.y,
+                     __builtin_amdgcn_alignbyte(E3, E2, sh) & M.z, __builtin_amdgcn_alignbyte(E4, E3, sh) & M.w};
+    if (((K[0] | K[1] | K[2] | K[3]) & 0x80808080u) != 0) continue;  // non-ASCII: never a dictionary word
+    // zero bytes of the 16: exactly 16 - len when the token has no NUL byte
+    const uint32_t nz = (uint32_t)__popcll(zero_bytes80(((uint64_t)K[1] << 32) | K[0])) +
+                        (uint32_t)__popcll(zero_bytes80(((uint64_t)K[3] << 32) | K[2]));
+    if (nz != 16 - len) continue;
+#pragma unroll
+    for (int i = 0; i < 4; i++) K[i] = lower32(K[i]);
+    const uint64_t w0 = ((uint64_t)K[1] << 32) | K[0], w1 = ((uint64_t)K[3] << 32) | K[2];
+    uint32_t slot = hash32(K[0], K[1], K[2], K[3]) & (SAMPLE_SLOTS - 1);
     for (int pr = 0; pr < 64; pr++) {
       if (claim16(&sk0[slot], &sk1[slot], w0, w1)) { atomicAdd(&scnt[slot], 1u); break; }
       slot = (slot + 1) & (SAMPLE_SLOTS - 1);
     }
   }
   __syncthreads();
-  WRec* out = w.cand + (uint64_t)blockIdx.x * SAMPLE_OUT;
-  for (int i = tid; i < SAMPLE_SLOTS; i += 1024) {
+  for (int i = tid; i < SAMPLE_SLOTS; i += 256) {
     const uint32_t n = scnt[i];
-    if (n < 2 || sk0[i] == 0 || sk1[i] == 0) continue;
-    const uint32_t o = atomicAdd(&nout, 1u);
-    if (o < SAMPLE_OUT) out[o] = WRec{sk0[i], sk1[i] & ~(1ull << 63), n};
+    if (n == 0 || sk0[i] == 0 || sk1[i] == 0) continue;
+    const uint64_t w0 = sk0[i], w1 = sk1[i] & ~(1ull << 63);
+    uint32_t g = key_hash(w0, w1) & (GC_SLOTS - 1);
+    for (int pr = 0; pr < 256; pr++) {
+      WRec* r = &w.cand[g];
+      if (claim16((unsigned long long*)&r->w0, (unsigned long long*)&r->w1, w0, w1)) {
+        atomicAdd((unsigned long long*)&r->count, (unsigned long long)n);
+        break;
+      }
+      g = (g + 1) & (GC_SLOTS - 1);
+    }
   }
-  __syncthreads();
-  if (tid == 0) w.cand_n[blockIdx.x] = nout < SAMPLE_OUT ? nout : SAMPLE_OUT;
 }
 
-// Merge the pieces' candidate lists in an LDS table, select the most frequent
-// words (count threshold from a log2 histogram refined by a linear one) and
-// lay them out as the LDS dictionary image: tag = key hash in the first free
-// slot of bucket b1, else of bucket b2, hottest words first.
-extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words, uint32_t npieces) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  unsigned long long* ck0 = (unsigned long long*)smem;
-  unsigned long long* ck1 = ck0 + CAND_SLOTS;
-  uint32_t* ccnt = (uint32_t*)(ck1 + CAND_SLOTS);
-  uint32_t* ltag = ccnt + CAND_SLOTS;  // DICT_SLOTS tags being placed
-  __shared__ uint32_t hist[64], fine[256];
-  __shared__ uint32_t nsel, thresh_lo, cls;
+extern "C" __global__ __launch_bounds__(1024) void k_dict_hist(Work w) {
+  __shared__ uint32_t h[256];
+  if (threadIdx.x < 256) h[threadIdx.x] = 0;
+  __syncthreads();
+  for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < GC_SLOTS; i += gridDim.x * 1024) {
+    const uint64_t n = w.cand[i].count;
+    if (n) atomicAdd(&h[n > 255 ? 255 : n], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < 256 && h[threadIdx.x]) atomicAdd(&w.dict_hist[threadIdx.x], h[threadIdx.x]);
+}
+
+extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t max_words) {
+  __shared__ uint32_t T;
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0, t = 2;
+    for (int cc = 255; cc >= 2; cc--) {
+      if (acc + w.dict_hist[cc] > max_words) { t = cc + 1; break; }
+      acc += w.dict_hist[cc];
+    }
+    T = t;
+    if (blockIdx.x == 0) w.ctl->dict_thresh = t;
+  }
+  __syncthreads();
+  const uint32_t t = T;
+  for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < GC_SLOTS; i += gridDim.x * 1024) {
+    const WRec r = w.cand[i];
+    if (r.count < t || r.w0 == 0 || r.w1 == 0) continue;
+    const uint32_t o = atomicAdd(&w.dict_hist[256], 1u);
+    if (o < max_words) w.dict_list[o] = WRec{r.w0, r.w1 & ~(1ull << 63), r.count};
+  }
+}
+
+extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
+  __shared__ uint32_t ltag[DICT_SLOTS];
+  __shared__ uint32_t nsel;
   const int tid = threadIdx.x;
-  for (int i = tid; i < CAND_SLOTS; i += 1024) { ck0[i] = 0; ck1[i] = 0; ccnt[i] = 0; }
   for (int i = tid; i < DICT_SLOTS; i += 1024) { ltag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
-  if (tid < 64) hist[tid] = 0;
-  if (tid < 256) fine[tid] = 0;
   if (tid == 0) nsel = 0;
   __syncthreads();
-  __shared__ uint32_t pn[MAX_SAMPLE_PIECES];
-  for (uint32_t i = tid; i < npieces; i += 1024) pn[i] = w.cand_n[i];
-  __syncthreads();
-  for (uint32_t x = tid; x < npieces * SAMPLE_OUT; x += 1024) {
-    const uint32_t pc = x / SAMPLE_OUT, i = x % SAMPLE_OUT;
-    {
-      if (i >= pn[pc]) continue;
-      const WRec r = w.cand[x];
-      uint32_t slot = key_hash(r.w0, r.w1) % CAND_SLOTS;
-      for (int pr = 0; pr < 256; pr++) {
-        if (claim16(&ck0[slot], &ck1[slot], r.w0, r.w1)) { atomicAdd(&ccnt[slot], (uint32_t)r.count); break; }
-        slot = slot + 1 == CAND_SLOTS ? 0 : slot + 1;
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = tid; i < CAND_SLOTS; i += 1024) {
-    const uint32_t cnt = ccnt[i];
-    if (cnt) atomicAdd(&hist[31 - __clz(cnt)], 1u);
-  }
-  __syncthreads();
-  // class k: all candidates with log2(count) > k fit; k itself may not
-  if (tid == 0) {
-    uint32_t acc = 0, k = 64;
-    for (int b = 63; b >= 0; b--) { if (acc + hist[b] > max_words) { k = b; break; } acc += hist[b]; k = b - 1; }
-    cls = k;       // candidates in class k are split by the fine histogram (k == ~0u: all fit)
-    nsel = acc;    // candidates strictly above class k
-  }
-  __syncthreads();
-  const uint32_t k = cls;
-  // fine histogram of class k: count in [2^k, 2^(k+1)) in 256 linear bins
-  for (int i = tid; i < CAND_SLOTS && k < 32; i += 1024) {
-    const uint64_t cnt = ccnt[i];
-    if (cnt == 0 || (uint32_t)(31 - __clz((uint32_t)cnt)) != k) continue;
-    const uint32_t bin = k >= 8 ? (uint32_t)((cnt - (1ull << k)) >> (k - 8)) : (uint32_t)((cnt - (1ull << k)) << (8 - k));
-    atomicAdd(&fine[bin > 255 ? 255 : bin], 1u);
-  }
-  __syncthreads();
-  if (tid == 0) {
-    uint64_t lo = 1;  // select count >= lo
-    if (k < 32) {
-      uint32_t acc = nsel;
-      int b = 255;
-      for (; b >= 0; b--) { if (acc + fine[b] > max_words) break; acc += fine[b]; }
-      const uint32_t fb = (uint32_t)(b + 1);  // bins >= fb fit
-      lo = (1ull << k) + (k >= 8 ? ((uint64_t)fb << (k - 8)) : (((uint64_t)fb + (1ull << (8 - k)) - 1) >> (8 - k)));
-      if (fb >= 256) lo = 1ull << (k + 1);
-    }
-    thresh_lo = (uint32_t)(lo > 0xFFFFFFFFull ? 0xFFFFFFFFull : lo);
-    nsel = 0;
-  }
-  __syncthreads();
-  const uint64_t lo = thresh_lo < 1 ? 1 : thresh_lo;
+  uint32_t n = w.dict_hist[256];
+  if (n > max_words) n = max_words;
   // insert by descending log2 count class, so that a word dropped because both
-  // of its buckets are full is never hotter than the words that filled them
+  // of its groups are full is never hotter than the words that filled them
   for (int cl = 31; cl >= 0; cl--) {
-    if (cl < 31 && (2ull << cl) <= lo) break;  // every count in this class is < lo
-    for (int i = tid; i < CAND_SLOTS; i += 1024) {
-      const uint32_t cnt = ccnt[i];
-      if (cnt == 0 || cnt < lo || (31 - __clz(cnt)) != cl) continue;
-      const uint64_t w0 = ck0[i], w1 = ck1[i] & ~(1ull << 63);
-      const uint32_t h = key_hash(w0, w1);
+    for (uint32_t i = tid; i < n; i += 1024) {
+      const WRec r = w.dict_list[i];
+      const uint32_t cnt = r.count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)r.count;
+      if ((31 - __clz(cnt)) != cl) continue;
+      const uint32_t h = key_hash(r.w0, r.w1);
       if (h == 0) continue;  // tag 0 marks an empty slot
-      // home slot, else a free slot of the home group, else of the second group
       int slot = -1;
       if (atomicCAS(&ltag[dict_home(h)], 0u, h) == 0u) slot = (int)dict_home(h);
-      for (int i = 0; i < 4 && slot < 0; i++) {
-        const uint32_t s1 = 4 * dict_g1(h) + i;
+      for (int k = 0; k < 4 && slot < 0; k++) {
+        const uint32_t s1 = 4 * dict_g1(h) + k;
         if (atomicCAS(&ltag[s1], 0u, h) == 0u) slot = (int)s1;
       }
-      for (int i = 0; i < 4 && slot < 0; i++) {
-        const uint32_t s2 = 4 * dict_g2(h) + i;
+      for (int k = 0; k < 4 && slot < 0; k++) {
+        const uint32_t s2 = 4 * dict_g2(h) + k;
         if (atomicCAS(&ltag[s2], 0u, h) == 0u) slot = (int)s2;
       }
       if (slot < 0) continue;  // both groups full: this word stays cold
-      w.dict_key[slot] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+      w.dict_key[slot] = make_uint4((uint32_t)r.w0, (uint32_t)(r.w0 >> 32), (uint32_t)r.w1, (uint32_t)(r.w1 >> 32));
       atomicAdd(&nsel, 1u);
     }
     __syncthreads();
   }
   for (int i = tid; i < DICT_SLOTS; i += 1024) w.dict_tag[i] = ltag[i];
-  if (tid == 0) { w.ctl->dict_n = nsel; w.ctl->dict_thresh = thresh_lo; }
+  if (tid == 0) w.ctl->dict_n = nsel;
 }
 
 // Emit the dictionary totals (summed by k_map's atomics) as weighted records.
