@@ -888,43 +888,63 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_hist(Work w) {
 }
 
 extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t max_words) {
-  __shared__ uint32_t T;
+  __shared__ uint32_t T, h[256];
+  if (threadIdx.x < 256) h[threadIdx.x] = w.dict_hist[threadIdx.x];
+  __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t acc = 0, t = 2;
     for (int cc = 255; cc >= 2; cc--) {
-      if (acc + w.dict_hist[cc] > max_words) { t = cc + 1; break; }
-      acc += w.dict_hist[cc];
+      if (acc + h[cc] > max_words) { t = cc + 1; break; }
+      acc += h[cc];
     }
     T = t;
     if (blockIdx.x == 0) w.ctl->dict_thresh = t;
   }
   __syncthreads();
+  // one slot per thread (grid = GC_SLOTS / 1024): rank picked entries in the
+  // workgroup, reserve the workgroup's range with one global atomic
+  __shared__ uint32_t wn[16], base;
   const uint32_t t = T;
-  for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < GC_SLOTS; i += gridDim.x * 1024) {
-    const WRec r = w.cand[i];
-    if (r.count < t || r.w0 == 0 || r.w1 == 0) continue;
-    const uint32_t o = atomicAdd(&w.dict_hist[256], 1u);
-    if (o < max_words) w.dict_list[o] = WRec{r.w0, r.w1 & ~(1ull << 63), r.count};
-  }
+  const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
+  const WRec r = w.cand[i];
+  const bool pick = r.count >= t && r.w0 != 0 && r.w1 != 0;
+  const uint64_t bm = __ballot(pick);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) wn[wv] = (uint32_t)__popcll(bm);
+  __syncthreads();
+  uint32_t pre = (uint32_t)__popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
+  for (int k = 0; k < 16; k++) { if (k < wv) pre += wn[k]; tot += wn[k]; }
+  if (threadIdx.x == 0) base = tot ? atomicAdd(&w.dict_hist[256], tot) : 0u;
+  __syncthreads();
+  const uint32_t o = base + pre;
+  if (pick && o < max_words) w.dict_list[o] = WRec{r.w0, r.w1 & ~(1ull << 63), r.count};
 }
 
 extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
   __shared__ uint32_t ltag[DICT_SLOTS];
+  __shared__ uint2 lk0[DICT_MAX_WORDS], lk1[DICT_MAX_WORDS];  // picked keys, staged once
+  __shared__ uint8_t lcl[DICT_MAX_WORDS];                     // log2 count class
   __shared__ uint32_t nsel;
   const int tid = threadIdx.x;
   for (int i = tid; i < DICT_SLOTS; i += 1024) { ltag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
   if (tid == 0) nsel = 0;
-  __syncthreads();
   uint32_t n = w.dict_hist[256];
   if (n > max_words) n = max_words;
+  for (uint32_t i = tid; i < n; i += 1024) {
+    const WRec r = w.dict_list[i];
+    const uint32_t cnt = r.count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)r.count;
+    lk0[i] = make_uint2((uint32_t)r.w0, (uint32_t)(r.w0 >> 32));
+    lk1[i] = make_uint2((uint32_t)r.w1, (uint32_t)(r.w1 >> 32));
+    lcl[i] = (uint8_t)(31 - __clz(cnt));
+  }
+  __syncthreads();
   // insert by descending log2 count class, so that a word dropped because both
   // of its groups are full is never hotter than the words that filled them
   for (int cl = 31; cl >= 0; cl--) {
     for (uint32_t i = tid; i < n; i += 1024) {
-      const WRec r = w.dict_list[i];
-      const uint32_t cnt = r.count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)r.count;
-      if ((31 - __clz(cnt)) != cl) continue;
-      const uint32_t h = key_hash(r.w0, r.w1);
+      if (lcl[i] != cl) continue;
+      const uint2 a = lk0[i], b = lk1[i];
+      const uint32_t h = hash32(a.x, a.y, b.x, b.y);
       if (h == 0) continue;  // tag 0 marks an empty slot
       int slot = -1;
       if (atomicCAS(&ltag[dict_home(h)], 0u, h) == 0u) slot = (int)dict_home(h);
@@ -937,7 +957,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
         if (atomicCAS(&ltag[s2], 0u, h) == 0u) slot = (int)s2;
       }
       if (slot < 0) continue;  // both groups full: this word stays cold
-      w.dict_key[slot] = make_uint4((uint32_t)r.w0, (uint32_t)(r.w0 >> 32), (uint32_t)r.w1, (uint32_t)(r.w1 >> 32));
+      w.dict_key[slot] = make_uint4(a.x, a.y, b.x, b.y);
       atomicAdd(&nsel, 1u);
     }
     __syncthreads();
