@@ -37,6 +37,8 @@ METRIC = "word-count input GB/s end-to-end at 1 and 8 MI355X; % of HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 HALO = 1 << 16
 
+KIND_DESC = {corpus.ZIPF: "Zipf(1.1) English-like text", corpus.HICARD: "random 4-16 byte [a-z0-9] tokens",
+             corpus.SKEW: "top-10 words 90% + Zipf(1.1) tail", corpus.UNICODE: "Zipf text with Unicode tokens"}
 WORKLOADS = {
     # name: (kind, seed, bytes per rank, description)
     "C2": (corpus.ZIPF, 0x5EED0002, 1 << 30, "C2: 1 GiB Zipf(s=1.1) English-like corpus per GPU (map+sort+reduce)"),
@@ -175,7 +177,10 @@ def main():
         traffic = None
         if a.traffic_json and os.path.exists(a.traffic_json):
             try:
-                traffic = json.load(open(a.traffic_json)).get("hbm_bytes_per_launch")
+                tj = json.load(open(a.traffic_json))
+                # PMC traffic is per launch of one workload and size: report it only for that one
+                if tj.get("workload", "C2") == a.workload and tj.get("bytes_per_gpu", 1 << 30) == per_rank:
+                    traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         line = {
@@ -190,8 +195,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: mox_corpus kind=%d seed=%#x (Zipf(1.1) English-like text, host-generated, "
-                    "copied to HBM before timing)" % (kind, seed),
+            "data": "synthetic: mox_corpus kind=%d seed=%#x (%s, host-generated, "
+                    "copied to HBM before timing)" % (kind, seed, KIND_DESC.get(kind, "?")),
             "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
                        "parallelism": "dp%d byte-range shards%s" % (
                            world, (" + %s all-to-all" % ("RCCL" if a.xport == "rccl" else "host/gloo")) if world > 1 else "")},
@@ -212,7 +217,8 @@ def main():
                           for k in ("ms_run", "ms_dict", "ms_map", "ms_lanes", "ms_reduce", "ms_finalize",
                                     "ms_exchange")},
             "stats": {k: last[k] for k in ("tokens", "uniques", "dict_words", "cold_records", "weighted_records",
-                                           "unicode_tokens", "long_tokens", "chunks", "max_subpasses", "retries")},
+                                           "unicode_tokens", "long_tokens", "chunks", "max_subpasses", "retries",
+                                           "reduce_units", "split_partitions")},
             "check_sum_counts_eq_tokens": ok,
             "cpu_baseline": None,
         }

@@ -97,6 +97,9 @@ typedef struct mox_stats {
   double ms_h2d;           /* host -> device corpus copy (mox_count / mox_count_file) */
   double ms_d2h;           /* table fetch */
   double ms_exchange;      /* multi-GPU all-to-all + final reduce */
+  uint64_t reduce_units;   /* reduce work units (partitions, or their sub-buckets when split) */
+  uint32_t split_partitions; /* partitions split by the high-cardinality path */
+  uint32_t pad0;
 } mox_stats;
 
 const char* mox_last_error(void);

@@ -40,6 +40,11 @@ __global__ void k_hist(Work w);
 __global__ void k_bucket_scan(Work w);
 __global__ void k_scatter(Work w);
 __global__ void k_reduce(Work w);
+__global__ void k_split_count(Work w);
+__global__ void k_unit_scan(Work w);
+__global__ void k_split_scatter(Work w);
+__global__ void k_unit_uniq_scan(Work w);
+__global__ void k_reduce_small(Work w);
 __global__ void k_scan_reduce(const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
                               uint64_t* part);
 __global__ void k_scan_parts(uint64_t* part, int nparts);
@@ -142,11 +147,11 @@ void dfree(void* p) {
 
 // (Re)allocate every size-dependent buffer for the given capacities.
 struct Caps {
-  uint64_t cold_cap, spill_cap, w_cap, u_cap, arena_cap, long_cap, table_cap, bytes_cap;
+  uint64_t cold_cap, spill_cap, w_cap, u_cap, arena_cap, long_cap, table_cap, bytes_cap, split_k_cap, split_w_cap;
 };
 
 Caps caps_of(const Work& w) {
-  return Caps{w.cold_cap, w.spill_cap, w.w_cap, w.u_cap, w.arena_cap, w.long_cap, w.table_cap, w.bytes_cap};
+  return Caps{w.cold_cap, w.spill_cap, w.w_cap, w.u_cap, w.arena_cap, w.long_cap, w.table_cap, w.bytes_cap, w.split_k_cap, w.split_w_cap};
 }
 
 Caps initial_caps(uint64_t n, int map_grid) {
@@ -160,6 +165,8 @@ Caps initial_caps(uint64_t n, int map_grid) {
   c.long_cap = 65536;
   c.table_cap = 65536 + n / 64;
   c.bytes_cap = c.table_cap * 8;
+  c.split_k_cap = 0;  // grown on demand (OVF_SPLIT): only high-cardinality inputs split partitions
+  c.split_w_cap = 0;
   return c;
 }
 
@@ -174,6 +181,7 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   FREE_FIELD(cold); FREE_FIELD(spill);
   FREE_FIELD(w); FREE_FIELD(w_sorted); FREE_FIELD(u); FREE_FIELD(arena); FREE_FIELD(ltab); FREE_FIELD(lpos);
   FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
+  FREE_FIELD(split_k); FREE_FIELD(split_w);
   dfree(e->d_lens);
   e->d_lens = nullptr;
   Work& w = e->w;
@@ -186,6 +194,8 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   w.uniq_cap = (uint64_t)w.map_grid * NB * w.cold_cap + c.w_cap;
   w.table_cap = c.table_cap;
   w.bytes_cap = c.bytes_cap;
+  w.split_k_cap = c.split_k_cap;
+  w.split_w_cap = c.split_w_cap;
   int rc;
   if ((rc = dalloc(e, (void**)&w.cold, (uint64_t)w.map_grid * NB * w.cold_cap * 16))) return rc;
   if ((rc = dalloc(e, (void**)&w.spill, (uint64_t)w.map_grid * w.spill_cap * 16))) return rc;
@@ -200,6 +210,8 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   if ((rc = dalloc(e, (void**)&w.t_counts, w.table_cap * 8))) return rc;
   if ((rc = dalloc(e, (void**)&w.t_offs, (w.table_cap + 1) * 8))) return rc;
   if ((rc = dalloc(e, (void**)&w.t_bytes, w.bytes_cap))) return rc;
+  if ((rc = dalloc(e, (void**)&w.split_k, w.split_k_cap * 16))) return rc;
+  if ((rc = dalloc(e, (void**)&w.split_w, w.split_w_cap * sizeof(WRec)))) return rc;
   e->lens_cap = std::max<uint64_t>(w.table_cap, w.long_cap) + 1;
   if ((rc = dalloc(e, (void**)&e->d_lens, e->lens_cap * 8))) return rc;
   return MOX_OK;
@@ -208,13 +220,14 @@ int realloc_sized(mox_engine* e, const Caps& c) {
 bool caps_cover(const Caps& have, const Caps& need) {
   return have.cold_cap >= need.cold_cap && have.spill_cap >= need.spill_cap && have.w_cap >= need.w_cap && have.u_cap >= need.u_cap &&
          have.arena_cap >= need.arena_cap && have.long_cap >= need.long_cap && have.table_cap >= need.table_cap &&
-         have.bytes_cap >= need.bytes_cap;
+         have.bytes_cap >= need.bytes_cap && have.split_k_cap >= need.split_k_cap && have.split_w_cap >= need.split_w_cap;
 }
 
 Caps caps_max(const Caps& a, const Caps& b) {
   return Caps{std::max(a.cold_cap, b.cold_cap), std::max(a.spill_cap, b.spill_cap), std::max(a.w_cap, b.w_cap), std::max(a.u_cap, b.u_cap),
               std::max(a.arena_cap, b.arena_cap), std::max(a.long_cap, b.long_cap),
-              std::max(a.table_cap, b.table_cap), std::max(a.bytes_cap, b.bytes_cap)};
+              std::max(a.table_cap, b.table_cap), std::max(a.bytes_cap, b.bytes_cap), std::max(a.split_k_cap, b.split_k_cap),
+              std::max(a.split_w_cap, b.split_w_cap)};
 }
 
 int ensure_caps(mox_engine* e, const Caps& need) {
@@ -248,6 +261,16 @@ int alloc_fixed(mox_engine* e) {
   w.b_uniq = (uint64_t*)d; d += NB * 8;
   w.uniq_off = (uint64_t*)d; d += (NB + 1) * 8;
   if ((rc = dalloc(e, (void**)&w.scan_part, (SCAN_WGS + 1) * 8))) return rc;
+  // reduce units (high-cardinality split)
+  if ((rc = dalloc(e, (void**)&w.b_kk, NB * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.u_base, (NB + 1) * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.sub_hist, (size_t)NB * 2 * SUB_N * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.sp_off, (NB + 1) * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.spw_off, (NB + 1) * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.udesc, (size_t)U_MAX * sizeof(UnitDesc)))) return rc;
+  if ((rc = dalloc(e, (void**)&w.big_units, (size_t)U_MAX * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.u_uniq, (size_t)U_MAX * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.u_uniq_off, (size_t)U_MAX * 8))) return rc;
   // Unicode tables
   size_t tb = (2 * MOX_LOWER_N + 2 * MOX_CASED_N + 2 * MOX_CI_N) * 4;
   uint32_t* t;
@@ -321,9 +344,19 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_bucket_scan");
   hipLaunchKernelGGL(k_scatter, dim3(w.map_grid), dim3(1024), 0, s, w);
   q.step("k_scatter");
-  hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);
+  hipLaunchKernelGGL(k_split_count, dim3(NB), dim3(1024), 0, s, w);
+  q.step("k_split_count");
+  hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(NB), 0, s, w);
+  q.step("k_unit_scan");
+  hipLaunchKernelGGL(k_split_scatter, dim3(NB), dim3(1024), 0, s, w);
+  q.step("k_split_scatter");
+  hipLaunchKernelGGL(k_reduce, dim3(2 * e->n_cu), dim3(RED_THREADS), reduce_lds_bytes(), s, w);  // persistent, 2 per CU
   q.step("k_reduce");
+  hipLaunchKernelGGL(k_reduce_small, dim3(4 * e->n_cu), dim3(256), 0, s, w);  // persistent, 4 per CU
+  q.step("k_reduce_small");
   q.rec(4);
+  hipLaunchKernelGGL(k_unit_uniq_scan, dim3(NB), dim3(1024), 0, s, w);
+  q.step("k_unit_uniq_scan");
   hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(NB), 0, s, w);
   q.step("k_final_scan");
   hipLaunchKernelGGL(k_long_flags, dim3(256), dim3(256), 0, s, w, e->d_lens);
@@ -416,6 +449,10 @@ Caps grow_for(mox_engine* e, const Ctl& h) {
   if (h.overflow & OVF_LONG) need.long_cap = next_pow2(2 * h.long_n + 1024);
   if (h.overflow & OVF_TABLE) need.table_cap = h.n_total + h.n_total / 4 + 1024;
   if (h.overflow & OVF_BYTES) need.bytes_cap = h.bytes_total + h.bytes_total / 4 + 65536;
+  if (h.overflow & OVF_SPLIT) {
+    need.split_k_cap = std::max<uint64_t>(need.split_k_cap, h.split_k + h.split_k / 8 + 4096);
+    need.split_w_cap = std::max<uint64_t>(need.split_w_cap, h.split_w + h.split_w / 8 + 4096);
+  }
   // a table overflow also means the byte estimate is stale
   if (h.overflow & OVF_TABLE) need.bytes_cap = std::max(need.bytes_cap, need.table_cap * 16);
   return need;
@@ -523,6 +560,8 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   e->stats.long_tokens = h.long_n;
   e->stats.chunks = h.cold_need;
   e->stats.max_subpasses = h.max_sub ? h.max_sub : 1;
+  e->stats.reduce_units = h.n_units;
+  e->stats.split_partitions = h.n_split;
   e->last_corpus = c;
   e->have_result = true;
   return MOX_OK;

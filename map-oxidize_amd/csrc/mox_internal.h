@@ -32,6 +32,18 @@ constexpr int MAX_SAMPLE_PIECES = 1024;
 constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B
 constexpr int SAMPLE_SLOTS = 2048;
 constexpr int RED_THREADS = 1024;
+// High-cardinality split: a partition whose sampled records are
+// mostly distinct is scattered into 2^kk sub-buckets (the next kk hash bits), and
+// every (partition, sub-bucket) "unit" is reduced by its own workgroup.
+constexpr int SUB_BITS_MAX = 11;
+constexpr int SUB_N = 1 << SUB_BITS_MAX;
+constexpr int U_MAX = NB * SUB_N;           // reduce units
+constexpr uint32_t SPLIT_MIN = 6144;        // records below which a partition is never split
+constexpr uint32_t SPLIT_TARGET = 640;      // records per sub-bucket aimed at
+constexpr uint32_t SMALL_CAP = 1024;        // sub-buckets up to this many records: k_reduce_small
+constexpr uint32_t SPLIT_SAMPLE = 4096;     // records sampled for the distinct-fraction estimate
+constexpr uint32_t SPLIT_PER_REGION = 16;   // ... the first 16 of every map workgroup's region
+constexpr int LC_BITS = 16384;              // linear-counting bitmap of the sample
 constexpr int SCAN_THREADS = 1024;
 constexpr int SCAN_WGS = 1024;
 
@@ -39,13 +51,20 @@ constexpr uint64_t LONG_TAG = 0xFF00000000000000ull;   // w1 marker of a hashed 
 constexpr uint64_t LONG_LEN_MASK = 0x0000FFFFFFFFFFFFull;
 constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points into the arena
 
+// Ablation switches (MOX_DBG env) are compiled in only with -DMOX_ABLATE, so the
+// production kernels carry no runtime debug branches (SGPR pressure in k_map).
+#ifdef MOX_ABLATE
+#define MOX_ABL(d, f) (((d) & (f)) != 0)
+#else
+#define MOX_ABL(d, f) (false)
+#endif
 enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u,
                   DBG_RED_NOSORT = 32u, DBG_RED_NOINSERT = 64u, DBG_RED_NOSLOW = 128u, DBG_COUNT = 256u, DBG_RED_PLAINADD = 512u, DBG_STAMP = 1024u };
 enum : uint32_t {
   OVF_POOL = 1u, OVF_W = 2u, OVF_U = 4u, OVF_LONG = 8u, OVF_ARENA = 16u, OVF_PROBE = 32u,
-  OVF_TABLE = 64u, OVF_BYTES = 128u, OVF_REDUCE = 256u,
+  OVF_TABLE = 64u, OVF_BYTES = 128u, OVF_REDUCE = 256u, OVF_SPLIT = 512u,
   // overflows that make the records of this attempt incomplete
-  OVF_RERUN = OVF_POOL | OVF_W | OVF_U | OVF_LONG | OVF_ARENA | OVF_PROBE
+  OVF_RERUN = OVF_POOL | OVF_W | OVF_U | OVF_LONG | OVF_ARENA | OVF_PROBE | OVF_SPLIT
 };
 
 // Control block: counters written by the kernels, read back once per run.
@@ -72,6 +91,13 @@ struct Ctl {
   unsigned long long spill_need;  // max spill records of any map workgroup
   unsigned long long w_total;     // weighted + spilled records
   unsigned long long dbg_cnt[4];  // MOX_DBG & DBG_COUNT instrumentation
+  unsigned long long n_units;     // reduce units (>= NB; > NB when partitions were split)
+  unsigned long long red_ticket;  // k_reduce work queue
+  unsigned long long split_k;     // cold records of split partitions
+  unsigned long long split_w;     // weighted records of split partitions
+  unsigned int n_split;           // partitions split
+  unsigned int pad2;
+  unsigned long long n_big;       // entries of big_units (k_reduce work list)
 };
 
 // Weighted record: a key with a count (dictionary totals, spills, Unicode-lane
@@ -132,6 +158,15 @@ struct Tables {  // Unicode case data in device memory
   int n_lower, n_cased, n_ci;
 };
 
+// Reduce unit: a whole partition (in_n == UNIT_WHOLE: its cold regions and
+// weighted records) or one sub-bucket of a split partition (contiguous ranges of
+// split_k / split_w).  Output: uk / uc from rec_off.
+constexpr uint32_t UNIT_WHOLE = 0xFFFFFFFFu;
+struct UnitDesc {
+  uint64_t in_off, win_off, rec_off;
+  uint32_t in_n, win_n, part, kk;
+};
+
 struct Corpus {
   const uint8_t* base;   // 16-byte aligned
   uint64_t lo, hi;       // valid bytes [lo, hi) (internal coordinates)
@@ -177,6 +212,20 @@ struct Work {  // device buffers of one engine
   uint64_t* rec_off;              // NB + 1 (output region offsets)
   uint64_t* b_uniq;               // NB
   uint64_t* uniq_off;             // NB + 1
+  // reduce units (partition b = units u_base[b] .. u_base[b+1]-1; one unit
+  // unless b was split into 2^b_kk[b] sub-buckets)
+  uint32_t* b_kk;                 // NB
+  uint32_t* u_base;               // NB + 1
+  uint32_t* sub_hist;             // NB x 2 x SUB_N: cold, weighted records per sub-bucket
+  uint64_t* sp_off;               // NB + 1: first split_k record of partition b
+  uint64_t* spw_off;              // NB + 1: first split_w record of partition b
+  UnitDesc* udesc;                // U_MAX: input ranges + output region of unit u
+  uint32_t* big_units;            // U_MAX: units for k_reduce (whole partitions + oversized sub-buckets)
+  uint64_t* u_uniq;               // U_MAX: distinct keys of unit u
+  uint64_t* u_uniq_off;           // U_MAX: dense table index of unit u's first key
+  uint4* split_k;                 // split_k_cap cold keys grouped by unit
+  WRec* split_w;                  // split_w_cap weighted records grouped by unit
+  uint64_t split_k_cap, split_w_cap;
   // reduce output (capacity = records)
   uint4* uk;                      // keys
   uint64_t* uc;                   // counts

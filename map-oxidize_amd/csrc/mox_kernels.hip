@@ -250,11 +250,11 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
 // region of the word's partition (the shuffle write), no global atomics.
 __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_t w1) {
   const uint32_t h = key_hash(w0, w1);
-  if (m.w.dbg & DBG_NO_EMIT) { asm volatile("" ::"v"(h)); return; }
-  if (m.dict_n && !(m.w.dbg & DBG_NO_DICT)) {
+  if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { asm volatile("" ::"v"(h)); return; }
+  if (m.dict_n && !MOX_ABL(m.w.dbg, DBG_NO_DICT)) {
     const int slot = dict_find(m.s, h, w0, w1);
     if (slot >= 0) {
-      if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
+      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
       return;
     }
   }
@@ -273,7 +273,7 @@ __device__ __forceinline__ void cold_spill(const MapCtx& m, uint4 key) {
 }
 __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
   const uint32_t b = bucket_of(h);
-  if (m.w.dbg & DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
+  if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < m.w.cold_cap) {
@@ -451,7 +451,7 @@ __device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbu
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const bool valid = !(e[u] & 0x8000u);
-    if (valid && hit[u] && !(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[home[u]], 1u);
+    if (valid && hit[u] && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[home[u]], 1u);
     const bool miss = valid && !hit[u];
     const uint64_t bm = __ballot(miss);
     if (miss) list[nmiss + (uint32_t)__popcll(bm & lt)] = (uint16_t)e[u];
@@ -503,7 +503,7 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
     if (!valid[u]) continue;
     const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
     if (hit[u]) {
-      if (!(m.w.dbg & DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
+      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
       continue;
     }
     if (slot[u] >= 0) {  // tag matched another word: full search (rare)
@@ -560,7 +560,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   } else {
     start = ctx ? 0u : slow_starts(m, p0);
   }
-  if (m.w.dbg & DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
+  if MOX_ABL(m.w.dbg, DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
   const uint32_t cnt = __popc(start);
   ntok += cnt;
   // wave-exclusive prefix of cnt (0..16) and the wave total
@@ -594,8 +594,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       if (e & 0x8000u) generic_token(m, sbase + (e & 1023u));
     }
   }
-  if (m.w.dbg & DBG_NO_EMIT) { wave_lds_fence(); return; }
-  const bool use_dict = m.dict_n && !(m.w.dbg & DBG_NO_DICT);
+  if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
+  const bool use_dict = m.dict_n && !MOX_ABL(m.w.dbg, DBG_NO_DICT);
   uint64_t t1 = 0;
   if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
   uint32_t nmiss = 0;
@@ -1277,14 +1277,206 @@ __device__ __forceinline__ bool red_less(const RedLds& s, uint16_t a, uint16_t b
   return (((uint64_t)ka.w << 32) | ka.z) < (((uint64_t)kb.w << 32) | kb.z);
 }
 
-__device__ __forceinline__ bool in_sub(uint32_t h, uint32_t kk, uint32_t sub) {
-  return kk == 0 || ((h << NB_LOG2) >> (32 - kk)) == sub;
+// hash bits used: partition = top NB_LOG2 bits, then (split partitions) the
+// unit's sub-bucket bits, then the in-kernel sub-pass bits, then the sort bins.
+// `shift` = bits above the ones being selected.
+__device__ __forceinline__ uint32_t hbits(uint32_t h, uint32_t shift, uint32_t nbits) {
+  if (nbits == 0 || shift >= 32) return 0;
+  return (h << shift) >> (32 - nbits);
+}
+__device__ __forceinline__ bool in_sub(uint32_t h, uint32_t shift, uint32_t kk, uint32_t sub) {
+  return kk == 0 || hbits(h, shift, kk) == sub;
+}
+// sort bin of a key hash: the RED_SORTB-way split of the 11 bits right below
+// `shift` (ascending bin = ascending hash within the unit / sub-pass); fewer
+// bits (coarser bins, still monotone) once the hash runs out.
+__device__ __forceinline__ uint32_t red_bin(uint32_t h, uint32_t shift) { return shift >= 32 ? 0u : (h << shift) >> (32 - 11); }
+
+// Every cold record of partition b (all map workgroups' regions), one wave per
+// region, 4 x 64 records in flight per wave.
+template <class F>
+__device__ __forceinline__ void for_partition_cold(const Work& w, uint32_t b, F f) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  for (uint32_t g = wv; g < w.map_grid; g += nwv) {
+    const uint32_t n = w.cold_n[(uint64_t)g * NB + b];
+    const uint4* reg = w.cold + ((uint64_t)g * NB + b) * w.cold_cap;
+    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const uint32_t i = i0 + u * 64 + lane;
+        v[u] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (i0 + u * 64 + lane < n) f(v[u]);
+    }
+  }
 }
 
-// sort bin of a key hash: the RED_SORTB-way split of the bits right below the
-// partition bits (ascending bin = ascending hash within the partition)
-__device__ __forceinline__ uint32_t red_bin(uint32_t h) { return (h << NB_LOG2) >> (32 - 11); }
+// ------------------------------------------------------------------ high-cardinality split
+// k_split_count (one workgroup per partition): partitions with more than
+// SPLIT_MIN records estimate their distinct fraction from the first
+// SPLIT_SAMPLE records (linear counting over LC_BITS hash bits).  A mostly
+// distinct partition gets kk = ceil(log2(estimated distinct / SPLIT_TARGET))
+// sub-bucket bits and a full histogram of its records per sub-bucket.
+// Partitions with few distinct keys stay whole (their reduce resolves them in
+// one table, or in a few in-kernel sub-passes).
+extern "C" __global__ __launch_bounds__(1024) void k_split_count(Work w) {
+  __shared__ uint32_t bm[LC_BITS / 32];
+  __shared__ uint32_t hc[SUB_N], hw[SUB_N];
+  __shared__ uint64_t wsum[16];
+  __shared__ uint32_t s_ones, s_kk;
+  const uint32_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (w.ctl->overflow & OVF_RERUN) { if (tid == 0) w.b_kk[b] = 0; return; }
+  const uint64_t nc = w.b_recs[b], nw = w.b_w[b];
+  if (nc + nw <= SPLIT_MIN) { if (tid == 0) w.b_kk[b] = 0; return; }
+  for (int i = tid; i < LC_BITS / 32; i += blockDim.x) bm[i] = 0;
+  if (tid == 0) s_ones = 0;
+  __syncthreads();
+  // sample = the first SPLIT_PER_REGION cold records of every map workgroup's
+  // region (spread over the whole corpus, all loads issued at once), topped
+  // up with weighted records
+  const uint32_t G = w.map_grid;
+  auto mark = [&](uint32_t h) {
+    const uint32_t bit = hbits(h, NB_LOG2, 14);
+    atomicOr(&bm[bit >> 5], 1u << (bit & 31));
+  };
+  uint32_t mine = 0;
+  {
+    constexpr int PER = SPLIT_SAMPLE / 1024;  // sample slots per thread
+    uint4 v[PER];
+    bool ok[PER];
+#pragma unroll
+    for (int j = 0; j < PER; j++) {
+      const uint32_t idx = tid + j * 1024;
+      const uint32_t g = idx / SPLIT_PER_REGION, i = idx % SPLIT_PER_REGION;
+      ok[j] = g < G && i < w.cold_n[(uint64_t)g * NB + b];
+      v[j] = ok[j] ? w.cold[((uint64_t)g * NB + b) * w.cold_cap + i] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < PER; j++)
+      if (ok[j]) { mark(hash32(v[j].x, v[j].y, v[j].z, v[j].w)); mine++; }
+  }
+  uint64_t cs;
+  (void)block_exscan(mine, wsum, cs);
+  const uint64_t ws = cs < SPLIT_SAMPLE ? (nw < SPLIT_SAMPLE - cs ? nw : SPLIT_SAMPLE - cs) : 0;
+  const uint64_t w0 = w.w_off[b];
+  for (uint64_t i = tid; i < ws; i += blockDim.x) { const WRec r = w.w_sorted[w0 + i]; mark(key_hash(r.w0, r.w1)); }
+  __syncthreads();
+  for (int i = tid; i < LC_BITS / 32; i += blockDim.x) atomicAdd(&s_ones, (uint32_t)__popc(bm[i]));
+  __syncthreads();
+  if (tid == 0) {
+    const float n_s = (float)(cs + ws);
+    const float zeros = (float)(LC_BITS - s_ones);
+    const float d = zeros > 0.f ? -(float)LC_BITS * __logf(zeros / (float)LC_BITS) : n_s;
+    const float r = n_s > 0.f ? fminf(d / n_s, 1.f) : 0.f;
+    uint32_t kk = 0;
+    if (r >= 0.5f) {
+      const float est = (float)(nc + nw) * r;
+      while (kk < SUB_BITS_MAX && est > (float)SPLIT_TARGET * (float)(1u << kk)) kk++;
+    }
+    s_kk = kk;
+    w.b_kk[b] = kk;
+  }
+  __syncthreads();
+  const uint32_t kk = s_kk;
+  if (!kk) return;
+  const uint32_t nsub = 1u << kk;
+  for (uint32_t i = tid; i < nsub; i += blockDim.x) { hc[i] = 0; hw[i] = 0; }
+  __syncthreads();
+  for_partition_cold(w, b, [&](uint4 k) { atomicAdd(&hc[hbits(hash32(k.x, k.y, k.z, k.w), NB_LOG2, kk)], 1u); });
+  for (uint64_t i = w0 + tid; i < w0 + nw; i += blockDim.x) {
+    const WRec r = w.w_sorted[i];
+    atomicAdd(&hw[hbits(key_hash(r.w0, r.w1), NB_LOG2, kk)], 1u);
+  }
+  __syncthreads();
+  uint32_t* o = w.sub_hist + (uint64_t)b * 2 * SUB_N;
+  for (uint32_t i = tid; i < nsub; i += blockDim.x) { o[i] = hc[i]; o[SUB_N + i] = hw[i]; }
+}
 
+// One workgroup of NB threads: units per partition, split-buffer offsets, the
+// reduce work-queue reset, and the output region of every whole partition.
+extern "C" __global__ __launch_bounds__(NB) void k_unit_scan(Work w) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t b = threadIdx.x;
+  const uint32_t kk = w.b_kk[b];
+  uint64_t U, tk, tw, ns, nwhole;
+  const uint64_t ub = block_exscan(1ull << kk, wsum, U);
+  const uint64_t ok = block_exscan(kk ? w.b_recs[b] : 0, wsum, tk);
+  const uint64_t ow = block_exscan(kk ? w.b_w[b] : 0, wsum, tw);
+  const uint64_t wi = block_exscan(kk ? 0 : 1, wsum, nwhole);
+  ns = NB - nwhole;
+  w.u_base[b] = (uint32_t)ub;
+  w.b_uniq[b] = 0;  // k_reduce*: set (whole partition) or accumulated (split)
+  w.sp_off[b] = ok;
+  w.spw_off[b] = ow;
+  if (!kk) {
+    w.udesc[ub] = UnitDesc{0, 0, w.rec_off[b], UNIT_WHOLE, 0, b, 0};
+    w.big_units[wi] = (uint32_t)ub;
+  }
+  if (b == 0) {
+    w.u_base[NB] = (uint32_t)U;
+    w.sp_off[NB] = tk;
+    w.spw_off[NB] = tw;
+    w.ctl->n_units = U;
+    w.ctl->n_big = nwhole;  // k_split_scatter appends oversized sub-buckets
+    w.ctl->red_ticket = 0;
+    w.ctl->split_k = tk;
+    w.ctl->split_w = tw;
+    w.ctl->n_split = (uint32_t)ns;
+    if (tk > w.split_k_cap || tw > w.split_w_cap) atomicOr(&w.ctl->overflow, OVF_SPLIT);
+  }
+}
+
+// k_split_scatter (one workgroup per split partition): unit directory from the
+// histogram, then every record of the partition to its unit's contiguous range
+// (LDS cursors: the workgroup owns the whole partition, no global atomics).
+extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
+  __shared__ uint32_t cc[SUB_N], cw[SUB_N];
+  __shared__ uint64_t wsum[16];
+  const uint32_t b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const uint32_t kk = w.b_kk[b];
+  if (!kk || (w.ctl->overflow & OVF_RERUN)) return;
+  const uint32_t nsub = 1u << kk, u0 = w.u_base[b];
+  const uint32_t* hist = w.sub_hist + (uint64_t)b * 2 * SUB_N;
+  const uint32_t s0 = 2 * tid, s1 = 2 * tid + 1;  // SUB_N == 2 x blockDim
+  const uint32_t c0 = s0 < nsub ? hist[s0] : 0, c1 = s1 < nsub ? hist[s1] : 0;
+  const uint32_t d0 = s0 < nsub ? hist[SUB_N + s0] : 0, d1 = s1 < nsub ? hist[SUB_N + s1] : 0;
+  uint64_t tc, tw;
+  const uint64_t ec = block_exscan(c0 + c1, wsum, tc);
+  const uint64_t ew = block_exscan(d0 + d1, wsum, tw);
+  const uint64_t kb = w.sp_off[b], wb = w.spw_off[b], rb = w.rec_off[b];
+  auto unit = [&](uint32_t sb, uint64_t ck, uint32_t nk, uint64_t cwo, uint32_t nwr) {
+    const uint32_t u = u0 + sb;
+    w.udesc[u] = UnitDesc{kb + ck, wb + cwo, rb + ck + cwo, nk, nwr, b, kk};
+    if (nk + nwr > SMALL_CAP) w.big_units[atomicAdd(&w.ctl->n_big, 1ull)] = u;
+    cc[sb] = (uint32_t)ck;
+    cw[sb] = (uint32_t)cwo;
+  };
+  if (s0 < nsub) unit(s0, ec, c0, ew, d0);
+  if (s1 < nsub) unit(s1, ec + c0, c1, ew + d0, d1);
+  __syncthreads();
+  uint4* ok = w.split_k + kb;
+  for_partition_cold(w, b, [&](uint4 k) {
+    const uint32_t p = atomicAdd(&cc[hbits(hash32(k.x, k.y, k.z, k.w), NB_LOG2, kk)], 1u);
+    ok[p] = k;
+  });
+  const uint64_t w0 = w.w_off[b], w1 = w.w_off[b + 1];
+  WRec* ow = w.split_w + wb;
+  for (uint64_t i = w0 + tid; i < w1; i += blockDim.x) {
+    const WRec r = w.w_sorted[i];
+    const uint32_t p = atomicAdd(&cw[hbits(key_hash(r.w0, r.w1), NB_LOG2, kk)], 1u);
+    ow[p] = r;
+  }
+}
+
+// ------------------------------------------------------------------ unit reduce
+// Persistent workgroups (2 per CU) take reduce units from a work queue.  A unit
+// is a whole partition (its cold regions + its weighted records) or one
+// sub-bucket of a split partition (contiguous ranges of split_k / split_w).
 extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) {  // 8 waves per SIMD: 2 workgroups per CU
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   RedLds s;
@@ -1297,163 +1489,397 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   s.fill = (uint16_t*)sp; sp += RED_SORTB * 2;
   s.misc = (uint32_t*)sp; sp += 16;
   __shared__ uint32_t dbgc[4];
-  s.dbg = (w.dbg & DBG_COUNT) ? dbgc : nullptr;
-  s.plain = (w.dbg & DBG_RED_PLAINADD) != 0;
+  __shared__ uint32_t s_unit;
+  s.dbg = MOX_ABL(w.dbg, DBG_COUNT) ? dbgc : nullptr;
+  s.plain = MOX_ABL(w.dbg, DBG_RED_PLAINADD) != 0;
   if (threadIdx.x < 4) dbgc[threadIdx.x] = 0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NWV = RED_THREADS / 64;
-  const uint32_t b = blockIdx.x;
   const uint32_t G = w.map_grid;
   uint32_t* tags = reinterpret_cast<uint32_t*>(s.tag4);
-  // an overflowed map or directory means this attempt is rerun with larger
-  // buffers: its records are incomplete (w_sorted may not even be written)
-  if (w.ctl->overflow & OVF_RERUN) {
-    if (tid == 0) w.b_uniq[b] = 0;
-    return;
-  }
-  const uint64_t ws0 = w.w_off[b], ws1 = w.w_off[b + 1];
-  const uint64_t out0 = w.rec_off[b];
-  const bool stamp = (w.dbg & DBG_STAMP) && tid == 0;
-  if (stamp) w.stamps[b * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-  uint32_t kk = 0;
-  uint64_t written = 0;
-  for (uint32_t sub = 0; sub < (1u << kk);) {
-    for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
-    if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
-    __syncthreads();
-    // cold regions: wave wv streams regions g = wv, wv + NWV, ... in chunks of
-    // 64 x RED_UNROLL records, the next chunk's loads in flight while the
-    // current one is inserted.  Lane k holds the size of the wave's k-th region.
-    {
-      const uint32_t nreg = G > (uint32_t)wv ? (G - wv + NWV - 1) / NWV : 0;  // <= 64 (G <= MAX_MAP_GRID)
-      const uint32_t myn = lane < (int)nreg ? w.cold_n[(uint64_t)(wv + lane * NWV) * NB + b] : 0u;
-      const uint64_t nonempty = __ballot(myn != 0);
-      auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
-        const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
-        return m ? (uint32_t)__builtin_ctzll(m) : nreg;
-      };
-      auto load = [&](uint32_t k, uint32_t i0, uint4 (&v)[RED_UNROLL]) {
-        const uint32_t n = __builtin_amdgcn_readlane(myn, k);
-        const uint4* reg = w.cold + ((uint64_t)(wv + k * NWV) * NB + b) * w.cold_cap;
-#pragma unroll
-        for (int u = 0; u < RED_UNROLL; u++) {
-          const uint32_t i = i0 + u * 64 + lane;
-          v[u] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
-        }
-      };
-      uint32_t k = next_region(0), i0 = 0;
-      uint4 cur[RED_UNROLL], nxt[RED_UNROLL];
-      if (k < nreg) load(k, 0, cur);
-      while (k < nreg) {
-        uint32_t k2 = k, i2 = i0 + 64 * RED_UNROLL;
-        if (i2 >= __builtin_amdgcn_readlane(myn, k)) { k2 = next_region(k + 1); i2 = 0; }
-        if (k2 < nreg) load(k2, i2, nxt);
-        if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // else: redone anyway
-          uint32_t h[RED_UNROLL];
-          bool todo[RED_UNROLL];
-#pragma unroll
-          for (int u = 0; u < RED_UNROLL; u++) {
-            h[u] = hash32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
-            todo[u] = (cur[u].x | cur[u].y) != 0 && in_sub(h[u], kk, sub);
-          }
-          if (!(w.dbg & DBG_RED_NOINSERT)) {
-#pragma unroll
-            for (int u = 0; u < RED_UNROLL; u++)
-              if (todo[u]) todo[u] = !red_try(s, h[u], cur[u], 1);
-#pragma unroll
-            for (int u = 0; u < RED_UNROLL; u++)
-              if (todo[u] && !(w.dbg & DBG_RED_NOSLOW)) red_insert(s, h[u], cur[u], 1);
-          } else {
-            asm volatile("" ::"v"(h[0]), "v"(h[1]), "v"(h[2]), "v"(h[3]));
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < RED_UNROLL; u++) cur[u] = nxt[u];
-        k = k2;
-        i0 = i2;
-      }
-    }
-    if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
-    for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
-      const WRec rr = w.w_sorted[i];
-      const uint4 k = make_uint4((uint32_t)rr.w0, (uint32_t)(rr.w0 >> 32), (uint32_t)rr.w1, (uint32_t)(rr.w1 >> 32));
-      const uint32_t h = hash32(k.x, k.y, k.z, k.w);
-      if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && in_sub(h, kk, sub) &&
-          !red_try(s, h, k, rr.count))
-        red_insert(s, h, k, rr.count);
+  // an overflowed map, directory or split means this attempt is rerun with
+  // larger buffers: its records are incomplete (nothing downstream reads them)
+  if (w.ctl->overflow & OVF_RERUN) return;
+  const uint32_t NBIG = (uint32_t)w.ctl->n_big;
+  uint32_t max_kk = 0;
+  for (;;) {
+    if (tid == 0) {
+      const uint32_t t = (uint32_t)atomicAdd(&w.ctl->red_ticket, 1ull);
+      s_unit = t < NBIG ? w.big_units[t] : 0xFFFFFFFFu;
     }
     __syncthreads();
-    if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the partition
-      kk++;
-      if (kk > 32 - NB_LOG2) {  // > RED_CAP distinct keys share every hash bit: cannot split
-        if (tid == 0) { atomicOr(&w.ctl->overflow, OVF_REDUCE); w.b_uniq[b] = 0; }
-        return;
-      }
-      sub = 0;
-      written = 0;
+    const uint32_t u = s_unit;
+    __syncthreads();
+    if (u == 0xFFFFFFFFu) break;
+    const UnitDesc ud = w.udesc[u];
+    const uint32_t b = ud.part;
+    const bool split = ud.in_n != UNIT_WHOLE;
+    const uint32_t shift0 = NB_LOG2 + ud.kk;
+    uint64_t ws0, ws1;
+    const WRec* wsrc;
+    if (split) { wsrc = w.split_w; ws0 = ud.win_off; ws1 = ws0 + ud.win_n; }
+    else { wsrc = w.w_sorted; ws0 = w.w_off[b]; ws1 = w.w_off[b + 1]; }
+    const uint64_t out0 = ud.rec_off;
+    // split unit: its contiguous cold range is cut into NWV wave chunks
+    const uint64_t kin0 = split ? ud.in_off : 0;
+    const uint32_t kin_n = split ? ud.in_n : 0;
+    const uint32_t kchunk = (kin_n + NWV - 1) / NWV;
+    const bool stamp = MOX_ABL(w.dbg, DBG_STAMP) && tid == 0 && !split;
+    if (stamp) w.stamps[b * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+    uint32_t kk = 0;
+    uint64_t written = 0;
+    bool failed = false;
+    for (uint32_t sub = 0; sub < (1u << kk);) {
+      for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
+      if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
       __syncthreads();
-      continue;
-    }
-    // deterministic order (h32, key): bucket sort by the hash bits below the
-    // partition bits, then (h32, key) insertion sort inside each bin (~0.7 keys)
-    if (stamp) w.stamps[b * 8 + 2] = __builtin_amdgcn_s_memrealtime();  // all waves done inserting
-    const uint32_t nu = s.misc[0];
-    for (int i = tid; i < RED_SORTB; i += RED_THREADS) { s.bin[i] = 0; s.fill[i] = 0; }
-    __syncthreads();
-    for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
-      if (tags[i]) atomicAdd(reinterpret_cast<uint32_t*>(s.bin) + (red_bin(tags[i]) >> 1), 1u << (16 * (red_bin(tags[i]) & 1)));
-    __syncthreads();
-    {  // exclusive scan of the RED_SORTB bin counts (2 per thread)
-      __shared__ uint64_t wsum[RED_THREADS / 64];
-      uint64_t tot;
-      const uint32_t c0 = s.bin[2 * tid], c1 = s.bin[2 * tid + 1];
-      const uint64_t ex = block_exscan(c0 + c1, wsum, tot);
-      s.bin[2 * tid] = (uint16_t)ex;
-      s.bin[2 * tid + 1] = (uint16_t)(ex + c0);
-      if (tid == 0) s.bin[RED_SORTB] = (uint16_t)tot;
-    }
-    __syncthreads();
-    for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
-      if (tags[i]) {
-        const uint32_t bn = red_bin(tags[i]);
-        const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(s.fill) + (bn >> 1), 1u << (16 * (bn & 1)));
-        const uint32_t p = s.bin[bn] + ((old >> (16 * (bn & 1))) & 0xFFFFu);
-        s.idx[p] = (uint16_t)i;
-      }
-    __syncthreads();
-    if (!(w.dbg & DBG_RED_NOSORT)) {
-      for (int bn = tid; bn < RED_SORTB; bn += RED_THREADS) {
-        const uint32_t lo = s.bin[bn], hi = s.bin[bn + 1];
-        for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort of a tiny bin
-          const uint16_t x = s.idx[i];
-          uint32_t j = i;
-          while (j > lo && red_less(s, x, s.idx[j - 1])) { s.idx[j] = s.idx[j - 1]; j--; }
-          s.idx[j] = x;
+      // cold records: wave wv streams its regions (whole partition: regions
+      // g = wv, wv + NWV, ...; split unit: one chunk) 64 x RED_UNROLL records at
+      // a time, the next chunk's loads in flight while the current one is
+      // inserted.  Lane k holds the size of the wave's k-th region.
+      {
+        uint32_t nreg, myn;
+        if (split) {
+          nreg = 1;
+          const uint64_t a = (uint64_t)wv * kchunk;
+          myn = lane == 0 && a < kin_n ? (uint32_t)(kin_n - a < kchunk ? kin_n - a : kchunk) : 0u;
+        } else {
+          nreg = G > (uint32_t)wv ? (G - wv + NWV - 1) / NWV : 0;  // <= 64 (G <= MAX_MAP_GRID)
+          myn = lane < (int)nreg ? w.cold_n[(uint64_t)(wv + lane * NWV) * NB + b] : 0u;
+        }
+        const uint64_t nonempty = __ballot(myn != 0);
+        auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
+          const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
+          return m ? (uint32_t)__builtin_ctzll(m) : nreg;
+        };
+        auto load = [&](uint32_t k, uint32_t i0, uint4 (&v)[RED_UNROLL]) {
+          const uint32_t n = __builtin_amdgcn_readlane(myn, k);
+          const uint4* reg = split ? w.split_k + kin0 + (uint64_t)wv * kchunk
+                                   : w.cold + ((uint64_t)(wv + k * NWV) * NB + b) * w.cold_cap;
+#pragma unroll
+          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+            const uint32_t i = i0 + u2 * 64 + lane;
+            v[u2] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
+          }
+        };
+        uint32_t k = next_region(0), i0 = 0;
+        uint4 cur[RED_UNROLL], nxt[RED_UNROLL];
+        if (k < nreg) load(k, 0, cur);
+        while (k < nreg) {
+          uint32_t k2 = k, i2 = i0 + 64 * RED_UNROLL;
+          if (i2 >= __builtin_amdgcn_readlane(myn, k)) { k2 = next_region(k + 1); i2 = 0; }
+          if (k2 < nreg) load(k2, i2, nxt);
+          if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // else: redone anyway
+            uint32_t h[RED_UNROLL];
+            bool todo[RED_UNROLL];
+#pragma unroll
+            for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+              h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
+              todo[u2] = (cur[u2].x | cur[u2].y) != 0 && in_sub(h[u2], shift0, kk, sub);
+            }
+            if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
+#pragma unroll
+              for (int u2 = 0; u2 < RED_UNROLL; u2++)
+                if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+#pragma unroll
+              for (int u2 = 0; u2 < RED_UNROLL; u2++)
+                if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
+            } else {
+              asm volatile("" ::"v"(h[0]), "v"(h[1]));
+            }
+          }
+#pragma unroll
+          for (int u2 = 0; u2 < RED_UNROLL; u2++) cur[u2] = nxt[u2];
+          k = k2;
+          i0 = i2;
         }
       }
+      if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
+      for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
+        const WRec rr = wsrc[i];
+        const uint4 k = make_uint4((uint32_t)rr.w0, (uint32_t)(rr.w0 >> 32), (uint32_t)rr.w1, (uint32_t)(rr.w1 >> 32));
+        const uint32_t h = hash32(k.x, k.y, k.z, k.w);
+        if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && in_sub(h, shift0, kk, sub) &&
+            !red_try(s, h, k, rr.count))
+          red_insert(s, h, k, rr.count);
+      }
+      __syncthreads();
+      if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the unit
+        kk++;
+        __syncthreads();
+        if (shift0 + kk > 32) {  // > RED_CAP distinct keys share every hash bit: cannot split
+          if (tid == 0) atomicOr(&w.ctl->overflow, OVF_REDUCE);
+          failed = true;
+          break;
+        }
+        sub = 0;
+        written = 0;
+        continue;
+      }
+      // deterministic order (h32, key): bucket sort by the hash bits below the
+      // unit and sub-pass bits, then (h32, key) insertion sort inside each bin
+      if (stamp) w.stamps[b * 8 + 2] = __builtin_amdgcn_s_memrealtime();  // all waves done inserting
+      const uint32_t nu = s.misc[0];
+      const uint32_t bsh = shift0 + kk;
+      for (int i = tid; i < RED_SORTB; i += RED_THREADS) { s.bin[i] = 0; s.fill[i] = 0; }
+      __syncthreads();
+      for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
+        if (tags[i]) {
+          const uint32_t bn = red_bin(tags[i], bsh);
+          atomicAdd(reinterpret_cast<uint32_t*>(s.bin) + (bn >> 1), 1u << (16 * (bn & 1)));
+        }
+      __syncthreads();
+      {  // exclusive scan of the RED_SORTB bin counts (2 per thread)
+        __shared__ uint64_t wsum[RED_THREADS / 64];
+        uint64_t tot;
+        const uint32_t c0 = s.bin[2 * tid], c1 = s.bin[2 * tid + 1];
+        const uint64_t ex = block_exscan(c0 + c1, wsum, tot);
+        s.bin[2 * tid] = (uint16_t)ex;
+        s.bin[2 * tid + 1] = (uint16_t)(ex + c0);
+        if (tid == 0) s.bin[RED_SORTB] = (uint16_t)tot;
+      }
+      __syncthreads();
+      for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
+        if (tags[i]) {
+          const uint32_t bn = red_bin(tags[i], bsh);
+          const uint32_t old = atomicAdd(reinterpret_cast<uint32_t*>(s.fill) + (bn >> 1), 1u << (16 * (bn & 1)));
+          const uint32_t p = s.bin[bn] + ((old >> (16 * (bn & 1))) & 0xFFFFu);
+          s.idx[p] = (uint16_t)i;
+        }
+      __syncthreads();
+      if (!MOX_ABL(w.dbg, DBG_RED_NOSORT)) {
+        for (int bn = tid; bn < RED_SORTB; bn += RED_THREADS) {
+          const uint32_t lo = s.bin[bn], hi = s.bin[bn + 1];
+          for (uint32_t i = lo + 1; i < hi; i++) {  // insertion sort of a tiny bin
+            const uint16_t x = s.idx[i];
+            uint32_t j = i;
+            while (j > lo && red_less(s, x, s.idx[j - 1])) { s.idx[j] = s.idx[j - 1]; j--; }
+            s.idx[j] = x;
+          }
+        }
+      }
+      __syncthreads();
+      if (stamp) w.stamps[b * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // sorted
+      for (uint32_t i = tid; i < nu; i += RED_THREADS) {
+        const uint16_t sl = s.idx[i];
+        w.uk[out0 + written + i] = s.key[sl];
+        w.uc[out0 + written + i] = s.cnt[sl];
+      }
+      written += nu;
+      sub++;
+      __syncthreads();
     }
-    __syncthreads();
-    if (stamp) w.stamps[b * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // sorted
-    for (uint32_t i = tid; i < nu; i += RED_THREADS) {
-      const uint16_t sl = s.idx[i];
-      w.uk[out0 + written + i] = s.key[sl];
-      w.uc[out0 + written + i] = s.cnt[sl];
+    if (stamp) {
+      w.stamps[b * 8 + 4] = __builtin_amdgcn_s_memrealtime();
+      uint32_t hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      w.stamps[b * 8 + 5] = hw;
+      w.stamps[b * 8 + 6] = s.misc[0];
     }
-    written += nu;
-    sub++;
+    if (tid == 0) {
+      w.u_uniq[u] = failed ? 0 : written;
+      if (!split) w.b_uniq[b] = failed ? 0 : written;  // split partitions: summed by k_unit_uniq_scan
+    }
+    if (kk > max_kk) max_kk = kk;
     __syncthreads();
-  }
-  if (stamp) {
-    w.stamps[b * 8 + 4] = __builtin_amdgcn_s_memrealtime();
-    uint32_t hw;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-    w.stamps[b * 8 + 5] = hw;
-    w.stamps[b * 8 + 6] = s.misc[0];
   }
   if (tid == 0) {
-    w.b_uniq[b] = written;
-    if (kk) atomicMax(&w.ctl->max_sub, 1u << kk);
+    if (max_kk) atomicMax(&w.ctl->max_sub, 1u << max_kk);
     if (s.dbg) for (int i = 0; i < 3; i++) atomicAdd(&w.ctl->dbg_cnt[i], (unsigned long long)dbgc[i]);
+  }
+}
+
+// ------------------------------------------------------------------ small-unit reduce
+// Sub-buckets of split partitions with <= SMALL_CAP records (the common case
+// of high-cardinality input).  Persistent 256-thread workgroups (4 per CU) take
+// units grid-strided, no work queue.  Per unit: records into LDS, counting sort
+// by the 10 hash bits below the unit's bits (~0.7 records per bin), (h32, key)
+// insertion sort inside bins, so equal keys are adjacent; run heads are
+// compacted by a block scan and each head sums its run.  Output order (h32,
+// key), as k_reduce.
+constexpr int SR_THREADS = 256;
+constexpr int SR_PER = SMALL_CAP / SR_THREADS;  // records (and sorted positions) per thread
+constexpr int SR_BINS = 1024;
+static_assert(SR_PER * SR_THREADS == (int)SMALL_CAP && SR_BINS == 4 * SR_THREADS, "k_reduce_small geometry");
+
+// LDS-only workgroup barrier: the DS queue drained, no wait on global stores
+// still in flight (a __syncthreads fence would wait for them).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// inclusive wave scan of x (wave64)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  return x;
+}
+
+struct SmallIn {
+  uint4 k[SR_PER];
+  unsigned long long c[SR_PER];
+};
+__device__ __forceinline__ bool small_unit(const UnitDesc& d) { return d.in_n != UNIT_WHOLE && d.in_n + d.win_n <= SMALL_CAP; }
+// Descriptor of unit min(u, U - 1): no select on the loaded value, so the load
+// stays in flight until first use (the caller checks u < U there).
+__device__ __forceinline__ UnitDesc load_desc(const Work& w, uint32_t u, uint32_t U) { return w.udesc[u < U ? u : U - 1]; }
+// Branch-free raw loads (one address select per slot, invalid slots read a
+// valid dummy address, no select on loaded values): the compiler leaves them
+// in flight until the next iteration uses them.  c[j] is meaningful only for
+// weighted slots (i >= in_n).
+__device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, bool ok, SmallIn& in) {
+  const uint32_t nk = d.in_n, n = d.in_n + d.win_n;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int j = 0; j < SR_PER; j++) {
+    const uint32_t i = threadIdx.x + j * SR_THREADS;
+    const bool valid = ok && i < n, cold = i < nk;
+    const uint8_t* kp = cold ? reinterpret_cast<const uint8_t*>(w.split_k + d.in_off + i)
+                             : reinterpret_cast<const uint8_t*>(w.split_w + d.win_off + (i - nk));
+    if (!valid) kp = reinterpret_cast<const uint8_t*>(w.split_k);
+    const uint8_t* cp = (valid && !cold) ? kp + 16 : kp;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(kp);
+    in.k[j] = make_uint4(v.x, v.y, v.z, v.w);
+    in.c[j] = *reinterpret_cast<const unsigned long long*>(cp);
+  }
+}
+
+// Sub-buckets of split partitions with <= SMALL_CAP records (the common case of
+// high-cardinality input).  Persistent 256-thread workgroups (4 per CU) take
+// units grid-strided (no work queue); the next unit's descriptor and records
+// are loaded into registers while the current one is processed.  Per unit:
+// records into LDS, counting sort by the 10 hash bits below the unit's bits
+// (~0.5 records per bin), (h32, key) insertion sort inside bins so equal keys
+// are adjacent, run heads compacted by a scan, each head sums its run.  Output
+// order (h32, key), as k_reduce.
+extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) {
+  __shared__ uint4 key[SMALL_CAP];
+  __shared__ unsigned long long cnt[SMALL_CAP];
+  __shared__ uint32_t hh[SMALL_CAP];
+  __shared__ uint16_t rk[SMALL_CAP];
+  __shared__ uint16_t idx[SMALL_CAP];
+  __shared__ uint32_t bins[SR_BINS / 2];  // u16 pairs: counts, then exclusive starts
+  __shared__ uint32_t wsa[SR_THREADS / 64], wsb[SR_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (w.ctl->overflow & OVF_RERUN) return;
+  const uint32_t U = (uint32_t)w.ctl->n_units;
+  const uint32_t G = gridDim.x;
+  uint16_t* bin16 = reinterpret_cast<uint16_t*>(bins);
+  __shared__ UnitDesc dring[2];  // descriptors of this and the next unit (written one unit ahead)
+  uint32_t u = blockIdx.x;
+  if (u >= U) return;
+  if (tid == 0) { dring[0] = load_desc(w, u, U); dring[1] = load_desc(w, u + G, U); }
+  bins[tid] = 0;
+  bins[tid + SR_THREADS] = 0;
+  lds_barrier();
+  SmallIn in;
+  {
+    const UnitDesc d0 = dring[0];
+    load_small(w, d0, small_unit(d0), in);
+  }
+  for (uint32_t it = 0; u < U; u += G, it++) {
+    const UnitDesc d = dring[it & 1], dn = dring[(it + 1) & 1];
+    const bool cur_small = small_unit(d);
+    const uint32_t n = d.in_n + d.win_n, shift = NB_LOG2 + d.kk;
+    // this unit's records into LDS + bin counts (bins were zeroed by the previous unit)
+    if (cur_small) {
+#pragma unroll
+      for (int j = 0; j < SR_PER; j++) {
+        const uint32_t i = tid + j * SR_THREADS;
+        if (i < n) {
+          const uint32_t h = hash32(in.k[j].x, in.k[j].y, in.k[j].z, in.k[j].w);
+          const uint32_t bn = hbits(h, shift, 10);
+          key[i] = in.k[j];
+          cnt[i] = i < d.in_n ? 1ull : in.c[j];
+          hh[i] = h;
+          const uint32_t old = atomicAdd(&bins[bn >> 1], 1u << (16 * (bn & 1)));
+          rk[i] = (uint16_t)((old >> (16 * (bn & 1))) & 0xFFFFu);
+        }
+      }
+    }
+    // the next unit's records and the descriptor after it: in flight during this unit
+    SmallIn inn;
+    load_small(w, dn, u + G < U && small_unit(dn), inn);
+    UnitDesc dnn;
+    if (tid == 0) dnn = load_desc(w, u + 2 * G, U);
+    if (cur_small) {
+      lds_barrier();
+      {  // exclusive scan of the bin counts: bins 4t..4t+3 per thread
+        const uint32_t p0 = bins[2 * tid], p1 = bins[2 * tid + 1];
+        const uint32_t c0 = p0 & 0xFFFFu, c1 = p0 >> 16, c2 = p1 & 0xFFFFu, c3 = p1 >> 16;
+        const uint32_t incl = wave_incl_scan(c0 + c1 + c2 + c3);
+        if (lane == 63) wsa[wv] = incl;
+        lds_barrier();
+        uint32_t ex = incl - (c0 + c1 + c2 + c3);
+        for (int k = 0; k < wv; k++) ex += wsa[k];
+        bins[2 * tid] = ex | ((ex + c0) << 16);
+        bins[2 * tid + 1] = (ex + c0 + c1) | ((ex + c0 + c1 + c2) << 16);
+      }
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < SR_PER; j++) {
+        const uint32_t i = tid + j * SR_THREADS;
+        if (i < n) idx[bin16[hbits(hh[i], shift, 10)] + rk[i]] = (uint16_t)i;
+      }
+      lds_barrier();
+#pragma unroll
+      for (int j = 0; j < 4; j++) {  // (h32, key) insertion sort of this thread's 4 tiny bins
+        const uint32_t bn = 4 * tid + j;
+        const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
+        for (uint32_t i = lo + 1; i < hi; i++) {
+          const uint16_t x = idx[i];
+          const uint32_t hx = hh[x];
+          const uint4 kx = key[x];
+          uint32_t q = i;
+          while (q > lo) {
+            const uint16_t y = idx[q - 1];
+            const uint32_t hy = hh[y];
+            bool less = hx < hy;
+            if (hx == hy) {
+              const uint4 ky = key[y];
+              const uint64_t a0 = ((uint64_t)kx.y << 32) | kx.x, b0 = ((uint64_t)ky.y << 32) | ky.x;
+              less = a0 != b0 ? a0 < b0 : ((((uint64_t)kx.w << 32) | kx.z) < (((uint64_t)ky.w << 32) | ky.z));
+            }
+            if (!less) break;
+            idx[q] = y;
+            q--;
+          }
+          idx[q] = x;
+        }
+      }
+      lds_barrier();
+      bins[tid] = 0;  // bin starts are dead after the sort: zero for the next unit
+      bins[tid + SR_THREADS] = 0;
+      // run heads at sorted positions 4t..4t+3 -> output index by scan
+      uint32_t hm = 0, nh = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const uint32_t p = 4 * tid + j;
+        if (p < n && (p == 0 || !key_eq16(key[idx[p]], key[idx[p - 1]]))) { hm |= 1u << j; nh++; }
+      }
+      const uint32_t incl = wave_incl_scan(nh);
+      if (lane == 63) wsb[wv] = incl;
+      lds_barrier();
+      uint32_t o = incl - nh, nu = 0;
+      for (int k = 0; k < SR_THREADS / 64; k++) { if (k < wv) o += wsb[k]; nu += wsb[k]; }
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        if (!((hm >> j) & 1u)) continue;
+        const uint32_t p = 4 * tid + j;
+        const uint4 k = key[idx[p]];
+        unsigned long long c = cnt[idx[p]];
+        for (uint32_t q = p + 1; q < n && key_eq16(key[idx[q]], k); q++) c += cnt[idx[q]];
+        w.uk[d.rec_off + o] = k;
+        w.uc[d.rec_off + o] = c;
+        o++;
+      }
+      if (tid == 0) w.u_uniq[u] = nu;  // summed per partition by k_unit_uniq_scan
+    }
+    if (tid == 0) dring[it & 1] = dnn;
+    lds_barrier();  // LDS reused by the next unit
+    in = inn;
   }
 }
 
@@ -1530,13 +1956,16 @@ __device__ __forceinline__ uint32_t short_len(uint64_t w0, uint64_t w1) {
   return 8 - (__clzll(w0) >> 3);
 }
 
-// After k_reduce: total short uniques + offsets; n_total = short + long.
+// After k_reduce + k_unit_uniq_scan: total short uniques + per-partition dense
+// offsets; n_total = short + long.
 extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {  // one workgroup of NB threads
   __shared__ uint64_t wsum[16];
   uint64_t tot;
-  const uint64_t ex = block_exscan(w.b_uniq[threadIdx.x], wsum, tot);
-  w.uniq_off[threadIdx.x] = ex;
-  if (threadIdx.x == 0) {
+  const bool rerun = (w.ctl->overflow & OVF_RERUN) != 0;  // nothing was reduced
+  const uint32_t b = threadIdx.x;
+  const uint64_t ex = block_exscan(rerun ? 0 : w.b_uniq[b], wsum, tot);
+  w.uniq_off[b] = ex;
+  if (b == 0) {
     w.uniq_off[NB] = tot;
     w.ctl->n_short = tot;
     const unsigned long long nl = w.ctl->long_uniq;
@@ -1545,24 +1974,43 @@ extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {  // one 
   }
 }
 
-// counts + lengths in dense order; lengths go to t_offs[] (scanned in place afterwards)
+// Dense offsets of units relative to their partition, and the distinct keys of
+// split partitions (one workgroup per partition; no global atomics in the
+// reduce kernels, whose units of one partition run side by side).
+extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t b = blockIdx.x;
+  if (w.ctl->overflow & OVF_RERUN) return;
+  const uint32_t kk = w.b_kk[b], u0 = w.u_base[b];
+  if (!kk) { if (threadIdx.x == 0) w.u_uniq_off[u0] = 0; return; }
+  const uint32_t nsub = 1u << kk;
+  const uint32_t s0 = 2 * threadIdx.x, s1 = s0 + 1;  // SUB_N == 2 x blockDim
+  const uint64_t v0 = s0 < nsub ? w.u_uniq[u0 + s0] : 0, v1 = s1 < nsub ? w.u_uniq[u0 + s1] : 0;
+  uint64_t tot;
+  const uint64_t ex = block_exscan(v0 + v1, wsum, tot);
+  if (s0 < nsub) w.u_uniq_off[u0 + s0] = ex;
+  if (s1 < nsub) w.u_uniq_off[u0 + s1] = ex + v0;
+  if (threadIdx.x == 0) w.b_uniq[b] = tot;
+}
+
+// True when this attempt produced a complete short-word table.
+__device__ __forceinline__ bool table_ok(const Work& w) {
+  return !(w.ctl->overflow & OVF_RERUN) && w.ctl->n_total <= w.table_cap;
+}
+
+// counts + lengths in dense order, one reduce unit per workgroup iteration;
+// lengths go to lens[] (scanned into t_offs afterwards)
 extern "C" __global__ void k_mat_counts(Work w, uint64_t* lens) {
-  __shared__ uint64_t uoff[NB + 1];
-  __shared__ uint64_t roff[NB + 1];
-  for (int i = threadIdx.x; i <= NB; i += blockDim.x) { uoff[i] = w.uniq_off[i]; roff[i] = w.rec_off[i]; }
-  __syncthreads();
-  uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
-  if (nt > w.table_cap) return;
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-    {
-      int a = 0, b = NB - 1;  // bucket with uoff[bk] <= i < uoff[bk+1]
-      while (a < b) { int m = (a + b + 1) >> 1; if (uoff[m] <= i) a = m; else b = m - 1; }
-      uint64_t src = roff[a] + (i - uoff[a]);
-      uint4 k = w.uk[src];
-      uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
-      w.t_counts[i] = w.uc[src];
-      lens[i] = short_len(w0, w1);
+  if (!table_ok(w)) return;
+  const uint32_t U = (uint32_t)w.ctl->n_units;
+  for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
+    const UnitDesc ud = w.udesc[u];
+    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint4 k = w.uk[src0 + i];
+      const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
+      w.t_counts[dst0 + i] = w.uc[src0 + i];
+      lens[dst0 + i] = short_len(w0, w1);
     }
   }
 }
@@ -1582,24 +2030,22 @@ extern "C" __global__ void k_mat_long(Work w, uint64_t* lens) {
 }
 
 extern "C" __global__ void k_mat_bytes(Work w, Corpus c) {
-  __shared__ uint64_t uoff[NB + 1];
-  __shared__ uint64_t roff[NB + 1];
-  for (int i = threadIdx.x; i <= NB; i += blockDim.x) { uoff[i] = w.uniq_off[i]; roff[i] = w.rec_off[i]; }
-  __syncthreads();
-  uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
-  if (nt > w.table_cap) return;
+  if (!table_ok(w)) return;
+  const uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
   if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->bytes_total = w.t_offs[nt];
   if (w.t_offs[nt] > w.bytes_cap) { if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&w.ctl->overflow, OVF_BYTES); return; }
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-    int a = 0, b = NB - 1;
-    while (a < b) { int m = (a + b + 1) >> 1; if (uoff[m] <= i) a = m; else b = m - 1; }
-    uint64_t src = roff[a] + (i - uoff[a]);
-    uint4 k = w.uk[src];
-    uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
-    uint32_t L = short_len(w0, w1);
-    uint8_t* o = w.t_bytes + w.t_offs[i];
-    for (uint32_t j = 0; j < L; j++) o[j] = (uint8_t)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xFF);
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  const uint32_t U = (uint32_t)w.ctl->n_units;
+  for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
+    const UnitDesc ud = w.udesc[u];
+    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint4 k = w.uk[src0 + i];
+      const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
+      const uint32_t L = short_len(w0, w1);
+      uint8_t* o = w.t_bytes + w.t_offs[dst0 + i];
+      for (uint32_t j = 0; j < L; j++) o[j] = (uint8_t)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xFF);
+    }
   }
   for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
     LSlot e = w.ltab[s];
@@ -1633,20 +2079,16 @@ extern "C" __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt) {
   }
 }
 
-// Short words in dense order as WRec (same source mapping as k_mat_counts).
+// Short words in dense order as WRec (same unit mapping as k_mat_counts).
 extern "C" __global__ void k_xpack_short(Work w, WRec* out) {
-  __shared__ uint64_t uoff[NB + 1];
-  __shared__ uint64_t roff[NB + 1];
-  for (int i = threadIdx.x; i <= NB; i += blockDim.x) { uoff[i] = w.uniq_off[i]; roff[i] = w.rec_off[i]; }
-  __syncthreads();
-  const uint64_t ns = w.ctl->n_short;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-    int a = 0, b = NB - 1;
-    while (a < b) { int m = (a + b + 1) >> 1; if (uoff[m] <= i) a = m; else b = m - 1; }
-    const uint64_t src = roff[a] + (i - uoff[a]);
-    const uint4 k = w.uk[src];
-    out[i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, w.uc[src]};
+  const uint32_t U = (uint32_t)w.ctl->n_units;
+  for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
+    const UnitDesc ud = w.udesc[u];
+    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const uint4 k = w.uk[src0 + i];
+      out[dst0 + i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, w.uc[src0 + i]};
+    }
   }
 }
 

@@ -87,6 +87,9 @@ class Stats(ctypes.Structure):
         ("ms_h2d", ctypes.c_double),
         ("ms_d2h", ctypes.c_double),
         ("ms_exchange", ctypes.c_double),
+        ("reduce_units", ctypes.c_uint64),
+        ("split_partitions", ctypes.c_uint32),
+        ("pad0", ctypes.c_uint32),
     ]
 
     def as_dict(self):
@@ -166,7 +169,8 @@ class Table:
         counts = np.ctypeslib.as_array(t.counts, shape=(n,)).copy() if n else np.zeros(0, np.uint64)
         offs = np.ctypeslib.as_array(t.offs, shape=(n + 1,)).copy()
         nb = int(offs[-1]) if n else 0
-        data = ctypes.string_at(t.bytes, nb) if nb else b""
+        # (ctypes.string_at takes a C int size: tables above 2 GiB of bytes need numpy)
+        data = np.ctypeslib.as_array(t.bytes, shape=(nb,)).tobytes() if nb else b""
         return counts, offs, data
 
     def arrays(self):

@@ -76,7 +76,7 @@ def count_arrays(data, nthreads=8):
         nn = t.n
         counts = np.ctypeslib.as_array(t.counts, shape=(nn,)).copy() if nn else np.zeros(0, np.uint64)
         offs = np.ctypeslib.as_array(t.offs, shape=(nn + 1,)).copy()
-        raw = ctypes.string_at(t.bytes, int(offs[-1])) if nn else b""
+        raw = np.ctypeslib.as_array(ctypes.cast(t.bytes, ctypes.POINTER(ctypes.c_uint8)), shape=(int(offs[-1]),)).tobytes() if nn and offs[-1] else b""
         return counts, offs, raw, int(t.tokens)
     finally:
         lib().moxo_free(ctypes.byref(t))

@@ -25,3 +25,35 @@ def kat_expected(case):
     if "error" in case:
         return "error"
     return [(bytes.fromhex(w), c) for w, c in case["expected"]]
+
+
+def canon_table(counts, offs, raw):
+    """(keys, counts) of a word table sorted bytewise, vectorised with numpy:
+    words become fixed-width 'S' strings (zero padded; words hold no NUL byte),
+    so big tables compare without building Python objects per word."""
+    import numpy as np
+    counts = np.asarray(counts, dtype=np.uint64)
+    offs = np.asarray(offs, dtype=np.int64)
+    n = counts.size
+    if n == 0:
+        return np.zeros(0, "S1"), counts
+    lens = np.diff(offs)
+    width = int(lens.max())
+    buf = np.frombuffer(raw, dtype=np.uint8)
+    assert not (buf == 0).any(), "canon_table needs NUL-free words"
+    cols = np.arange(width, dtype=np.int64)
+    idx = offs[:-1, None] + cols[None, :]
+    mat = np.where(cols[None, :] < lens[:, None], buf[np.minimum(idx, max(buf.size - 1, 0))], 0).astype(np.uint8)
+    keys = np.ascontiguousarray(mat).view("S%d" % width).ravel()
+    order = np.argsort(keys, kind="stable")
+    return keys[order], counts[order]
+
+
+def assert_tables_equal(a, b):
+    """a, b: (counts, offs, raw) word tables; equal as (word, count) multisets."""
+    import numpy as np
+    ka, ca = canon_table(*a)
+    kb, cb = canon_table(*b)
+    assert ka.size == kb.size, (ka.size, kb.size)
+    assert np.array_equal(ka, kb)
+    assert np.array_equal(ca, cb)

@@ -117,3 +117,20 @@ def test_host_exchange_gloo_processes(tmp_path):
     res = json.loads(out.read_text())
     data = mixed_corpus(4 << 20, 77)
     assert [(bytes.fromhex(w), c) for w, c in res] == coracle.count(data)[0]
+
+
+def test_host_exchange_high_cardinality():
+    """The reduce-only pass over received partials splits mostly-distinct
+    partitions too (weighted records only)."""
+    from conftest import assert_tables_equal
+    import numpy as np
+    data = corpus.fill(corpus.HICARD, 91, 0, 96 << 20).tobytes()
+    out = run_ranks(data, 2)
+    items = [w for part, _ in out for w in part]
+    counts = np.array([c for _, c in items], dtype=np.uint64)
+    words = [w for w, _ in items]
+    offs = np.zeros(len(words) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(w) for w in words])
+    wc, wo, wraw, wtok = coracle.count_arrays(np.frombuffer(data, np.uint8), nthreads=16)
+    assert sum(tok for _, tok in out) == wtok
+    assert_tables_equal((counts, offs, b"".join(words)), (wc, wo, wraw))

@@ -228,3 +228,46 @@ def test_full_size_c2(eng):
     words = [raw[offs[i]:offs[i + 1]] for i in range(counts.size)]
     order = sorted(range(counts.size), key=words.__getitem__)
     assert all(words[j] == wraw[wo[i]:wo[i + 1]] and counts[j] == wc[i] for i, j in enumerate(order))
+
+
+def _gpu_arrays(e, data):
+    t = e.count(data)
+    try:
+        counts, offs, raw = t.arrays()
+        assert int(counts.sum()) == t.tokens
+        return counts, offs, raw
+    finally:
+        t.close()
+
+
+def test_high_cardinality_split(eng):
+    """C4-like input (random 4-16 byte tokens): partitions are mostly distinct, so
+    the reduce splits them into sub-bucket units; exact vs oracle."""
+    from conftest import assert_tables_equal
+    data = corpus.fill(corpus.HICARD, 0x5EED0004, 0, 96 << 20)
+    got = _gpu_arrays(eng, data.tobytes())
+    st = eng.stats()
+    assert st["split_partitions"] > 0 and st["reduce_units"] > 1024, st
+    wc, wo, wraw, _ = coracle.count_arrays(data, nthreads=16)
+    assert_tables_equal(got, (wc, wo, wraw))
+
+
+def test_split_mixed_partitions(eng, eng_nodict):
+    """Zipf text and high-cardinality tokens in one corpus: split and whole
+    partitions side by side, with dictionary words and spills as weighted records."""
+    from conftest import assert_tables_equal
+    import numpy as np
+    z = corpus.fill(corpus.ZIPF, 77, 0, 40 << 20)
+    h = corpus.fill(corpus.HICARD, 78, 0, 88 << 20)
+    data = np.concatenate([z, np.frombuffer(b" \n", np.uint8), h])
+    want = coracle.count_arrays(data, nthreads=16)[:3]
+    for e in (eng, eng_nodict):
+        assert_tables_equal(_gpu_arrays(e, data.tobytes()), want)
+        assert e.stats()["split_partitions"] > 0
+
+
+def test_split_deterministic_order(eng):
+    data = corpus.fill(corpus.HICARD, 5, 0, 96 << 20).tobytes()
+    a = _gpu_arrays(eng, data)
+    b = _gpu_arrays(eng, data)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]

@@ -119,3 +119,20 @@ def test_meduce_ref_faithful_pipeline(tmp_path):
     bad.write_bytes(b"ok \xff no")
     r = subprocess.run([coracle.MEDUCE_REF, str(bad), "--workdir", str(tmp_path)], capture_output=True)
     assert r.returncode == 1
+
+
+def test_canon_table_matches_python_sort():
+    """The vectorised table comparison used by the big GPU parity tests."""
+    import numpy as np
+    from conftest import canon_table
+    from mox import corpus
+    data = corpus.fill(corpus.HICARD, 3, 0, 1 << 20)
+    counts, offs, raw, _ = coracle.count_arrays(data)
+    perm = np.random.default_rng(0).permutation(counts.size)
+    words = [raw[offs[i]:offs[i + 1]] for i in perm]
+    poffs = np.zeros(len(words) + 1, dtype=np.int64)
+    poffs[1:] = np.cumsum([len(w) for w in words])
+    keys, cs = canon_table(counts[perm], poffs, b"".join(words))
+    want = sorted(zip(words, counts[perm].tolist()))
+    assert [k for k in keys.tolist()] == [w for w, _ in want]
+    assert cs.tolist() == [c for _, c in want]

@@ -9,7 +9,7 @@ for grp in "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAVE_CYCLES,SQ_
            "SQ_LDS_IDX_ACTIVE,SQ_LDS_ADDR_CONFLICT,SQ_LDS_UNALIGNED_STALL,SQ_INSTS_BRANCH,SQ_ACTIVE_INST_SCA,SQ_INSTS_SMEM,SQ_IFETCH,SQ_ACTIVE_INST_MISC" \
            "GRBM_GUI_ACTIVE,GRBM_COUNT"; do
   i=$((i+1))
-  timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-include-regex "$K" --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $OUT/p$i.log 2>&1
+  timeout -s KILL 90 rocprofv3 --pmc $grp --kernel-include-regex "$K" --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit $rc; }
   python3 - "$OUT/p$i" <<'PY'
 import csv, glob, sys, collections
