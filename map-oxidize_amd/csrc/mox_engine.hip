@@ -30,6 +30,7 @@ using namespace mox;
 
 extern "C" {
 __global__ void k_map(Corpus c, Work w, uint64_t ntiles);
+__global__ void k_init(Work w, unsigned long long w_n, uint32_t flags);
 __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
 __global__ void k_dict_hist(Work w);
 __global__ void k_dict_pick(Work w, uint32_t max_words);
@@ -45,16 +46,8 @@ __global__ void k_unit_scan(Work w);
 __global__ void k_split_scatter(Work w);
 __global__ void k_unit_uniq_scan(Work w);
 __global__ void k_reduce_small(Work w);
-__global__ void k_scan_reduce(const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
-                              uint64_t* part);
-__global__ void k_scan_parts(uint64_t* part, int nparts);
-__global__ void k_scan_apply(const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
-                             const uint64_t* part, uint64_t* out);
-__global__ void k_long_flags(Work w, uint64_t* flags);
 __global__ void k_final_scan(Work w);
-__global__ void k_mat_counts(Work w, uint64_t* lens);
-__global__ void k_mat_long(Work w, uint64_t* lens);
-__global__ void k_mat_bytes(Work w, Corpus c);
+__global__ void k_mat(Work w, Corpus c);
 __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
 __global__ void k_xpack_short(Work w, WRec* out);
 __global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob);
@@ -111,8 +104,6 @@ struct mox_engine {
   Tables tables{};
   Ctl* h_ctl = nullptr;       // pinned
   Ctl* h_ctl_init = nullptr;  // pinned
-  uint64_t* d_lens = nullptr; // table_cap + 1 scratch (lengths / long flags)
-  uint64_t lens_cap = 0;
   // engine-owned corpus staging for host inputs
   uint8_t* d_text = nullptr;
   size_t d_text_cap = 0;
@@ -182,8 +173,6 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   FREE_FIELD(w); FREE_FIELD(w_sorted); FREE_FIELD(u); FREE_FIELD(arena); FREE_FIELD(ltab); FREE_FIELD(lpos);
   FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
   FREE_FIELD(split_k); FREE_FIELD(split_w);
-  dfree(e->d_lens);
-  e->d_lens = nullptr;
   Work& w = e->w;
   w.cold_cap = (uint32_t)std::min<uint64_t>(c.cold_cap, 0xFFFFFFF0u);
   w.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
@@ -212,8 +201,6 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   if ((rc = dalloc(e, (void**)&w.t_bytes, w.bytes_cap))) return rc;
   if ((rc = dalloc(e, (void**)&w.split_k, w.split_k_cap * 16))) return rc;
   if ((rc = dalloc(e, (void**)&w.split_w, w.split_w_cap * sizeof(WRec)))) return rc;
-  e->lens_cap = std::max<uint64_t>(w.table_cap, w.long_cap) + 1;
-  if ((rc = dalloc(e, (void**)&e->d_lens, e->lens_cap * 8))) return rc;
   return MOX_OK;
 }
 
@@ -241,7 +228,7 @@ int alloc_fixed(mox_engine* e) {
   int rc;
   if ((rc = dalloc(e, (void**)&w.ctl, sizeof(Ctl)))) return rc;
   if ((rc = dalloc(e, (void**)&w.cand, (size_t)GC_SLOTS * sizeof(WRec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dict_hist, 257 * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.dict_hist, 260 * 4))) return rc;  // 257 used, zeroed as 260 (k_init)
   if ((rc = dalloc(e, (void**)&w.dict_list, (size_t)DICT_MAX_WORDS * sizeof(WRec)))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_tag, DICT_SLOTS * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_key, DICT_SLOTS * 16))) return rc;
@@ -260,7 +247,6 @@ int alloc_fixed(mox_engine* e) {
   w.rec_off = (uint64_t*)d; d += (NB + 1) * 8;
   w.b_uniq = (uint64_t*)d; d += NB * 8;
   w.uniq_off = (uint64_t*)d; d += (NB + 1) * 8;
-  if ((rc = dalloc(e, (void**)&w.scan_part, (SCAN_WGS + 1) * 8))) return rc;
   // reduce units (high-cardinality split)
   if ((rc = dalloc(e, (void**)&w.b_kk, NB * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.u_base, (NB + 1) * 4))) return rc;
@@ -269,6 +255,18 @@ int alloc_fixed(mox_engine* e) {
   if ((rc = dalloc(e, (void**)&w.spw_off, (NB + 1) * 8))) return rc;
   if ((rc = dalloc(e, (void**)&w.udesc, (size_t)U_MAX * sizeof(UnitDesc)))) return rc;
   if ((rc = dalloc(e, (void**)&w.big_units, (size_t)U_MAX * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.u_bytes, (size_t)U_MAX * 8))) return rc;
+  if ((rc = dalloc(e, (void**)&w.u_bytes_off, (size_t)U_MAX * 8))) return rc;
+  {
+    uint64_t* t2;
+    if ((rc = dalloc(e, (void**)&t2, 6 * (NB + 1) * 8))) return rc;
+    w.b_bytes = t2; t2 += NB + 1;
+    w.bytes_off = t2; t2 += NB + 1;
+    w.ls_n = t2; t2 += NB + 1;
+    w.ls_b = t2; t2 += NB + 1;
+    w.ls_off = t2; t2 += NB + 1;
+    w.ls_boff = t2;
+  }
   if ((rc = dalloc(e, (void**)&w.u_uniq, (size_t)U_MAX * 8))) return rc;
   if ((rc = dalloc(e, (void**)&w.u_uniq_off, (size_t)U_MAX * 8))) return rc;
   // Unicode tables
@@ -296,17 +294,6 @@ int alloc_fixed(mox_engine* e) {
 
 size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
 size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
-
-// exclusive scan of v[0, n) into out[0, n], n = min(*n_ptr or n_const, n_cap)
-int launch_scan(mox_engine* e, const uint64_t* v, const unsigned long long* n_ptr, uint64_t n_const, uint64_t n_cap,
-                uint64_t* out) {
-  hipLaunchKernelGGL(k_scan_reduce, dim3(SCAN_WGS), dim3(SCAN_THREADS), 0, e->stream, v, n_ptr, n_const, n_cap,
-                     e->w.scan_part);
-  hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_WGS), 0, e->stream, e->w.scan_part, SCAN_WGS);
-  hipLaunchKernelGGL(k_scan_apply, dim3(SCAN_WGS), dim3(SCAN_THREADS), 0, e->stream, v, n_ptr, n_const, n_cap,
-                     (const uint64_t*)e->w.scan_part, out);
-  return MOX_OK;
-}
 
 float ev_ms(mox_engine* e, int a, int b) {
   float ms = 0;
@@ -344,13 +331,13 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_bucket_scan");
   hipLaunchKernelGGL(k_scatter, dim3(w.map_grid), dim3(1024), 0, s, w);
   q.step("k_scatter");
-  hipLaunchKernelGGL(k_split_count, dim3(NB), dim3(1024), 0, s, w);
+  hipLaunchKernelGGL(k_split_count, dim3(NB), dim3(256), 0, s, w);  // SC_THREADS
   q.step("k_split_count");
   hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(NB), 0, s, w);
   q.step("k_unit_scan");
   hipLaunchKernelGGL(k_split_scatter, dim3(NB), dim3(1024), 0, s, w);
   q.step("k_split_scatter");
-  hipLaunchKernelGGL(k_reduce, dim3(2 * e->n_cu), dim3(RED_THREADS), reduce_lds_bytes(), s, w);  // persistent, 2 per CU
+  hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);  // workgroup b: partition b, then the work list
   q.step("k_reduce");
   hipLaunchKernelGGL(k_reduce_small, dim3(4 * e->n_cu), dim3(256), 0, s, w);  // persistent, 4 per CU
   q.step("k_reduce_small");
@@ -359,18 +346,8 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_unit_uniq_scan");
   hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(NB), 0, s, w);
   q.step("k_final_scan");
-  hipLaunchKernelGGL(k_long_flags, dim3(256), dim3(256), 0, s, w, e->d_lens);
-  q.step("k_long_flags");
-  launch_scan(e, e->d_lens, nullptr, w.long_cap, w.long_cap, w.lpos);
-  q.step("scan_long");
-  hipLaunchKernelGGL(k_mat_counts, dim3(1024), dim3(256), 0, s, w, e->d_lens);
-  q.step("k_mat_counts");
-  hipLaunchKernelGGL(k_mat_long, dim3(256), dim3(256), 0, s, w, e->d_lens);
-  q.step("k_mat_long");
-  launch_scan(e, e->d_lens, &w.ctl->n_total, 0, w.table_cap, w.t_offs);
-  q.step("scan_offs");
-  hipLaunchKernelGGL(k_mat_bytes, dim3(1024), dim3(256), 0, s, w, c);
-  q.step("k_mat_bytes");
+  hipLaunchKernelGGL(k_mat, dim3(1024), dim3(256), 0, s, w, c);  // grid >= NB long-table slices
+  q.step("k_mat");
   q.rec(5);
 }
 
@@ -397,14 +374,12 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   hipStream_t s = e->stream;
   const Seq q = seq_of(e);
   q.rec(0);
-  HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_init, sizeof(Ctl), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
-  HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
+  const bool dict = !(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo;
+  // control block, partition counters, long table, sampling buffers: one launch
+  hipLaunchKernelGGL(k_init, dim3(256), dim3(256), 0, s, w, 0ull, dict ? 1u : 0u);
+  q.step("k_init");
   // 1. hot dictionary from a sample
-  if (!(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo) {
-    HIPCHK(hipMemsetAsync(w.dict_tot, 0, DICT_SLOTS * 8, s));
-    HIPCHK(hipMemsetAsync(w.cand, 0, (size_t)GC_SLOTS * sizeof(WRec), s));
-    HIPCHK(hipMemsetAsync(w.dict_hist, 0, 257 * 4, s));
+  if (dict) {
     hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(256), 0, s, c, w, e->sample_pieces);
     q.step("k_sample");
     hipLaunchKernelGGL(k_dict_hist, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w);
@@ -694,13 +669,8 @@ int exchange_pass_once(mox_engine* e, uint64_t r_short, uint64_t blob_bytes, con
   hipStream_t s = e->stream;
   const Seq q = seq_of(e);
   q.rec(0);
-  *e->h_ctl_x = *e->h_ctl_init;
-  e->h_ctl_x->w_n = r_short;
-  HIPCHK(hipMemcpyAsync(w.ctl, e->h_ctl_x, sizeof(Ctl), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemsetAsync(w.b_recs, 0, NB * 8 + NB * 4, s));
-  HIPCHK(hipMemsetAsync(w.ltab, 0, w.long_cap * sizeof(LSlot), s));
-  HIPCHK(hipMemsetAsync(w.cold_n, 0, (size_t)w.map_grid * NB * 4, s));
-  HIPCHK(hipMemsetAsync(w.spill_n, 0, (size_t)w.map_grid * 4, s));
+  // control block (w_n = received records), counters, long table, no map regions
+  hipLaunchKernelGGL(k_init, dim3(256), dim3(256), 0, s, w, (unsigned long long)r_short, 2u);
   if (r_short) HIPCHK(hipMemcpyAsync(w.w, e->x_recv_short.p, r_short * sizeof(WRec), hipMemcpyDeviceToDevice, s));
   if (blob_bytes) HIPCHK(hipMemcpyAsync(w.arena, e->x_recv_blob.p, blob_bytes, hipMemcpyDeviceToDevice, s));
   q.rec(1);
@@ -881,9 +851,11 @@ void mox_engine_destroy(mox_engine* e) {
   (void)hipDeviceSynchronize();
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
-  void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, w.scan_part, (void*)e->tables.lower_src,
+  void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
-                  w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_lens, e->d_text};
+                  w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_text,
+                  w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.u_uniq, w.u_uniq_off,
+                  w.u_bytes, w.u_bytes_off, w.b_bytes, w.split_k, w.split_w};
   for (void* p : ptrs) dfree(p);
   for (DevBuf* b : {&e->x_send_short, &e->x_send_blob, &e->x_recv_short, &e->x_recv_blob}) dfree(b->p);
   for (DevBuf* b : {&e->hx_send, &e->hx_recv}) if (b->p) (void)hipHostFree(b->p);

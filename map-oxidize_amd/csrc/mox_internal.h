@@ -41,11 +41,9 @@ constexpr int U_MAX = NB * SUB_N;           // reduce units
 constexpr uint32_t SPLIT_MIN = 6144;        // records below which a partition is never split
 constexpr uint32_t SPLIT_TARGET = 640;      // records per sub-bucket aimed at
 constexpr uint32_t SMALL_CAP = 1024;        // sub-buckets up to this many records: k_reduce_small
-constexpr uint32_t SPLIT_SAMPLE = 4096;     // records sampled for the distinct-fraction estimate
-constexpr uint32_t SPLIT_PER_REGION = 16;   // ... the first 16 of every map workgroup's region
-constexpr int LC_BITS = 16384;              // linear-counting bitmap of the sample
-constexpr int SCAN_THREADS = 1024;
-constexpr int SCAN_WGS = 1024;
+constexpr uint32_t SPLIT_SAMPLE = 1024;     // records sampled for the distinct-fraction estimate
+constexpr uint32_t SPLIT_PER_REGION = 4;    // ... the first 4 of every map workgroup's region
+constexpr int LC_BITS = 4096;               // linear-counting bitmap of the sample (4 bits per sample)
 
 constexpr uint64_t LONG_TAG = 0xFF00000000000000ull;   // w1 marker of a hashed (long) key
 constexpr uint64_t LONG_LEN_MASK = 0x0000FFFFFFFFFFFFull;
@@ -98,6 +96,7 @@ struct Ctl {
   unsigned int n_split;           // partitions split
   unsigned int pad2;
   unsigned long long n_big;       // entries of big_units (k_reduce work list)
+  unsigned long long short_bytes; // table bytes of the short words (long words follow)
 };
 
 // Weighted record: a key with a count (dictionary totals, spills, Unicode-lane
@@ -222,7 +221,16 @@ struct Work {  // device buffers of one engine
   UnitDesc* udesc;                // U_MAX: input ranges + output region of unit u
   uint32_t* big_units;            // U_MAX: units for k_reduce (whole partitions + oversized sub-buckets)
   uint64_t* u_uniq;               // U_MAX: distinct keys of unit u
-  uint64_t* u_uniq_off;           // U_MAX: dense table index of unit u's first key
+  uint64_t* u_bytes;              // U_MAX: key bytes of unit u's distinct keys
+  uint64_t* u_bytes_off;          // U_MAX: byte offset of unit u inside its partition
+  // table directory (k_unit_uniq_scan -> k_final_scan -> k_mat)
+  uint64_t* b_bytes;              // NB: key bytes of partition b
+  uint64_t* bytes_off;            // NB + 1: byte offset of partition b's first key
+  uint64_t* ls_n;                 // NB: occupied long-table slots of slice b
+  uint64_t* ls_b;                 // NB: bytes of slice b's long words
+  uint64_t* ls_off;               // NB + 1: table index (after the short words) of slice b's first long word
+  uint64_t* ls_boff;              // NB + 1: byte offset (after the short words' bytes) of slice b
+  uint64_t* u_uniq_off;           // U_MAX: table index of unit u's first key inside its partition
   uint4* split_k;                 // split_k_cap cold keys grouped by unit
   WRec* split_w;                  // split_w_cap weighted records grouped by unit
   uint64_t split_k_cap, split_w_cap;
@@ -238,7 +246,6 @@ struct Work {  // device buffers of one engine
   uint8_t* t_bytes;               // bytes_cap
   uint64_t table_cap, bytes_cap;
   // scan scratch
-  uint64_t* scan_part;            // SCAN_WGS + 1
   uint32_t dbg;                   // ablation switches (MOX_DBG env), 0 in production
   unsigned long long* stamps;     // DBG_STAMP: per-workgroup phase timestamps (8 per workgroup)
 };

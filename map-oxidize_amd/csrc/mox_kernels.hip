@@ -199,6 +199,12 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   return hash32((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
 }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - NB_LOG2); }
+// byte length of a short key (lowered word, zero padded to 16 bytes, no NUL inside)
+__device__ __forceinline__ uint32_t key_len16(uint4 k) {
+  const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
+  if (w1) return 16 - (__clzll(w1) >> 3);
+  return 8 - (__clzll(w0) >> 3);
+}
 // Dictionary: DICT_SLOTS slots in groups of 4.  A word sits in its home slot
 // (h mod DICT_SLOTS) when that was free at build time (words are placed
 // hottest first), else in a free slot of its home group, else of its second
@@ -772,6 +778,45 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   if (lane == 0 && ntok) atomicAdd(&w.ctl->tokens, ntok);
 }
 
+// ------------------------------------------------------------------ pass init
+// One launch instead of a control-block copy and five memsets: the control
+// block (zero, no UTF-8 / halo error, w_n), the partition counters, the long
+// table, and (INIT_DICT) the dictionary sampling buffers or (INIT_MAP) the map
+// region counters of an exchange pass.
+enum : uint32_t { INIT_DICT = 1u, INIT_MAP = 2u };
+__device__ __forceinline__ void zero_words(void* p, uint64_t bytes, uint64_t t, uint64_t stride) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+  const uint64_t n16 = bytes / 16;
+  for (uint64_t i = t; i < n16; i += stride) q[i] = make_uint4(0, 0, 0, 0);
+  uint32_t* r = reinterpret_cast<uint32_t*>(q + n16);
+  for (uint64_t i = t; i < (bytes % 16) / 4; i += stride) r[i] = 0;
+}
+extern "C" __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  constexpr int CW = sizeof(Ctl) / 8;
+  static_assert(sizeof(Ctl) % 8 == 0, "Ctl is zeroed in 8-byte words");
+  if (t < CW) {
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(w.ctl);
+    const uint64_t off = t * 8;
+    unsigned long long v = 0;
+    if (off == offsetof(Ctl, err_utf8) || off == offsetof(Ctl, halo_err)) v = ~0ull;
+    if (off == offsetof(Ctl, w_n)) v = w_n;
+    c[t] = v;
+  }
+  zero_words(w.b_recs, NB * 8, t, stride);
+  zero_words(w.b_w, NB * 4, t, stride);
+  zero_words(w.ltab, w.long_cap * sizeof(LSlot), t, stride);
+  if (flags & INIT_DICT) {
+    zero_words(w.dict_tot, DICT_SLOTS * 8, t, stride);
+    zero_words(w.cand, (uint64_t)GC_SLOTS * sizeof(WRec), t, stride);
+    zero_words(w.dict_hist, 260 * 4, t, stride);
+  }
+  if (flags & INIT_MAP) {
+    zero_words(w.cold_n, (uint64_t)w.map_grid * NB * 4, t, stride);
+    zero_words(w.spill_n, (uint64_t)w.map_grid * 4, t, stride);
+  }
+}
+
 // ------------------------------------------------------------------ dictionary
 // Two-CAS claim of a 16-byte key in a global or LDS table (w1 is stored with the
 // top bit set so that 0 always means "unclaimed"); used only for heuristics.
@@ -864,7 +909,7 @@ extern "C" __global__ __launch_bounds__(256) void k_sample(Corpus c, Work w, uin
     if (n == 0 || sk0[i] == 0 || sk1[i] == 0) continue;
     const uint64_t w0 = sk0[i], w1 = sk1[i] & ~(1ull << 63);
     uint32_t g = key_hash(w0, w1) & (GC_SLOTS - 1);
-    for (int pr = 0; pr < 256; pr++) {
+    for (int pr = 0; pr < 16; pr++) {  // bounded: a full table (high-cardinality input) just drops words
       WRec* r = &w.cand[g];
       if (claim16((unsigned long long*)&r->w0, (unsigned long long*)&r->w1, w0, w1)) {
         atomicAdd((unsigned long long*)&r->count, (unsigned long long)n);
@@ -891,16 +936,25 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
   __shared__ uint32_t T, h[256];
   if (threadIdx.x < 256) h[threadIdx.x] = w.dict_hist[threadIdx.x];
   __syncthreads();
-  if (threadIdx.x == 0) {
-    uint32_t acc = 0, t = 2;
-    for (int cc = 255; cc >= 2; cc--) {
-      if (acc + h[cc] > max_words) { t = cc + 1; break; }
-      acc += h[cc];
+  // T = smallest count class cc >= 2 whose suffix sum S(cc) = sum_{c >= cc} h[c]
+  // fits max_words (S is non-increasing in cc, so the fitting classes are a
+  // suffix); S from an exclusive scan over the reversed histogram
+  {
+    __shared__ uint64_t wsum[16];
+    uint64_t tot;
+    const int cc = 255 - (int)threadIdx.x;
+    const uint64_t x = threadIdx.x < 256 ? h[cc] : 0;
+    const uint64_t ex = block_exscan(x, wsum, tot);
+    if (threadIdx.x == 0) T = 256;
+    __syncthreads();
+    if (threadIdx.x < 254 && ex + x <= max_words) atomicMin(&T, (uint32_t)cc);  // cc in [2, 255]
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (T > 255) T = 256;  // nothing fits: pick nothing
+      if (blockIdx.x == 0) w.ctl->dict_thresh = T;
     }
-    T = t;
-    if (blockIdx.x == 0) w.ctl->dict_thresh = t;
+    __syncthreads();
   }
-  __syncthreads();
   // one slot per thread (grid = GC_SLOTS / 1024): rank picked entries in the
   // workgroup, reserve the workgroup's range with one global atomic
   __shared__ uint32_t wn[16], base;
@@ -924,25 +978,41 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
   __shared__ uint32_t ltag[DICT_SLOTS];
   __shared__ uint2 lk0[DICT_MAX_WORDS], lk1[DICT_MAX_WORDS];  // picked keys, staged once
   __shared__ uint8_t lcl[DICT_MAX_WORDS];                     // log2 count class
+  __shared__ uint16_t order[DICT_MAX_WORDS];                  // words grouped by class, hottest first
+  __shared__ uint32_t ccnt[32], cstart[33], cfill[32];
   __shared__ uint32_t nsel;
   const int tid = threadIdx.x;
   for (int i = tid; i < DICT_SLOTS; i += 1024) { ltag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
+  if (tid < 32) { ccnt[tid] = 0; cfill[tid] = 0; }
   if (tid == 0) nsel = 0;
   uint32_t n = w.dict_hist[256];
   if (n > max_words) n = max_words;
+  __syncthreads();
   for (uint32_t i = tid; i < n; i += 1024) {
     const WRec r = w.dict_list[i];
     const uint32_t cnt = r.count > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)r.count;
     lk0[i] = make_uint2((uint32_t)r.w0, (uint32_t)(r.w0 >> 32));
     lk1[i] = make_uint2((uint32_t)r.w1, (uint32_t)(r.w1 >> 32));
-    lcl[i] = (uint8_t)(31 - __clz(cnt));
+    lcl[i] = (uint8_t)(31 - __clz(cnt | 1u));
+    atomicAdd(&ccnt[lcl[i]], 1u);
   }
   __syncthreads();
+  if (tid == 0) {  // class starts, hottest class first
+    uint32_t a = 0;
+    for (int cl = 31; cl >= 0; cl--) { cstart[cl] = a; a += ccnt[cl]; }
+    cstart[32] = a;
+  }
+  __syncthreads();
+  for (uint32_t i = tid; i < n; i += 1024) order[cstart[lcl[i]] + atomicAdd(&cfill[lcl[i]], 1u)] = (uint16_t)i;
+  __syncthreads();
   // insert by descending log2 count class, so that a word dropped because both
-  // of its groups are full is never hotter than the words that filled them
+  // of its groups are full is never hotter than the words that filled them;
+  // one barrier per non-empty class
   for (int cl = 31; cl >= 0; cl--) {
-    for (uint32_t i = tid; i < n; i += 1024) {
-      if (lcl[i] != cl) continue;
+    const uint32_t c0 = cstart[cl], c1 = c0 + ccnt[cl];
+    if (c0 == c1) continue;  // uniform
+    for (uint32_t j = c0 + tid; j < c1; j += 1024) {
+      const uint32_t i = order[j];
       const uint2 a = lk0[i], b = lk1[i];
       const uint32_t h = hash32(a.x, a.y, b.x, b.y);
       if (h == 0) continue;  // tag 0 marks an empty slot
@@ -1322,10 +1392,11 @@ __device__ __forceinline__ void for_partition_cold(const Work& w, uint32_t b, F 
 // sub-bucket bits and a full histogram of its records per sub-bucket.
 // Partitions with few distinct keys stay whole (their reduce resolves them in
 // one table, or in a few in-kernel sub-passes).
-extern "C" __global__ __launch_bounds__(1024) void k_split_count(Work w) {
+constexpr int SC_THREADS = 256;  // 8 workgroups per CU: every partition's decision in one round
+extern "C" __global__ __launch_bounds__(SC_THREADS) void k_split_count(Work w) {
   __shared__ uint32_t bm[LC_BITS / 32];
   __shared__ uint32_t hc[SUB_N], hw[SUB_N];
-  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t wsum[SC_THREADS / 64];
   __shared__ uint32_t s_ones, s_kk;
   const uint32_t b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -1340,19 +1411,19 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_count(Work w) {
   // up with weighted records
   const uint32_t G = w.map_grid;
   auto mark = [&](uint32_t h) {
-    const uint32_t bit = hbits(h, NB_LOG2, 14);
+    const uint32_t bit = hbits(h, NB_LOG2, 12);  // LC_BITS = 2^12
     atomicOr(&bm[bit >> 5], 1u << (bit & 31));
   };
   uint32_t mine = 0;
   {
-    constexpr int PER = SPLIT_SAMPLE / 1024;  // sample slots per thread
+    constexpr int PER = (SPLIT_SAMPLE + SC_THREADS - 1) / SC_THREADS;  // sample slots per thread
     uint4 v[PER];
     bool ok[PER];
 #pragma unroll
     for (int j = 0; j < PER; j++) {
-      const uint32_t idx = tid + j * 1024;
+      const uint32_t idx = tid + j * SC_THREADS;
       const uint32_t g = idx / SPLIT_PER_REGION, i = idx % SPLIT_PER_REGION;
-      ok[j] = g < G && i < w.cold_n[(uint64_t)g * NB + b];
+      ok[j] = idx < SPLIT_SAMPLE && g < G && i < w.cold_n[(uint64_t)g * NB + b];
       v[j] = ok[j] ? w.cold[((uint64_t)g * NB + b) * w.cold_cap + i] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
@@ -1406,7 +1477,7 @@ extern "C" __global__ __launch_bounds__(NB) void k_unit_scan(Work w) {
   const uint64_t ub = block_exscan(1ull << kk, wsum, U);
   const uint64_t ok = block_exscan(kk ? w.b_recs[b] : 0, wsum, tk);
   const uint64_t ow = block_exscan(kk ? w.b_w[b] : 0, wsum, tw);
-  const uint64_t wi = block_exscan(kk ? 0 : 1, wsum, nwhole);
+  (void)block_exscan(kk ? 0 : 1, wsum, nwhole);
   ns = NB - nwhole;
   w.u_base[b] = (uint32_t)ub;
   w.b_uniq[b] = 0;  // k_reduce*: set (whole partition) or accumulated (split)
@@ -1414,14 +1485,13 @@ extern "C" __global__ __launch_bounds__(NB) void k_unit_scan(Work w) {
   w.spw_off[b] = ow;
   if (!kk) {
     w.udesc[ub] = UnitDesc{0, 0, w.rec_off[b], UNIT_WHOLE, 0, b, 0};
-    w.big_units[wi] = (uint32_t)ub;
   }
   if (b == 0) {
     w.u_base[NB] = (uint32_t)U;
     w.sp_off[NB] = tk;
     w.spw_off[NB] = tw;
     w.ctl->n_units = U;
-    w.ctl->n_big = nwhole;  // k_split_scatter appends oversized sub-buckets
+    w.ctl->n_big = 0;  // k_split_scatter lists oversized sub-buckets (whole partitions: k_reduce workgroup b)
     w.ctl->red_ticket = 0;
     w.ctl->split_k = tk;
     w.ctl->split_w = tw;
@@ -1500,16 +1570,25 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   // an overflowed map, directory or split means this attempt is rerun with
   // larger buffers: its records are incomplete (nothing downstream reads them)
   if (w.ctl->overflow & OVF_RERUN) return;
+  // workgroup b < NB first reduces partition b if it was not split (no queue),
+  // then all workgroups take oversized sub-buckets from the work list
   const uint32_t NBIG = (uint32_t)w.ctl->n_big;
   uint32_t max_kk = 0;
+  bool own = blockIdx.x < NB && w.b_kk[blockIdx.x] == 0;
   for (;;) {
-    if (tid == 0) {
-      const uint32_t t = (uint32_t)atomicAdd(&w.ctl->red_ticket, 1ull);
-      s_unit = t < NBIG ? w.big_units[t] : 0xFFFFFFFFu;
+    uint32_t u;
+    if (own) {
+      u = w.u_base[blockIdx.x];
+      own = false;
+    } else {
+      if (tid == 0) {
+        const uint32_t t = (uint32_t)atomicAdd(&w.ctl->red_ticket, 1ull);
+        s_unit = t < NBIG ? w.big_units[t] : 0xFFFFFFFFu;
+      }
+      __syncthreads();
+      u = s_unit;
+      __syncthreads();
     }
-    __syncthreads();
-    const uint32_t u = s_unit;
-    __syncthreads();
     if (u == 0xFFFFFFFFu) break;
     const UnitDesc ud = w.udesc[u];
     const uint32_t b = ud.part;
@@ -1527,11 +1606,11 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     const bool stamp = MOX_ABL(w.dbg, DBG_STAMP) && tid == 0 && !split;
     if (stamp) w.stamps[b * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     uint32_t kk = 0;
-    uint64_t written = 0;
+    uint64_t written = 0, wbytes = 0;
     bool failed = false;
     for (uint32_t sub = 0; sub < (1u << kk);) {
       for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
-      if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; }
+      if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
       __syncthreads();
       // cold records: wave wv streams its regions (whole partition: regions
       // g = wv, wv + NWV, ...; split unit: one chunk) 64 x RED_UNROLL records at
@@ -1614,6 +1693,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         }
         sub = 0;
         written = 0;
+        wbytes = 0;
         continue;
       }
       // deterministic order (h32, key): bucket sort by the hash bits below the
@@ -1660,14 +1740,19 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       }
       __syncthreads();
       if (stamp) w.stamps[b * 8 + 3] = __builtin_amdgcn_s_memrealtime();  // sorted
+      uint32_t lb = 0;
       for (uint32_t i = tid; i < nu; i += RED_THREADS) {
         const uint16_t sl = s.idx[i];
-        w.uk[out0 + written + i] = s.key[sl];
+        const uint4 kk4 = s.key[sl];
+        w.uk[out0 + written + i] = kk4;
         w.uc[out0 + written + i] = s.cnt[sl];
+        lb += key_len16(kk4);
       }
+      if (lb) atomicAdd(&s.misc[3], lb);
       written += nu;
       sub++;
       __syncthreads();
+      if (tid == 0) wbytes += s.misc[3];  // read (and reset at the next sub-pass) by tid 0 only
     }
     if (stamp) {
       w.stamps[b * 8 + 4] = __builtin_amdgcn_s_memrealtime();
@@ -1678,6 +1763,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     }
     if (tid == 0) {
       w.u_uniq[u] = failed ? 0 : written;
+      w.u_bytes[u] = failed ? 0 : wbytes;
       if (!split) w.b_uniq[b] = failed ? 0 : written;  // split partitions: summed by k_unit_uniq_scan
     }
     if (kk > max_kk) max_kk = kk;
@@ -1717,18 +1803,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
-struct SmallIn {
+struct SmallIn {  // prefetched keys (weighted counts are read at use: rare outside exchange passes)
   uint4 k[SR_PER];
-  unsigned long long c[SR_PER];
 };
 __device__ __forceinline__ bool small_unit(const UnitDesc& d) { return d.in_n != UNIT_WHOLE && d.in_n + d.win_n <= SMALL_CAP; }
 // Descriptor of unit min(u, U - 1): no select on the loaded value, so the load
 // stays in flight until first use (the caller checks u < U there).
 __device__ __forceinline__ UnitDesc load_desc(const Work& w, uint32_t u, uint32_t U) { return w.udesc[u < U ? u : U - 1]; }
-// Branch-free raw loads (one address select per slot, invalid slots read a
-// valid dummy address, no select on loaded values): the compiler leaves them
-// in flight until the next iteration uses them.  c[j] is meaningful only for
-// weighted slots (i >= in_n).
+// Branch-free raw key loads (one address select per slot, invalid slots read
+// a valid dummy address, no select on loaded values): the compiler leaves them
+// in flight until the next iteration uses them.
 __device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, bool ok, SmallIn& in) {
   const uint32_t nk = d.in_n, n = d.in_n + d.win_n;
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -1739,10 +1823,8 @@ __device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, boo
     const uint8_t* kp = cold ? reinterpret_cast<const uint8_t*>(w.split_k + d.in_off + i)
                              : reinterpret_cast<const uint8_t*>(w.split_w + d.win_off + (i - nk));
     if (!valid) kp = reinterpret_cast<const uint8_t*>(w.split_k);
-    const uint8_t* cp = (valid && !cold) ? kp + 16 : kp;
     const u32x4 v = *reinterpret_cast<const u32x4*>(kp);
     in.k[j] = make_uint4(v.x, v.y, v.z, v.w);
-    in.c[j] = *reinterpret_cast<const unsigned long long*>(cp);
   }
 }
 
@@ -1754,14 +1836,16 @@ __device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, boo
 // (~0.5 records per bin), (h32, key) insertion sort inside bins so equal keys
 // are adjacent, run heads compacted by a scan, each head sums its run.  Output
 // order (h32, key), as k_reduce.
-extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) {
+extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work w) {  // 4 per CU: <= 128 VGPRs
   __shared__ uint4 key[SMALL_CAP];
   __shared__ unsigned long long cnt[SMALL_CAP];
   __shared__ uint32_t hh[SMALL_CAP];
   __shared__ uint16_t rk[SMALL_CAP];
-  __shared__ uint16_t idx[SMALL_CAP];
+  __shared__ uint16_t idx[SMALL_CAP];     // records grouped by bin
+  __shared__ uint16_t idx2[SMALL_CAP];    // records in (h32, key) order
   __shared__ uint32_t bins[SR_BINS / 2];  // u16 pairs: counts, then exclusive starts
   __shared__ uint32_t wsa[SR_THREADS / 64], wsb[SR_THREADS / 64];
+  __shared__ uint32_t sbytes;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (w.ctl->overflow & OVF_RERUN) return;
   const uint32_t U = (uint32_t)w.ctl->n_units;
@@ -1770,7 +1854,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) 
   __shared__ UnitDesc dring[2];  // descriptors of this and the next unit (written one unit ahead)
   uint32_t u = blockIdx.x;
   if (u >= U) return;
-  if (tid == 0) { dring[0] = load_desc(w, u, U); dring[1] = load_desc(w, u + G, U); }
+  if (tid == 0) { dring[0] = load_desc(w, u, U); dring[1] = load_desc(w, u + G, U); sbytes = 0; }
   bins[tid] = 0;
   bins[tid + SR_THREADS] = 0;
   lds_barrier();
@@ -1779,6 +1863,12 @@ extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) 
     const UnitDesc d0 = dring[0];
     load_small(w, d0, small_unit(d0), in);
   }
+#ifdef MOX_SR_STATS
+  uint64_t cyc[4] = {0, 0, 0, 0}, tprev = __builtin_amdgcn_s_memtime();
+#define SR_MARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); cyc[k] += t_ - tprev; tprev = t_; } while (0)
+#else
+#define SR_MARK(k) do { } while (0)
+#endif
   for (uint32_t it = 0; u < U; u += G, it++) {
     const UnitDesc d = dring[it & 1], dn = dring[(it + 1) & 1];
     const bool cur_small = small_unit(d);
@@ -1792,7 +1882,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) 
           const uint32_t h = hash32(in.k[j].x, in.k[j].y, in.k[j].z, in.k[j].w);
           const uint32_t bn = hbits(h, shift, 10);
           key[i] = in.k[j];
-          cnt[i] = i < d.in_n ? 1ull : in.c[j];
+          cnt[i] = i < d.in_n ? 1ull : w.split_w[d.win_off + (i - d.in_n)].count;
           hh[i] = h;
           const uint32_t old = atomicAdd(&bins[bn >> 1], 1u << (16 * (bn & 1)));
           rk[i] = (uint16_t)((old >> (16 * (bn & 1))) & 0xFFFFu);
@@ -1806,6 +1896,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) 
     if (tid == 0) dnn = load_desc(w, u + 2 * G, U);
     if (cur_small) {
       lds_barrier();
+      SR_MARK(0);
       {  // exclusive scan of the bin counts: bins 4t..4t+3 per thread
         const uint32_t p0 = bins[2 * tid], p1 = bins[2 * tid + 1];
         const uint32_t c0 = p0 & 0xFFFFu, c1 = p0 >> 16, c2 = p1 & 0xFFFFu, c3 = p1 >> 16;
@@ -1824,32 +1915,45 @@ extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) 
         if (i < n) idx[bin16[hbits(hh[i], shift, 10)] + rk[i]] = (uint16_t)i;
       }
       lds_barrier();
+      // final position of each record: its bin start + its (h32, key) rank among
+      // the bin's records, ties between equal keys broken by record index (they
+      // are summed, so their order is immaterial).  O(bin size) per record, so a
+      // bin full of one repeated word costs no thread more than its own scan.
+#pragma unroll 1
+      for (int j = 0; j < SR_PER; j++) {
+        const uint32_t i = tid + j * SR_THREADS;
+        if (i < n) {
+          const uint32_t hx = hh[i];
+          const uint32_t bn = hbits(hx, shift, 10);
+          const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
+          uint32_t r = 0;
+          if (hi - lo > 1) {
+            const uint4 kx = key[i];
+            const uint64_t x0 = ((uint64_t)kx.y << 32) | kx.x, x1 = ((uint64_t)kx.w << 32) | kx.z;
+            // batches of 4 with branch-free bodies: the LDS reads of a batch are
+            // issued together (a bin of one repeated word costs ~c/4 latencies)
+            for (uint32_t q0 = lo; q0 < hi; q0 += 4) {
+              uint32_t y[4], hy[4];
+              uint4 ky[4];
 #pragma unroll
-      for (int j = 0; j < 4; j++) {  // (h32, key) insertion sort of this thread's 4 tiny bins
-        const uint32_t bn = 4 * tid + j;
-        const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
-        for (uint32_t i = lo + 1; i < hi; i++) {
-          const uint16_t x = idx[i];
-          const uint32_t hx = hh[x];
-          const uint4 kx = key[x];
-          uint32_t q = i;
-          while (q > lo) {
-            const uint16_t y = idx[q - 1];
-            const uint32_t hy = hh[y];
-            bool less = hx < hy;
-            if (hx == hy) {
-              const uint4 ky = key[y];
-              const uint64_t a0 = ((uint64_t)kx.y << 32) | kx.x, b0 = ((uint64_t)ky.y << 32) | ky.x;
-              less = a0 != b0 ? a0 < b0 : ((((uint64_t)kx.w << 32) | kx.z) < (((uint64_t)ky.w << 32) | ky.z));
+              for (int t = 0; t < 4; t++) y[t] = idx[q0 + t < hi ? q0 + t : lo];
+#pragma unroll
+              for (int t = 0; t < 4; t++) { hy[t] = hh[y[t]]; ky[t] = key[y[t]]; }
+#pragma unroll
+              for (int t = 0; t < 4; t++) {
+                const uint64_t y0 = ((uint64_t)ky[t].y << 32) | ky[t].x, y1 = ((uint64_t)ky[t].w << 32) | ky[t].z;
+                const bool kl = y0 != x0 ? y0 < x0 : (y1 != x1 ? y1 < x1 : y[t] < i);
+                const bool less = hy[t] != hx ? hy[t] < hx : kl;
+                r += (q0 + t < hi && less) ? 1u : 0u;
+              }
             }
-            if (!less) break;
-            idx[q] = y;
-            q--;
           }
-          idx[q] = x;
+          idx2[lo + r] = (uint16_t)i;
         }
       }
+      SR_MARK(1);
       lds_barrier();
+      SR_MARK(2);
       bins[tid] = 0;  // bin starts are dead after the sort: zero for the next unit
       bins[tid + SR_THREADS] = 0;
       // run heads at sorted positions 4t..4t+3 -> output index by scan
@@ -1857,203 +1961,198 @@ extern "C" __global__ __launch_bounds__(SR_THREADS) void k_reduce_small(Work w) 
 #pragma unroll
       for (int j = 0; j < 4; j++) {
         const uint32_t p = 4 * tid + j;
-        if (p < n && (p == 0 || !key_eq16(key[idx[p]], key[idx[p - 1]]))) { hm |= 1u << j; nh++; }
+        if (p < n && (p == 0 || !key_eq16(key[idx2[p]], key[idx2[p - 1]]))) { hm |= 1u << j; nh++; }
       }
       const uint32_t incl = wave_incl_scan(nh);
       if (lane == 63) wsb[wv] = incl;
       lds_barrier();
       uint32_t o = incl - nh, nu = 0;
       for (int k = 0; k < SR_THREADS / 64; k++) { if (k < wv) o += wsb[k]; nu += wsb[k]; }
-#pragma unroll
+      uint32_t lb = 0;
+#pragma unroll 1
       for (int j = 0; j < 4; j++) {
         if (!((hm >> j) & 1u)) continue;
         const uint32_t p = 4 * tid + j;
-        const uint4 k = key[idx[p]];
-        unsigned long long c = cnt[idx[p]];
-        for (uint32_t q = p + 1; q < n && key_eq16(key[idx[q]], k); q++) c += cnt[idx[q]];
+        const uint4 k = key[idx2[p]];
+        unsigned long long c = cnt[idx2[p]];
+        // the run of equal keys after p, in batches of 4 (reads issued together)
+        for (uint32_t q0 = p + 1; q0 < n; q0 += 4) {
+          uint32_t y[4];
+#pragma unroll
+          for (int t = 0; t < 4; t++) y[t] = idx2[q0 + t < n ? q0 + t : p];
+          bool go = true;
+#pragma unroll
+          for (int t = 0; t < 4; t++) {
+            go = go && q0 + t < n && key_eq16(key[y[t]], k);
+            if (go) c += cnt[y[t]];
+          }
+          if (!go) break;
+        }
         w.uk[d.rec_off + o] = k;
         w.uc[d.rec_off + o] = c;
+        lb += key_len16(k);
         o++;
       }
+      if (lb) atomicAdd(&sbytes, lb);
       if (tid == 0) w.u_uniq[u] = nu;  // summed per partition by k_unit_uniq_scan
     }
     if (tid == 0) dring[it & 1] = dnn;
     lds_barrier();  // LDS reused by the next unit
+    if (cur_small && tid == 0) { w.u_bytes[u] = sbytes; sbytes = 0; }  // next adds come after >= 5 barriers
+    SR_MARK(3);
     in = inn;
   }
+#ifdef MOX_SR_STATS
+  if ((tid & 63) == 0)
+    for (int k = 0; k < 4; k++) atomicAdd(&w.ctl->dbg_cnt[k], (unsigned long long)cyc[k]);
+#endif
+#undef SR_MARK
 }
 
-// ------------------------------------------------------------------ scans
-extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_reduce(const uint64_t* v, const unsigned long long* n_ptr,
-                                                                      uint64_t n_const, uint64_t n_cap, uint64_t* part) {
-  __shared__ uint64_t red[SCAN_THREADS / 64];
-  uint64_t n = n_ptr ? *n_ptr : n_const;
-  if (n > n_cap) n = n_cap;
-  uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint64_t a = per * blockIdx.x, e = a + per;
-  if (e > n) e = n;
-  uint64_t sum = 0;
-  for (uint64_t i = a + threadIdx.x; i < e; i += SCAN_THREADS) sum += v[i];
-  for (int off = 32; off > 0; off >>= 1) sum += __shfl_down(sum, off);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sum;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    uint64_t t = 0;
-    for (int i = 0; i < SCAN_THREADS / 64; i++) t += red[i];
-    part[blockIdx.x] = t;
-  }
-}
-extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_parts(uint64_t* part, int nparts) {  // nparts == blockDim
-  __shared__ uint64_t wsum[16];
-  uint64_t tot;
-  const uint64_t ex = block_exscan(threadIdx.x < (unsigned)nparts ? part[threadIdx.x] : 0, wsum, tot);
-  if (threadIdx.x < (unsigned)nparts) part[threadIdx.x] = ex;
-  if (threadIdx.x == 0) part[nparts] = tot;
-}
-extern "C" __global__ __launch_bounds__(SCAN_THREADS) void k_scan_apply(const uint64_t* v, const unsigned long long* n_ptr,
-                                                                     uint64_t n_const, uint64_t n_cap, const uint64_t* part,
-                                                                     uint64_t* out) {
-  __shared__ uint64_t wsum[SCAN_THREADS / 64];
-  __shared__ uint64_t carry;
-  uint64_t n = n_ptr ? *n_ptr : n_const;
-  if (n > n_cap) n = n_cap;
-  uint64_t per = (n + gridDim.x - 1) / gridDim.x;
-  uint64_t a = per * blockIdx.x, e = a + per;
-  if (e > n) e = n;
-  if (threadIdx.x == 0) carry = part[blockIdx.x];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (uint64_t base = a; base < e; base += SCAN_THREADS) {
-    uint64_t i = base + threadIdx.x;
-    uint64_t x = i < e ? v[i] : 0;
-    uint64_t incl = x;
-    for (int off = 1; off < 64; off <<= 1) {
-      uint64_t y = __shfl_up(incl, off);
-      if (lane >= off) incl += y;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    uint64_t wpre = 0, tot = 0;
-    for (int k = 0; k < SCAN_THREADS / 64; k++) { if (k < wv) wpre += wsum[k]; tot += wsum[k]; }
-    if (i < e) out[i] = carry + wpre + incl - x;
-    __syncthreads();
-    if (threadIdx.x == 0) carry += tot;
-    __syncthreads();
-  }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) out[n] = part[gridDim.x];
-}
-
-// ------------------------------------------------------------------ long-word compaction
-extern "C" __global__ void k_long_flags(Work w, uint64_t* flags) {
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < w.long_cap; i += stride)
-    flags[i] = w.ltab[i].h != 0 ? 1 : 0;
-}
-
-// ------------------------------------------------------------------ table materialisation
-__device__ __forceinline__ uint32_t short_len(uint64_t w0, uint64_t w1) {
-  if (w1) return 16 - (__clzll(w1) >> 3);
-  return 8 - (__clzll(w0) >> 3);
-}
-
-// After k_reduce + k_unit_uniq_scan: total short uniques + per-partition dense
-// offsets; n_total = short + long.
-extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {  // one workgroup of NB threads
-  __shared__ uint64_t wsum[16];
-  uint64_t tot;
-  const bool rerun = (w.ctl->overflow & OVF_RERUN) != 0;  // nothing was reduced
-  const uint32_t b = threadIdx.x;
-  const uint64_t ex = block_exscan(rerun ? 0 : w.b_uniq[b], wsum, tot);
-  w.uniq_off[b] = ex;
-  if (b == 0) {
-    w.uniq_off[NB] = tot;
-    w.ctl->n_short = tot;
-    const unsigned long long nl = w.ctl->long_uniq;
-    w.ctl->n_total = tot + nl;
-    if (tot + nl > w.table_cap) atomicOr(&w.ctl->overflow, OVF_TABLE);
-  }
-}
-
-// Dense offsets of units relative to their partition, and the distinct keys of
-// split partitions (one workgroup per partition; no global atomics in the
-// reduce kernels, whose units of one partition run side by side).
+// ------------------------------------------------------------------ table directory
+// k_unit_uniq_scan (one workgroup per partition): offsets of a split
+// partition's units inside the partition (keys and key bytes) and the
+// partition's totals; plus, for long-table slice b, its occupied slots and their
+// bytes.  No global atomics in the reduce kernels, whose units of one partition
+// run side by side.
 extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) {
   __shared__ uint64_t wsum[16];
+  __shared__ unsigned long long lsn, lsb;
   const uint32_t b = blockIdx.x;
+  const int tid = threadIdx.x;
   if (w.ctl->overflow & OVF_RERUN) return;
   const uint32_t kk = w.b_kk[b], u0 = w.u_base[b];
-  if (!kk) { if (threadIdx.x == 0) w.u_uniq_off[u0] = 0; return; }
-  const uint32_t nsub = 1u << kk;
-  const uint32_t s0 = 2 * threadIdx.x, s1 = s0 + 1;  // SUB_N == 2 x blockDim
-  const uint64_t v0 = s0 < nsub ? w.u_uniq[u0 + s0] : 0, v1 = s1 < nsub ? w.u_uniq[u0 + s1] : 0;
-  uint64_t tot;
-  const uint64_t ex = block_exscan(v0 + v1, wsum, tot);
-  if (s0 < nsub) w.u_uniq_off[u0 + s0] = ex;
-  if (s1 < nsub) w.u_uniq_off[u0 + s1] = ex + v0;
-  if (threadIdx.x == 0) w.b_uniq[b] = tot;
+  if (!kk) {
+    if (tid == 0) { w.u_uniq_off[u0] = 0; w.u_bytes_off[u0] = 0; w.b_bytes[b] = w.u_bytes[u0]; }
+  } else {
+    const uint32_t nsub = 1u << kk;
+    const uint32_t s0 = 2 * tid, s1 = s0 + 1;  // SUB_N == 2 x blockDim
+    const uint64_t v0 = s0 < nsub ? w.u_uniq[u0 + s0] : 0, v1 = s1 < nsub ? w.u_uniq[u0 + s1] : 0;
+    const uint64_t y0 = s0 < nsub ? w.u_bytes[u0 + s0] : 0, y1 = s1 < nsub ? w.u_bytes[u0 + s1] : 0;
+    uint64_t tot, btot;
+    const uint64_t ex = block_exscan(v0 + v1, wsum, tot);
+    const uint64_t ey = block_exscan(y0 + y1, wsum, btot);
+    if (s0 < nsub) { w.u_uniq_off[u0 + s0] = ex; w.u_bytes_off[u0 + s0] = ey; }
+    if (s1 < nsub) { w.u_uniq_off[u0 + s1] = ex + v0; w.u_bytes_off[u0 + s1] = ey + y0; }
+    if (tid == 0) { w.b_uniq[b] = tot; w.b_bytes[b] = btot; }
+  }
+  // long-table slice b
+  const uint64_t L = w.long_cap / NB, s0 = (uint64_t)b * L;
+  if (tid == 0) { lsn = 0; lsb = 0; }
+  __syncthreads();
+  unsigned long long n = 0, by = 0;
+  for (uint64_t i = tid; i < L; i += blockDim.x) {
+    const LSlot e = w.ltab[s0 + i];
+    if (e.h) { n++; by += e.len; }
+  }
+  if (n) { atomicAdd(&lsn, n); atomicAdd(&lsb, by); }
+  __syncthreads();
+  if (tid == 0) { w.ls_n[b] = lsn; w.ls_b[b] = lsb; }
 }
 
-// True when this attempt produced a complete short-word table.
+// One workgroup of NB threads: partition / slice offsets, table sizes and the
+// table-capacity checks.  Short words come first (partition order = hash
+// order), then long words in slot order.
+extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {
+  __shared__ uint64_t wsum[16];
+  const bool rerun = (w.ctl->overflow & OVF_RERUN) != 0;  // nothing was reduced
+  const uint32_t b = threadIdx.x;
+  uint64_t ns, sb, nl, lb;
+  w.uniq_off[b] = block_exscan(rerun ? 0 : w.b_uniq[b], wsum, ns);
+  w.bytes_off[b] = block_exscan(rerun ? 0 : w.b_bytes[b], wsum, sb);
+  w.ls_off[b] = block_exscan(rerun ? 0 : w.ls_n[b], wsum, nl);
+  w.ls_boff[b] = block_exscan(rerun ? 0 : w.ls_b[b], wsum, lb);
+  if (b == 0) {
+    w.uniq_off[NB] = ns;
+    w.bytes_off[NB] = sb;
+    w.ls_off[NB] = nl;
+    w.ls_boff[NB] = lb;
+    w.ctl->n_short = ns;
+    w.ctl->short_bytes = sb;
+    w.ctl->n_total = ns + nl;
+    w.ctl->bytes_total = sb + lb;
+    if (ns + nl > w.table_cap) atomicOr(&w.ctl->overflow, OVF_TABLE);
+    else w.t_offs[ns + nl] = sb + lb;
+    if (sb + lb > w.bytes_cap) atomicOr(&w.ctl->overflow, OVF_BYTES);
+  }
+}
+
+// True when this attempt produced a complete table that fits its buffers.
 __device__ __forceinline__ bool table_ok(const Work& w) {
-  return !(w.ctl->overflow & OVF_RERUN) && w.ctl->n_total <= w.table_cap;
+  return !(w.ctl->overflow & (OVF_RERUN | OVF_TABLE | OVF_BYTES));
 }
 
-// counts + lengths in dense order, one reduce unit per workgroup iteration;
-// lengths go to lens[] (scanned into t_offs afterwards)
-extern "C" __global__ void k_mat_counts(Work w, uint64_t* lens) {
+// Exclusive scan over a 256-thread workgroup of two values at once.
+__device__ __forceinline__ void exscan2_256(uint32_t a, uint32_t b, uint32_t (*ws)[2], uint32_t& ea, uint32_t& eb,
+                                            uint32_t& ta, uint32_t& tb) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
+  if (lane == 63) { ws[wv][0] = ia; ws[wv][1] = ib; }
+  __syncthreads();
+  uint32_t pa = 0, pb = 0;
+  ta = 0; tb = 0;
+  for (int k = 0; k < 4; k++) { if (k < wv) { pa += ws[k][0]; pb += ws[k][1]; } ta += ws[k][0]; tb += ws[k][1]; }
+  __syncthreads();
+  ea = pa + ia - a;
+  eb = pb + ib - b;
+}
+
+// k_mat (256-thread workgroups): the dense table in one pass -- counts, byte
+// offsets and bytes of every short word (unit by unit, a workgroup scan of the
+// key lengths inside the unit) and of every long word (slice b by workgroup
+// b: scan of the occupied slots), and lpos for the exchange pack.
+extern "C" __global__ __launch_bounds__(256) void k_mat(Work w, Corpus c) {
+  __shared__ uint32_t ws[4][2];
   if (!table_ok(w)) return;
+  const int tid = threadIdx.x;
   const uint32_t U = (uint32_t)w.ctl->n_units;
   for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
     const UnitDesc ud = w.udesc[u];
-    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
-    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint4 k = w.uk[src0 + i];
-      const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
-      w.t_counts[dst0 + i] = w.uc[src0 + i];
-      lens[dst0 + i] = short_len(w0, w1);
+    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off;
+    const uint64_t dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
+    uint64_t boff = w.bytes_off[ud.part] + w.u_bytes_off[u];
+    for (uint64_t i0 = 0; i0 < n; i0 += 256) {
+      const uint64_t i = i0 + tid;
+      uint4 k = make_uint4(0, 0, 0, 0);
+      uint32_t len = 0;
+      if (i < n) { k = w.uk[src0 + i]; len = key_len16(k); }
+      uint32_t ex, dummy, tot, t2;
+      exscan2_256(len, 0, ws, ex, dummy, tot, t2);
+      if (i < n) {
+        const uint64_t o = boff + ex;
+        w.t_counts[dst0 + i] = w.uc[src0 + i];
+        w.t_offs[dst0 + i] = o;
+        uint8_t* ob = w.t_bytes + o;
+        const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+        for (uint32_t j = 0; j < len; j++) ob[j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
+      }
+      boff += tot;
     }
   }
-}
-
-// long uniques in slot order: slot s occupied -> dense index ns + lpos[s]
-extern "C" __global__ void k_mat_long(Work w, uint64_t* lens) {
-  uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
-  if (nt > w.table_cap) return;
-  uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
-    LSlot e = w.ltab[s];
-    if (!e.h) continue;
-    uint64_t i = ns + w.lpos[s];
-    w.t_counts[i] = e.count;
-    lens[i] = e.len;
-  }
-}
-
-extern "C" __global__ void k_mat_bytes(Work w, Corpus c) {
-  if (!table_ok(w)) return;
-  const uint64_t ns = w.ctl->n_short, nt = w.ctl->n_total;
-  if (blockIdx.x == 0 && threadIdx.x == 0) w.ctl->bytes_total = w.t_offs[nt];
-  if (w.t_offs[nt] > w.bytes_cap) { if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&w.ctl->overflow, OVF_BYTES); return; }
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  const uint32_t U = (uint32_t)w.ctl->n_units;
-  for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
-    const UnitDesc ud = w.udesc[u];
-    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
-    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint4 k = w.uk[src0 + i];
-      const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
-      const uint32_t L = short_len(w0, w1);
-      uint8_t* o = w.t_bytes + w.t_offs[dst0 + i];
-      for (uint32_t j = 0; j < L; j++) o[j] = (uint8_t)((j < 8 ? w0 >> (8 * j) : w1 >> (8 * (j - 8))) & 0xFF);
+  // long words: slice b = slots [b L, (b + 1) L), in slot order
+  const uint64_t ns = w.ctl->n_short, sb = w.ctl->short_bytes, L = w.long_cap / NB;
+  for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
+    if (w.ls_n[b] == 0) continue;
+    uint64_t idx = w.ls_off[b], boff = sb + w.ls_boff[b];
+    for (uint64_t i0 = 0; i0 < L; i0 += 256) {
+      const uint64_t sl = (uint64_t)b * L + i0 + tid;
+      LSlot e{};
+      if (i0 + tid < L) e = w.ltab[sl];
+      const uint32_t occ = e.h ? 1u : 0u;
+      const uint32_t len = e.h ? (uint32_t)e.len : 0u;  // long words < 4 GiB
+      uint32_t ei, eb, ti, tb;
+      exscan2_256(occ, len, ws, ei, eb, ti, tb);
+      if (occ) {
+        const uint64_t di = ns + idx + ei, o = boff + eb;
+        w.lpos[sl] = idx + ei;
+        w.t_counts[di] = e.count;
+        w.t_offs[di] = o;
+        const uint64_t ref = e.ref - 1;
+        for (uint64_t j = 0; j < e.len; j++) w.t_bytes[o + j] = ref_byte(c.base, w.arena, ref, j);
+      }
+      idx += ti;
+      boff += tb;
     }
-  }
-  for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < w.long_cap; s += stride) {
-    LSlot e = w.ltab[s];
-    if (!e.h) continue;
-    uint64_t i = ns + w.lpos[s];
-    uint8_t* o = w.t_bytes + w.t_offs[i];
-    uint64_t ref = e.ref - 1;
-    for (uint64_t j = 0; j < e.len; j++) o[j] = ref_byte(c.base, w.arena, ref, j);
   }
 }
 

@@ -107,9 +107,10 @@ def lib():
     """Load libmox.so (fails loudly: there is no fallback path)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            raise MoxError(MOX_ESTATE, "%s not built (run `make` or __graft_entry__.build())" % LIB_PATH)
-        L = ctypes.CDLL(LIB_PATH)
+        path = os.environ.get("MOX_LIB", LIB_PATH)  # diagnostics builds only (tools/)
+        if not os.path.exists(path):
+            raise MoxError(MOX_ESTATE, "%s not built (run `make` or __graft_entry__.build())" % path)
+        L = ctypes.CDLL(path)
         P, U64, I, VP = ctypes.POINTER, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
         sz = ctypes.c_size_t
         sig = {
