@@ -598,9 +598,9 @@ int grow_pinned(DevBuf& b, size_t bytes) {
 // every pair by construction).
 struct Transport {
   virtual ~Transport() = default;
-  // per-peer count rows: h_send[d] -> peer d; fills h_recv[s] from peer s.
-  // d_send / d_recv are device mirrors (d_send already holds h_send).
-  virtual int counts(const XCnt* d_send, XCnt* d_recv, const XCnt* h_send, XCnt* h_recv) = 0;
+  // per-peer count rows: d_send[d] (device, just written by k_xcount) -> peer
+  // d; on return h_send holds this rank's rows and h_recv[s] peer s's rows.
+  virtual int counts(const XCnt* d_send, XCnt* d_recv, XCnt* h_send, XCnt* h_recv) = 0;
   virtual int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
                         const uint64_t* rlen) = 0;
 };
@@ -608,7 +608,8 @@ struct Transport {
 struct RcclTransport : Transport {
   mox_engine* e;
   explicit RcclTransport(mox_engine* e_) : e(e_) {}
-  int counts(const XCnt* d_send, XCnt* d_recv, const XCnt*, XCnt* h_recv) override {
+  int counts(const XCnt* d_send, XCnt* d_recv, XCnt* h_send, XCnt* h_recv) override {
+    // device to device right after k_xcount: one host synchronisation for both rows
     const int P = e->nranks;
     RCCLCHK(ncclGroupStart());
     for (int p = 0; p < P; p++) {
@@ -616,6 +617,7 @@ struct RcclTransport : Transport {
       RCCLCHK(ncclRecv(d_recv + p, sizeof(XCnt), ncclUint8, p, e->comm, e->stream));
     }
     RCCLCHK(ncclGroupEnd());
+    HIPCHK(hipMemcpyAsync(h_send, d_send, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipMemcpyAsync(h_recv, d_recv, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
     return MOX_OK;
@@ -644,7 +646,9 @@ struct HostTransport : Transport {
   mox_alltoallv_fn fn;
   void* user;
   HostTransport(mox_engine* e_, int P_, mox_alltoallv_fn f, void* u) : e(e_), P(P_), fn(f), user(u) {}
-  int counts(const XCnt*, XCnt*, const XCnt* h_send, XCnt* h_recv) override {
+  int counts(const XCnt* d_send, XCnt*, XCnt* h_send, XCnt* h_recv) override {
+    HIPCHK(hipMemcpyAsync(h_send, d_send, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
     uint64_t len[MAX_RANKS];
     for (int p = 0; p < P; p++) len[p] = sizeof(XCnt);
     if (fn(user, h_send, len, h_recv, len) != 0) return fail(MOX_EIO, "host all-to-all callback failed (counts)");
@@ -706,8 +710,6 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   // 1. per-destination counts
   HIPCHK(hipMemsetAsync(d_send, 0, P * sizeof(XCnt), s));
   hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, s, w, (uint32_t)P, d_send);
-  HIPCHK(hipMemcpyAsync(h_send, d_send, P * sizeof(XCnt), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipStreamSynchronize(s));
   if ((rc = T.counts(d_send, d_recv, h_send, h_recv))) return rc;
   // 2. send layout + pack
   uint64_t s_short_off[MAX_RANKS], s_short_len[MAX_RANKS], s_blob_off[MAX_RANKS], s_blob_len[MAX_RANKS];
@@ -758,9 +760,8 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   need.bytes_cap = std::max<uint64_t>(need.bytes_cap, rs * 16 + rb + 65536);
   need.long_cap = std::max<uint64_t>(need.long_cap, next_pow2(2 * r_long + 1024));
   need.arena_cap = std::max<uint64_t>(need.arena_cap, rb + 65536);
-  HIPCHK(hipStreamSynchronize(s));
   e->have_result = false;
-  if ((rc = ensure_caps(e, need))) return rc;
+  if ((rc = ensure_caps(e, need))) return rc;  // stream-ordered; a regrow synchronises the device itself
   for (int attempt = 0;; attempt++) {
     if ((rc = exchange_pass_once(e, rs, rb, rdir))) return rc;
     const Ctl& h = *e->h_ctl;

@@ -425,39 +425,55 @@ __device__ __forceinline__ void key_at(const MapLds& s, const uint8_t* rowbuf, u
   K[2] = __builtin_amdgcn_alignbyte(E3, E2, sh) & M.z;
   K[3] = __builtin_amdgcn_alignbyte(E4, E3, sh) & M.w;
 }
+
+// 16-byte key equality as one OR of XORs (kept opaque: the combiner would
+// otherwise split it into four compares and a boolean tree)
 __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
-  return ((k.x ^ K[0]) | (k.y ^ K[1]) | (k.z ^ K[2]) | (k.w ^ K[3])) == 0;
+  uint32_t d;
+  asm("v_xor_b32 %0, %1, %2" : "=v"(d) : "v"(k.x), "v"(K[0]));
+  uint32_t d1, d2, d3;
+  asm("v_xor_b32 %0, %1, %2" : "=v"(d1) : "v"(k.y), "v"(K[1]));
+  asm("v_xor_b32 %0, %1, %2" : "=v"(d2) : "v"(k.z), "v"(K[2]));
+  asm("v_xor_b32 %0, %1, %2" : "=v"(d3) : "v"(k.w), "v"(K[3]));
+  uint32_t o;
+  asm("v_or3_b32 %0, %1, %2, %3" : "=v"(o) : "v"(d), "v"(d1), "v"(d2));
+  return (o | d3) == 0;
 }
 
 // Token pass A over TU batches of 64 list entries (lane = token): key, hash,
 // one LDS read of the home slot.  Hits count in LDS; misses are compacted in
 // place to the front of the list (entry index <= read index, and every read of
-// this call precedes its writes).  Returns the new miss count.
+// this call precedes its writes).  Returns the new miss count.  Branch-free up
+// to the hit test, so the TU batches' LDS reads are issued together (the
+// dictionary arrays are zero when there is no dictionary: a real key is never
+// zero, so nothing hits).
 template <int TU>
 __device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbuf, uint16_t* list, uint32_t j0,
-                                           uint32_t total, uint32_t nmiss, bool use_dict) {
+                                           uint32_t total, uint32_t nmiss) {
   const int lane = threadIdx.x & 63;
   const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t e[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
-    e[u] = j < total ? (uint32_t)list[j] : 0x8000u;  // inactive = odd
+    const uint32_t r = list[j < TOKMAX ? j : TOKMAX - 1];
+    e[u] = j < total ? r : 0x8000u;  // inactive = odd
   }
-  bool hit[TU];
-  uint32_t home[TU];
+  uint32_t K[TU][4], home[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) {
-    uint32_t K[4];
-    key_at(m.s, rowbuf, e[u], K);
-    const uint32_t h = hash32(K[0], K[1], K[2], K[3]);
-    home[u] = dict_home(h);
-    hit[u] = use_dict && key_eq4(m.s.dkey[home[u]], K);
-  }
+  for (int u = 0; u < TU; u++) key_at(m.s, rowbuf, e[u], K[u]);
+#pragma unroll
+  for (int u = 0; u < TU; u++) home[u] = dict_home(hash32(K[u][0], K[u][1], K[u][2], K[u][3]));
+  uint4 dk[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) dk[u] = m.s.dkey[home[u]];
+  bool hit[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) hit[u] = !(e[u] & 0x8000u) && key_eq4(dk[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const bool valid = !(e[u] & 0x8000u);
-    if (valid && hit[u] && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[home[u]], 1u);
+    if (hit[u] && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[home[u]], 1u);
     const bool miss = valid && !hit[u];
     const uint64_t bm = __ballot(miss);
     if (miss) list[nmiss + (uint32_t)__popcll(bm & lt)] = (uint16_t)e[u];
@@ -470,15 +486,16 @@ __device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbu
 // (8 tags), key check, then an LDS count or the cold store.
 template <int TU>
 __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t nmiss, bool use_dict) {
+                                       uint32_t nmiss) {
   const int lane = threadIdx.x & 63;
   uint32_t e[TU];
   bool valid[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
+    const uint32_t r = list[j < TOKMAX ? j : TOKMAX - 1];
     valid[u] = j < nmiss;
-    e[u] = valid[u] ? (uint32_t)list[j] : 0u;
+    e[u] = valid[u] ? r : 0u;
   }
   uint32_t K[TU][4], h[TU];
   int slot[TU];
@@ -486,24 +503,29 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
   for (int u = 0; u < TU; u++) {
     key_at(m.s, rowbuf, e[u], K[u]);
     h[u] = hash32(K[u][0], K[u][1], K[u][2], K[u][3]);
-    slot[u] = -1;
-    if (use_dict) {
-      const uint32_t b1 = dict_g1(h[u]), b2 = dict_g2(h[u]);
-      const uint4 t1 = m.s.dtag4[b1], t2 = m.s.dtag4[b2];
-      int sl = t2.w == h[u] ? (int)(4 * b2 + 3) : -1;
-      sl = t2.z == h[u] ? (int)(4 * b2 + 2) : sl;
-      sl = t2.y == h[u] ? (int)(4 * b2 + 1) : sl;
-      sl = t2.x == h[u] ? (int)(4 * b2 + 0) : sl;
-      sl = t1.w == h[u] ? (int)(4 * b1 + 3) : sl;
-      sl = t1.z == h[u] ? (int)(4 * b1 + 2) : sl;
-      sl = t1.y == h[u] ? (int)(4 * b1 + 1) : sl;
-      sl = t1.x == h[u] ? (int)(4 * b1 + 0) : sl;
-      slot[u] = sl;
-    }
   }
+  uint4 t1[TU], t2[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) { t1[u] = m.s.dtag4[dict_g1(h[u])]; t2[u] = m.s.dtag4[dict_g2(h[u])]; }
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const uint32_t b1 = dict_g1(h[u]), b2 = dict_g2(h[u]);
+    int sl = t2[u].w == h[u] ? (int)(4 * b2 + 3) : -1;
+    sl = t2[u].z == h[u] ? (int)(4 * b2 + 2) : sl;
+    sl = t2[u].y == h[u] ? (int)(4 * b2 + 1) : sl;
+    sl = t2[u].x == h[u] ? (int)(4 * b2 + 0) : sl;
+    sl = t1[u].w == h[u] ? (int)(4 * b1 + 3) : sl;
+    sl = t1[u].z == h[u] ? (int)(4 * b1 + 2) : sl;
+    sl = t1[u].y == h[u] ? (int)(4 * b1 + 1) : sl;
+    sl = t1[u].x == h[u] ? (int)(4 * b1 + 0) : sl;
+    slot[u] = sl;
+  }
+  uint4 dk[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) dk[u] = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
   bool hit[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) hit[u] = slot[u] >= 0 && key_eq4(m.s.dkey[slot[u] < 0 ? 0 : slot[u]], K[u]);
+  for (int u = 0; u < TU; u++) hit[u] = slot[u] >= 0 && key_eq4(dk[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     if (!valid[u]) continue;
@@ -601,22 +623,21 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     }
   }
   if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
-  const bool use_dict = m.dict_n && !MOX_ABL(m.w.dbg, DBG_NO_DICT);
   uint64_t t1 = 0;
   if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
   uint32_t nmiss = 0;
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
-    if (rem > 128) { nmiss = pass_a<3>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 192; }
-    else if (rem > 64) { nmiss = pass_a<2>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 128; }
-    else { nmiss = pass_a<1>(m, rowbuf, list, j0, total, nmiss, use_dict); j0 += 64; }
+    if (rem > 128) { nmiss = pass_a<3>(m, rowbuf, list, j0, total, nmiss); j0 += 192; }
+    else if (rem > 64) { nmiss = pass_a<2>(m, rowbuf, list, j0, total, nmiss); j0 += 128; }
+    else { nmiss = pass_a<1>(m, rowbuf, list, j0, total, nmiss); j0 += 64; }
   }
   wave_lds_fence();
   uint64_t t2 = 0;
   if (cyc) { t2 = __builtin_amdgcn_s_memtime(); cyc->pa += t2 - t1; }
   for (uint32_t j0 = 0; j0 < nmiss;) {
-    if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 128; }
-    else { pass_b<1>(m, rowbuf, list, j0, nmiss, use_dict); j0 += 64; }
+    if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss); j0 += 128; }
+    else { pass_b<1>(m, rowbuf, list, j0, nmiss); j0 += 64; }
   }
   if (cyc) { cyc->pb += __builtin_amdgcn_s_memtime() - t2; cyc->miss += nmiss; }
   wave_lds_fence();
@@ -651,9 +672,14 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   uint16_t* lists = (uint16_t*)sp;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.ctl->dict_n;
-  if (m.dict_n) {
-    for (int i = tid; i < DICT_BUCKETS; i += MAP_THREADS) m.s.dtag4[i] = reinterpret_cast<const uint4*>(w.dict_tag)[i];
-    for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) { m.s.dkey[i] = w.dict_key[i]; m.s.dcnt[i] = 0; }
+  if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
+  // the token passes probe unconditionally: without a dictionary the arrays are
+  // zero (no real key is zero, so nothing hits)
+  for (int i = tid; i < DICT_BUCKETS; i += MAP_THREADS)
+    m.s.dtag4[i] = m.dict_n ? reinterpret_cast<const uint4*>(w.dict_tag)[i] : make_uint4(0, 0, 0, 0);
+  for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
+    m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);
+    m.s.dcnt[i] = 0;
   }
   for (int i = tid; i < NB; i += MAP_THREADS) m.s.bcnt[i] = 0;
   if (tid < 4) m.s.misc[tid] = 0;
@@ -764,18 +790,35 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
       if (cnt) atomicAdd(&w.dict_tot[i], (unsigned long long)cnt);
     }
   }
+  // workgroup totals first: one global atomic each per workgroup (a per-thread
+  // atomic on one control-block word serialises 256K updates at the L2)
+  __shared__ unsigned long long s_tok;
+  __shared__ uint32_t s_cmax;
+  if (tid == 0) { s_tok = 0; s_cmax = 0; }
+  __syncthreads();
+  uint32_t cmax = 0;
   for (int i = tid; i < NB; i += MAP_THREADS) {
     const uint32_t cnt = m.s.bcnt[i];
     w.cold_n[(uint64_t)blockIdx.x * NB + i] = cnt < w.cold_cap ? cnt : w.cold_cap;
-    if (cnt) atomicMax(&w.ctl->cold_need, cnt);
+    cmax = cnt > cmax ? cnt : cmax;
   }
+  for (int off = 32; off > 0; off >>= 1) {
+    ntok += __shfl_down(ntok, off);
+    const uint32_t o = __shfl_down(cmax, off);
+    cmax = o > cmax ? o : cmax;
+  }
+  if (lane == 0) {
+    if (ntok) atomicAdd(&s_tok, ntok);
+    if (cmax) atomicMax(&s_cmax, cmax);
+  }
+  __syncthreads();
   if (tid == 0) {
     const uint32_t sn = m.s.misc[0];
     w.spill_n[blockIdx.x] = sn < w.spill_cap ? sn : w.spill_cap;
     if (sn) atomicMax(&w.ctl->spill_need, sn);
+    if (s_cmax) atomicMax(&w.ctl->cold_need, (unsigned long long)s_cmax);
+    if (s_tok) atomicAdd(&w.ctl->tokens, s_tok);
   }
-  for (int off = 32; off > 0; off >>= 1) ntok += __shfl_down(ntok, off);
-  if (lane == 0 && ntok) atomicAdd(&w.ctl->tokens, ntok);
 }
 
 // ------------------------------------------------------------------ pass init
@@ -1214,24 +1257,57 @@ extern "C" __global__ __launch_bounds__(NB) void k_bucket_scan(Work w) {  // one
   }
 }
 
-extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {  // same mapping as k_hist
+// Weighted records (and this map workgroup's spills) to their partition's range
+// of w_sorted.  Each workgroup takes a contiguous chunk, ranks its records per
+// partition in LDS, reserves one range per (workgroup, partition) with a single
+// global atomic, then writes: no per-record global atomics (an exchange pass
+// scatters ~1e6 received records per rank, in partition order per source).
+constexpr int SCT_PER = 8;  // records per thread per sub-chunk
+template <bool KEYS>  // KEYS: src holds uint4 keys (spills, count 1); else WRec
+__device__ __forceinline__ void scatter_sub(const Work& w, uint32_t* lh, uint32_t* base, uint64_t n, const void* src) {
+  const int tid = threadIdx.x;
+  uint32_t bk[SCT_PER], li[SCT_PER];
+  uint64_t r0[SCT_PER], r1[SCT_PER], rc[SCT_PER];
+  for (int i = tid; i < NB; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SCT_PER; j++) {
+    const uint64_t i = (uint64_t)j * blockDim.x + tid;
+    const bool ok = i < n;
+    const uint64_t ii = ok ? i : 0;
+    if (KEYS) {
+      const uint4 k = reinterpret_cast<const uint4*>(src)[ii];
+      r0[j] = ((uint64_t)k.y << 32) | k.x;
+      r1[j] = ((uint64_t)k.w << 32) | k.z;
+      rc[j] = 1;
+    } else {
+      const WRec q = reinterpret_cast<const WRec*>(src)[ii];
+      r0[j] = q.w0;
+      r1[j] = q.w1;
+      rc[j] = q.count;
+    }
+    bk[j] = ok ? bucket_of(key_hash(r0[j], r1[j])) : 0xFFFFFFFFu;
+    li[j] = ok ? atomicAdd(&lh[bk[j]], 1u) : 0u;
+  }
+  __syncthreads();
+  for (int i = tid; i < NB; i += blockDim.x) base[i] = lh[i] ? atomicAdd(&w.b_cur[i], lh[i]) : 0u;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SCT_PER; j++)
+    if (bk[j] != 0xFFFFFFFFu) w.w_sorted[w.w_off[bk[j]] + base[bk[j]] + li[j]] = WRec{r0[j], r1[j], rc[j]};
+  __syncthreads();
+}
+extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {
+  __shared__ uint32_t lh[NB], base[NB];
   if (w.ctl->w_total > w.w_cap) return;
-  const uint32_t g = blockIdx.x;
+  const uint32_t g = blockIdx.x, G = gridDim.x;
   uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
-  for (uint64_t i = (uint64_t)g * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
-    const WRec r = w.w[i];
-    const uint32_t b = bucket_of(key_hash(r.w0, r.w1));
-    const uint32_t k = atomicAdd(&w.b_cur[b], 1u);
-    w.w_sorted[w.w_off[b] + k] = r;
-  }
+  const uint64_t per = (nw + G - 1) / G, lo = (uint64_t)g * per, hi = lo + per < nw ? lo + per : nw;
+  const uint64_t sub = (uint64_t)SCT_PER * blockDim.x;
+  for (uint64_t a = lo; a < hi; a += sub) scatter_sub<false>(w, lh, base, hi - a < sub ? hi - a : sub, w.w + a);
   const uint32_t ns = w.spill_n[g];
-  for (uint32_t i = threadIdx.x; i < ns; i += blockDim.x) {
-    const uint4 k = w.spill[(uint64_t)g * w.spill_cap + i];
-    const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
-    const uint32_t b = bucket_of(key_hash(w0, w1));
-    const uint32_t j = atomicAdd(&w.b_cur[b], 1u);
-    w.w_sorted[w.w_off[b] + j] = WRec{w0, w1, 1};
-  }
+  const uint4* sp = w.spill + (uint64_t)g * w.spill_cap;
+  for (uint64_t a = 0; a < ns; a += sub) scatter_sub<true>(w, lh, base, ns - a < sub ? ns - a : sub, sp + a);
 }
 
 // ------------------------------------------------------------------ bucket reduce
@@ -2230,8 +2306,13 @@ extern "C" __global__ void k_xingest(Work w, XDir dir, uint64_t n_short) {
     atomicAdd(&w.ctl->long_n, 1ull);
     tok += hd.count;
   }
+  __shared__ unsigned long long s_tok;
+  if (threadIdx.x == 0) s_tok = 0;
+  __syncthreads();
   for (int off = 32; off > 0; off >>= 1) tok += __shfl_down(tok, off);
-  if ((threadIdx.x & 63) == 0 && tok) atomicAdd(&w.ctl->tokens, tok);
+  if ((threadIdx.x & 63) == 0 && tok) atomicAdd(&s_tok, tok);
+  __syncthreads();
+  if (threadIdx.x == 0 && s_tok) atomicAdd(&w.ctl->tokens, s_tok);  // one global atomic per workgroup
 }
 
 }  // namespace mox
