@@ -1912,7 +1912,7 @@ __device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, boo
 // (~0.5 records per bin), (h32, key) insertion sort inside bins so equal keys
 // are adjacent, run heads compacted by a scan, each head sums its run.  Output
 // order (h32, key), as k_reduce.
-extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work w) {  // 4 per CU: <= 128 VGPRs
+extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work w) {  // 4 per CU: <= 128 VGPRs (no spills: batches of 2)
   __shared__ uint4 key[SMALL_CAP];
   __shared__ unsigned long long cnt[SMALL_CAP];
   __shared__ uint32_t hh[SMALL_CAP];
@@ -1947,7 +1947,19 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
 #endif
   for (uint32_t it = 0; u < U; u += G, it++) {
     const UnitDesc d = dring[it & 1], dn = dring[(it + 1) & 1];
-    const bool cur_small = small_unit(d);
+    bool cur_small = small_unit(d);
+#ifdef MOX_SR_CHECK
+    if (cur_small && (d.in_off + d.in_n > w.split_k_cap || d.win_off + d.win_n > w.split_w_cap ||
+                      d.rec_off + d.in_n + d.win_n > w.uniq_cap)) {
+      if (tid == 0) {
+        atomicAdd(&w.ctl->dbg_cnt[0], 1ull);
+        atomicMax(&w.ctl->dbg_cnt[1], (unsigned long long)u);
+        atomicMax(&w.ctl->dbg_cnt[2], (unsigned long long)d.in_off + d.in_n);
+        atomicMax(&w.ctl->dbg_cnt[3], (unsigned long long)d.rec_off + d.in_n + d.win_n);
+      }
+      cur_small = false;
+    }
+#endif
     const uint32_t n = d.in_n + d.win_n, shift = NB_LOG2 + d.kk;
     // this unit's records into LDS + bin counts (bins were zeroed by the previous unit)
     if (cur_small) {
@@ -2006,17 +2018,17 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
           if (hi - lo > 1) {
             const uint4 kx = key[i];
             const uint64_t x0 = ((uint64_t)kx.y << 32) | kx.x, x1 = ((uint64_t)kx.w << 32) | kx.z;
-            // batches of 4 with branch-free bodies: the LDS reads of a batch are
-            // issued together (a bin of one repeated word costs ~c/4 latencies)
-            for (uint32_t q0 = lo; q0 < hi; q0 += 4) {
-              uint32_t y[4], hy[4];
-              uint4 ky[4];
+            // batches of 2 with branch-free bodies: the LDS reads of a batch are
+            // issued together (a bin of one repeated word costs ~c/2 latencies)
+            for (uint32_t q0 = lo; q0 < hi; q0 += 2) {
+              uint32_t y[2], hy[2];
+              uint4 ky[2];
 #pragma unroll
-              for (int t = 0; t < 4; t++) y[t] = idx[q0 + t < hi ? q0 + t : lo];
+              for (int t = 0; t < 2; t++) y[t] = idx[q0 + t < hi ? q0 + t : lo];
 #pragma unroll
-              for (int t = 0; t < 4; t++) { hy[t] = hh[y[t]]; ky[t] = key[y[t]]; }
+              for (int t = 0; t < 2; t++) { hy[t] = hh[y[t]]; ky[t] = key[y[t]]; }
 #pragma unroll
-              for (int t = 0; t < 4; t++) {
+              for (int t = 0; t < 2; t++) {
                 const uint64_t y0 = ((uint64_t)ky[t].y << 32) | ky[t].x, y1 = ((uint64_t)ky[t].w << 32) | ky[t].z;
                 const bool kl = y0 != x0 ? y0 < x0 : (y1 != x1 ? y1 < x1 : y[t] < i);
                 const bool less = hy[t] != hx ? hy[t] < hx : kl;
@@ -2051,14 +2063,14 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
         const uint32_t p = 4 * tid + j;
         const uint4 k = key[idx2[p]];
         unsigned long long c = cnt[idx2[p]];
-        // the run of equal keys after p, in batches of 4 (reads issued together)
-        for (uint32_t q0 = p + 1; q0 < n; q0 += 4) {
-          uint32_t y[4];
+        // the run of equal keys after p, in batches of 2 (reads issued together)
+        for (uint32_t q0 = p + 1; q0 < n; q0 += 2) {
+          uint32_t y[2];
 #pragma unroll
-          for (int t = 0; t < 4; t++) y[t] = idx2[q0 + t < n ? q0 + t : p];
+          for (int t = 0; t < 2; t++) y[t] = idx2[q0 + t < n ? q0 + t : p];
           bool go = true;
 #pragma unroll
-          for (int t = 0; t < 4; t++) {
+          for (int t = 0; t < 2; t++) {
             go = go && q0 + t < n && key_eq16(key[y[t]], k);
             if (go) c += cnt[y[t]];
           }
