@@ -22,6 +22,7 @@ constexpr int LD_GROUP = 6;                 // loader: rows per register group
 constexpr int LD_GROUPS = 3;                // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_LOADERS = 2;              // loader waves (alternate row groups)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
+static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
 constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots

@@ -605,15 +605,34 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   // list entry (u16): slot offset (10 bits) | length (5 bits, <= 16) | odd (bit 15)
   uint32_t k = pre;
   bool any_odd = false;
-  while (start) {
-    const uint32_t p = __builtin_ctz(start);
-    start &= start - 1;
-    const uint32_t rest = ws32 >> p;
-    const uint32_t len = rest ? __builtin_ctz(rest) : 32;
-    bool odd = slow || len > 16;
-    if (chk) odd = odd || p + len >= lim || ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
-    any_odd |= odd;
-    list[k++] = (uint16_t)((uint32_t)(lane * 16) + p + (odd ? 0x8000u : (len << 10)));
+  if (!chk && !slow) {
+    // common rows: a wave-uniform loop (trip count = most starts in any lane)
+    // with no divergence; a lane that has run out of starts writes the sink
+    // entry list[TOKMAX - 1], which no row reaches (<= PAY / 2 tokens)
+    uint32_t st = start;
+    uint16_t* const sink = list + (TOKMAX - 1);
+    while (__any(st != 0)) {
+      const bool valid = st != 0;
+      const uint32_t p = valid ? (uint32_t)__builtin_ctz(st) : 0u;
+      st &= st - 1;
+      const uint32_t rest = ws32 >> p;
+      const uint32_t len = rest ? (uint32_t)__builtin_ctz(rest) : 32u;
+      const bool odd = len > 16;
+      any_odd |= odd && valid;
+      *(valid ? list + k : sink) = (uint16_t)((uint32_t)(lane * 16) + p + (odd ? 0x8000u : (len << 10)));
+      k += valid ? 1u : 0u;
+    }
+  } else {
+    while (start) {
+      const uint32_t p = __builtin_ctz(start);
+      start &= start - 1;
+      const uint32_t rest = ws32 >> p;
+      const uint32_t len = rest ? __builtin_ctz(rest) : 32;
+      bool odd = slow || len > 16;
+      if (chk) odd = odd || p + len >= lim || ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
+      any_odd |= odd;
+      list[k++] = (uint16_t)((uint32_t)(lane * 16) + p + (odd ? 0x8000u : (len << 10)));
+    }
   }
   wave_lds_fence();
   if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
