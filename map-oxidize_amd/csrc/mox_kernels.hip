@@ -11,14 +11,15 @@
 //                             32-byte window), UTF-8 validation + Unicode whitespace
 //                             on tiles with non-ASCII bytes, hot words counted in an
 //                             LDS dictionary, all other words emitted as exact 16-byte
-//                             keys into 256 hash partitions through LDS queues
+//                             keys into 1024 hash partitions
 //                             (= the shuffle write, main.rs:103-109)
 //   k_unicode                 full Unicode lowercase + Final_Sigma for non-ASCII tokens
 //   k_dict_totals, k_hist, k_bucket_scan, k_scatter   shuffle directory
-//   k_reduce                  per-partition LDS hash group-by (= reduce_phase merge,
-//                             main.rs:132-134) + LDS bitonic sort by hash
-//   k_long_*                  words > 16 bytes: hashed keys, byte-compare resolution
-//   k_mat_* + scans           dense (word, count) table in HBM
+//   k_split_*, k_unit_scan    high-cardinality split of partitions into sub-bucket units
+//   k_reduce, k_reduce_small  per-unit LDS hash group-by / sort-based reduce (= reduce_phase merge,
+//                             main.rs:132-134), deterministic (hash, key) order
+//   long table                words > 16 bytes: hashed keys, byte-compare resolution
+//   k_unit_uniq_scan, k_final_scan, k_mat   dense (word, count) table in HBM, one pass
 #include "mox_internal.h"
 
 namespace mox {
