@@ -4,7 +4,7 @@
 //   split_file (:36-51) -> map_phase/count_words (:53-101) -> write/read map files
 //   (:103-109, :152-168) -> reduce_phase (:111-150)
 // re-designed as (DESIGN.md has the data layout and rooflines):
-//   k_sample + k_dict_build   hot-word dictionary from a 64 x 64 KiB sample
+//   k_sample + k_dict_*       hot-word dictionary from a 192 x 4 KiB sample
 //   k_map                     one streaming pass over the corpus in HBM: 16 B/lane
 //                             coalesced loads, ASCII fast path (SWAR whitespace /
 //                             case classification, per-lane token extraction from a

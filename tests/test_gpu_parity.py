@@ -271,3 +271,28 @@ def test_split_deterministic_order(eng):
     a = _gpu_arrays(eng, data)
     b = _gpu_arrays(eng, data)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+
+
+def test_count_file_streamed_chunks(tmp_path, eng):
+    """mox_count_file reads in 32 MiB chunks through 8 reader threads x 2 pinned
+    buffers: a 600 MiB + 12345 byte file exercises buffer reuse and a ragged tail;
+    the empty file and a one-word file the edges."""
+    from conftest import assert_tables_equal
+    import numpy as np
+    data = corpus.fill(corpus.ZIPF, 33, 0, (600 << 20) + 12345)
+    f = tmp_path / "big.txt"
+    data.tofile(str(f))
+    t = eng.count_file(str(f))
+    got = t.arrays()
+    t.close()
+    assert eng.stats()["ms_h2d"] > 0
+    wc, wo, wraw, _ = coracle.count_arrays(data, nthreads=16)
+    assert_tables_equal(got, (wc, wo, wraw))
+    for small in (b"", b"Word"):
+        g = tmp_path / "small.txt"
+        g.write_bytes(small)
+        t = eng.count_file(str(g))
+        assert t.sorted_items() == coracle.count(small)[0]
+        t.close()
+    with pytest.raises(mox.MoxError):
+        eng.count_file(str(tmp_path / "missing.txt"))
