@@ -134,3 +134,20 @@ def test_host_exchange_high_cardinality():
     wc, wo, wraw, wtok = coracle.count_arrays(np.frombuffer(data, np.uint8), nthreads=16)
     assert sum(tok for _, tok in out) == wtok
     assert_tables_equal((counts, offs, b"".join(words)), (wc, wo, wraw))
+
+
+def test_host_exchange_zipf_many_records():
+    """2 ranks x 48 MiB of Zipf text: ~1e5 received partials per rank go through
+    the LDS-aggregated scatter of the reduce-only pass; exact vs the oracle."""
+    from conftest import assert_tables_equal
+    import numpy as np
+    data = corpus.fill(corpus.ZIPF, 92, 0, 96 << 20).tobytes()
+    out = run_ranks(data, 2)
+    items = [w for part, _ in out for w in part]
+    counts = np.array([c for _, c in items], dtype=np.uint64)
+    words = [w for w, _ in items]
+    offs = np.zeros(len(words) + 1, dtype=np.int64)
+    offs[1:] = np.cumsum([len(w) for w in words])
+    wc, wo, wraw, wtok = coracle.count_arrays(np.frombuffer(data, np.uint8), nthreads=16)
+    assert sum(tok for _, tok in out) == wtok
+    assert_tables_equal((counts, offs, b"".join(words)), (wc, wo, wraw))
