@@ -1727,46 +1727,67 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
           return m ? (uint32_t)__builtin_ctzll(m) : nreg;
         };
-        auto load = [&](uint32_t k, uint32_t i0, uint4 (&v)[RED_UNROLL]) {
-          const uint32_t n = __builtin_amdgcn_readlane(myn, k);
+        // Loads are unconditional (an index past the region end, or a region
+        // past the last, reads a valid dummy record; process() masks by
+        // position), so every chunk issues exactly RED_UNROLL loads and the
+        // compiler can wait for one chunk while the next is still in flight.
+        auto load = [&](uint32_t kq, uint32_t iq, uint4 (&v)[RED_UNROLL]) {
+          const uint32_t kc = kq < nreg ? kq : 0u;  // nreg >= 1 inside the loop
+          const uint32_t n = __builtin_amdgcn_readlane(myn, kc);
           const uint4* reg = split ? w.split_k + kin0 + (uint64_t)wv * kchunk
-                                   : w.cold + ((uint64_t)(wv + k * NWV) * NB + b) * w.cold_cap;
+                                   : w.cold + ((uint64_t)(wv + kc * NWV) * NB + b) * w.cold_cap;
+          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
           for (int u2 = 0; u2 < RED_UNROLL; u2++) {
-            const uint32_t i = i0 + u2 * 64 + lane;
-            v[u2] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
+            const uint32_t i = iq + u2 * 64 + lane;
+            const u32x4 x = *reinterpret_cast<const u32x4*>(reg + (i < n ? i : 0u));
+            v[u2] = make_uint4(x.x, x.y, x.z, x.w);
           }
         };
-        uint32_t k = next_region(0), i0 = 0;
-        uint4 cur[RED_UNROLL], nxt[RED_UNROLL];
-        if (k < nreg) load(k, 0, cur);
-        while (k < nreg) {
-          uint32_t k2 = k, i2 = i0 + 64 * RED_UNROLL;
-          if (i2 >= __builtin_amdgcn_readlane(myn, k)) { k2 = next_region(k + 1); i2 = 0; }
-          if (k2 < nreg) load(k2, i2, nxt);
-          if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // else: redone anyway
-            uint32_t h[RED_UNROLL];
-            bool todo[RED_UNROLL];
+        // ping-pong buffers A / B (no register copy between them): the chunk
+        // in one is inserted while the other's loads are in flight
+        auto process = [&](const uint4 (&cur)[RED_UNROLL], uint32_t kq, uint32_t iq) {
+          if (__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;  // redone anyway
+          const uint32_t n = __builtin_amdgcn_readlane(myn, kq);
+          uint32_t h[RED_UNROLL];
+          bool todo[RED_UNROLL];
 #pragma unroll
-            for (int u2 = 0; u2 < RED_UNROLL; u2++) {
-              h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
-              todo[u2] = (cur[u2].x | cur[u2].y) != 0 && in_sub(h[u2], shift0, kk, sub);
-            }
-            if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
-#pragma unroll
-              for (int u2 = 0; u2 < RED_UNROLL; u2++)
-                if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
-#pragma unroll
-              for (int u2 = 0; u2 < RED_UNROLL; u2++)
-                if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
-            } else {
-              asm volatile("" ::"v"(h[0]), "v"(h[1]));
-            }
+          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+            h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
+            todo[u2] = iq + u2 * 64 + lane < n && in_sub(h[u2], shift0, kk, sub);
           }
+          if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
 #pragma unroll
-          for (int u2 = 0; u2 < RED_UNROLL; u2++) cur[u2] = nxt[u2];
-          k = k2;
-          i0 = i2;
+            for (int u2 = 0; u2 < RED_UNROLL; u2++)
+              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+#pragma unroll
+            for (int u2 = 0; u2 < RED_UNROLL; u2++)
+              if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
+          } else {
+            asm volatile("" ::"v"(h[0]), "v"(h[1]));
+          }
+        };
+        auto advance = [&](uint32_t& kq, uint32_t& iq) {  // the chunk after (kq, iq)
+          iq += 64 * RED_UNROLL;
+          if (iq >= __builtin_amdgcn_readlane(myn, kq)) { kq = next_region(kq + 1); iq = 0; }
+        };
+        uint32_t k = next_region(0), i0 = 0;
+        uint4 A[RED_UNROLL], B[RED_UNROLL];
+        if (k < nreg) load(k, 0, A);
+        while (k < nreg) {
+          uint32_t kb = k, ib = i0;
+          advance(kb, ib);
+          load(kb, ib, B);
+          process(A, k, i0);
+          k = kb;
+          i0 = ib;
+          if (k >= nreg) break;
+          uint32_t ka = k, ia = i0;
+          advance(ka, ia);
+          load(ka, ia, A);
+          process(B, k, i0);
+          k = ka;
+          i0 = ia;
         }
       }
       if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
