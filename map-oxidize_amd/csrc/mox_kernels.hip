@@ -2232,6 +2232,7 @@ __device__ __forceinline__ void exscan2_256(uint32_t a, uint32_t b, uint32_t (*w
 // b: scan of the occupied slots), and lpos for the exchange pack.
 extern "C" __global__ __launch_bounds__(256) void k_mat(Work w, Corpus c) {
   __shared__ uint32_t ws[4][2];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[256 * 16 + 32];  // one chunk's key bytes
   if (!table_ok(w)) return;
   const int tid = threadIdx.x;
   const uint32_t U = (uint32_t)w.ctl->n_units;
@@ -2247,14 +2248,32 @@ extern "C" __global__ __launch_bounds__(256) void k_mat(Work w, Corpus c) {
       if (i < n) { k = w.uk[src0 + i]; len = key_len16(k); }
       uint32_t ex, dummy, tot, t2;
       exscan2_256(len, 0, ws, ex, dummy, tot, t2);
+      // the chunk's bytes [boff, boff + tot) are staged in LDS at their offset
+      // from the 16-byte line below boff, then written as aligned 16-byte stores
+      // (bytes at the partial first/last line one by one: neighbours share them)
+      const uint64_t gbase = boff & ~15ull;
+      const uint32_t sh = (uint32_t)(boff - gbase);
       if (i < n) {
         const uint64_t o = boff + ex;
         w.t_counts[dst0 + i] = w.uc[src0 + i];
         w.t_offs[dst0 + i] = o;
-        uint8_t* ob = w.t_bytes + o;
         const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-        for (uint32_t j = 0; j < len; j++) ob[j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
+        for (uint32_t j = 0; j < len; j++) stage[sh + ex + j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
       }
+      __syncthreads();
+      {
+        const uint64_t ge = boff + tot;
+        const uint64_t a0 = (boff + 15) & ~15ull, a1 = ge & ~15ull;  // whole lines [a0, a1)
+        if (a0 < a1) {
+          for (uint64_t q = a0 + 16ull * tid; q < a1; q += 16ull * 256)
+            *reinterpret_cast<uint4*>(w.t_bytes + q) = *reinterpret_cast<const uint4*>(stage + (q - gbase));
+          if (tid < 16 && boff + tid < a0) w.t_bytes[boff + tid] = stage[sh + tid];
+          if (tid >= 16 && tid < 32 && a1 + (tid - 16) < ge) w.t_bytes[a1 + (tid - 16)] = stage[(a1 - gbase) + (tid - 16)];
+        } else if (tid < 32 && boff + tid < ge) {
+          w.t_bytes[boff + tid] = stage[sh + tid];
+        }
+      }
+      __syncthreads();
       boff += tot;
     }
   }
