@@ -342,7 +342,7 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_split_scatter");
   hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);  // workgroup b: partition b, then the work list
   q.step("k_reduce");
-  hipLaunchKernelGGL(k_reduce_small, dim3(4 * e->n_cu), dim3(256), 0, s, w);  // persistent, 4 per CU
+  hipLaunchKernelGGL(k_reduce_small, dim3(8 * e->n_cu), dim3(128), 0, s, w);  // persistent, 8 per CU (SR_THREADS)
   q.step("k_reduce_small");
   q.rec(4);
   hipLaunchKernelGGL(k_unit_uniq_scan, dim3(NB), dim3(1024), 0, s, w);

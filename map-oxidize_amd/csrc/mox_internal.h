@@ -36,12 +36,13 @@ constexpr int RED_THREADS = 1024;
 // High-cardinality split: a partition whose sampled records are
 // mostly distinct is scattered into 2^kk sub-buckets (the next kk hash bits), and
 // every (partition, sub-bucket) "unit" is reduced by its own workgroup.
-constexpr int SUB_BITS_MAX = 11;
+constexpr int SUB_BITS_MAX = 12;
 constexpr int SUB_N = 1 << SUB_BITS_MAX;
 constexpr int U_MAX = NB * SUB_N;           // reduce units
+constexpr int SUB_PER_T = SUB_N / 1024;     // sub-buckets per thread in the 1024-thread unit kernels
 constexpr uint32_t SPLIT_MIN = 6144;        // records below which a partition is never split
-constexpr uint32_t SPLIT_TARGET = 640;      // records per sub-bucket aimed at
-constexpr uint32_t SMALL_CAP = 1024;        // sub-buckets up to this many records: k_reduce_small
+constexpr uint32_t SPLIT_TARGET = 320;      // records per sub-bucket aimed at
+constexpr uint32_t SMALL_CAP = 512;         // sub-buckets up to this many records: k_reduce_small
 constexpr uint32_t SPLIT_SAMPLE = 1024;     // records sampled for the distinct-fraction estimate
 constexpr uint32_t SPLIT_PER_REGION = 4;    // ... the first 4 of every map workgroup's region
 constexpr int LC_BITS = 4096;               // linear-counting bitmap of the sample (4 bits per sample)

@@ -1608,22 +1608,33 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   if (!kk || (w.ctl->overflow & OVF_RERUN)) return;
   const uint32_t nsub = 1u << kk, u0 = w.u_base[b];
   const uint32_t* hist = w.sub_hist + (uint64_t)b * 2 * SUB_N;
-  const uint32_t s0 = 2 * tid, s1 = 2 * tid + 1;  // SUB_N == 2 x blockDim
-  const uint32_t c0 = s0 < nsub ? hist[s0] : 0, c1 = s1 < nsub ? hist[s1] : 0;
-  const uint32_t d0 = s0 < nsub ? hist[SUB_N + s0] : 0, d1 = s1 < nsub ? hist[SUB_N + s1] : 0;
+  // sub-buckets SUB_PER_T t .. SUB_PER_T t + SUB_PER_T - 1 per thread
+  uint32_t c[SUB_PER_T], d[SUB_PER_T], sc = 0, sd = 0;
+#pragma unroll
+  for (int j = 0; j < SUB_PER_T; j++) {
+    const uint32_t sb = SUB_PER_T * tid + j;
+    c[j] = sb < nsub ? hist[sb] : 0;
+    d[j] = sb < nsub ? hist[SUB_N + sb] : 0;
+    sc += c[j];
+    sd += d[j];
+  }
   uint64_t tc, tw;
-  const uint64_t ec = block_exscan(c0 + c1, wsum, tc);
-  const uint64_t ew = block_exscan(d0 + d1, wsum, tw);
+  uint64_t ec = block_exscan(sc, wsum, tc);
+  uint64_t ew = block_exscan(sd, wsum, tw);
   const uint64_t kb = w.sp_off[b], wb = w.spw_off[b], rb = w.rec_off[b];
-  auto unit = [&](uint32_t sb, uint64_t ck, uint32_t nk, uint64_t cwo, uint32_t nwr) {
-    const uint32_t u = u0 + sb;
-    w.udesc[u] = UnitDesc{kb + ck, wb + cwo, rb + ck + cwo, nk, nwr, b, kk};
-    if (nk + nwr > SMALL_CAP) w.big_units[atomicAdd(&w.ctl->n_big, 1ull)] = u;
-    cc[sb] = (uint32_t)ck;
-    cw[sb] = (uint32_t)cwo;
-  };
-  if (s0 < nsub) unit(s0, ec, c0, ew, d0);
-  if (s1 < nsub) unit(s1, ec + c0, c1, ew + d0, d1);
+#pragma unroll
+  for (int j = 0; j < SUB_PER_T; j++) {
+    const uint32_t sb = SUB_PER_T * tid + j;
+    if (sb < nsub) {
+      const uint32_t u = u0 + sb;
+      w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + ec + ew, c[j], d[j], b, kk};
+      if (c[j] + d[j] > SMALL_CAP) w.big_units[atomicAdd(&w.ctl->n_big, 1ull)] = u;
+      cc[sb] = (uint32_t)ec;
+      cw[sb] = (uint32_t)ew;
+    }
+    ec += c[j];
+    ew += d[j];
+  }
   __syncthreads();
   uint4* ok = w.split_k + kb;
   for_partition_cold(w, b, [&](uint4 k) {
@@ -1900,23 +1911,27 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 // insertion sort inside bins, so equal keys are adjacent; run heads are
 // compacted by a block scan and each head sums its run.  Output order (h32,
 // key), as k_reduce.
-constexpr int SR_THREADS = 256;
+constexpr int SR_THREADS = 128;
 constexpr int SR_PER = SMALL_CAP / SR_THREADS;  // records (and sorted positions) per thread
-constexpr int SR_BINS = 1024;
+constexpr int SR_BIN_BITS = 9;
+constexpr int SR_BINS = 1 << SR_BIN_BITS;  // hash bits right below the unit bits
 static_assert(SR_PER * SR_THREADS == (int)SMALL_CAP && SR_BINS == 4 * SR_THREADS, "k_reduce_small geometry");
 
 // LDS-only workgroup barrier: the DS queue drained, no wait on global stores
 // still in flight (a __syncthreads fence would wait for them).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// inclusive wave scan of x (wave64)
+// inclusive wave scan of x (wave64) on the VALU: Hillis-Steele inside each row
+// of 16 lanes (DPP row_shr 1, 2, 4, 8 with zero fill), then row 0 / row 2 totals
+// into the next row (row_bcast:15) and lane 31 into rows 2, 3 (row_bcast:31);
+// no LDS crossbar round trips (a __shfl_up scan is 6 ds_bpermute latencies)
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const uint32_t y = __shfl_up(x, off);
-    if (lane >= off) x += y;
-  }
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
   return x;
 }
 
@@ -1953,7 +1968,7 @@ __device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, boo
 // (~0.5 records per bin), (h32, key) insertion sort inside bins so equal keys
 // are adjacent, run heads compacted by a scan, each head sums its run.  Output
 // order (h32, key), as k_reduce.
-extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work w) {  // 4 per CU: <= 128 VGPRs (no spills: batches of 2)
+extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work w) {  // 8 per CU (4 waves/SIMD): <= 128 VGPRs
   __shared__ uint4 key[SMALL_CAP];
   __shared__ unsigned long long cnt[SMALL_CAP];
   __shared__ uint32_t hh[SMALL_CAP];
@@ -2009,7 +2024,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
         const uint32_t i = tid + j * SR_THREADS;
         if (i < n) {
           const uint32_t h = hash32(in.k[j].x, in.k[j].y, in.k[j].z, in.k[j].w);
-          const uint32_t bn = hbits(h, shift, 10);
+          const uint32_t bn = hbits(h, shift, SR_BIN_BITS);
           key[i] = in.k[j];
           cnt[i] = i < d.in_n ? 1ull : w.split_w[d.win_off + (i - d.in_n)].count;
           hh[i] = h;
@@ -2041,7 +2056,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
 #pragma unroll
       for (int j = 0; j < SR_PER; j++) {
         const uint32_t i = tid + j * SR_THREADS;
-        if (i < n) idx[bin16[hbits(hh[i], shift, 10)] + rk[i]] = (uint16_t)i;
+        if (i < n) idx[bin16[hbits(hh[i], shift, SR_BIN_BITS)] + rk[i]] = (uint16_t)i;
       }
       lds_barrier();
       // final position of each record: its bin start + its (h32, key) rank among
@@ -2053,7 +2068,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
         const uint32_t i = tid + j * SR_THREADS;
         if (i < n) {
           const uint32_t hx = hh[i];
-          const uint32_t bn = hbits(hx, shift, 10);
+          const uint32_t bn = hbits(hx, shift, SR_BIN_BITS);
           const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
           uint32_t r = 0;
           if (hi - lo > 1) {
@@ -2155,14 +2170,25 @@ extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) {
     if (tid == 0) { w.u_uniq_off[u0] = 0; w.u_bytes_off[u0] = 0; w.b_bytes[b] = w.u_bytes[u0]; }
   } else {
     const uint32_t nsub = 1u << kk;
-    const uint32_t s0 = 2 * tid, s1 = s0 + 1;  // SUB_N == 2 x blockDim
-    const uint64_t v0 = s0 < nsub ? w.u_uniq[u0 + s0] : 0, v1 = s1 < nsub ? w.u_uniq[u0 + s1] : 0;
-    const uint64_t y0 = s0 < nsub ? w.u_bytes[u0 + s0] : 0, y1 = s1 < nsub ? w.u_bytes[u0 + s1] : 0;
+    uint64_t v[SUB_PER_T], y[SUB_PER_T], sv = 0, sy = 0;
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; j++) {
+      const uint32_t sb = SUB_PER_T * tid + j;
+      v[j] = sb < nsub ? w.u_uniq[u0 + sb] : 0;
+      y[j] = sb < nsub ? w.u_bytes[u0 + sb] : 0;
+      sv += v[j];
+      sy += y[j];
+    }
     uint64_t tot, btot;
-    const uint64_t ex = block_exscan(v0 + v1, wsum, tot);
-    const uint64_t ey = block_exscan(y0 + y1, wsum, btot);
-    if (s0 < nsub) { w.u_uniq_off[u0 + s0] = ex; w.u_bytes_off[u0 + s0] = ey; }
-    if (s1 < nsub) { w.u_uniq_off[u0 + s1] = ex + v0; w.u_bytes_off[u0 + s1] = ey + y0; }
+    uint64_t ex = block_exscan(sv, wsum, tot);
+    uint64_t ey = block_exscan(sy, wsum, btot);
+#pragma unroll
+    for (int j = 0; j < SUB_PER_T; j++) {
+      const uint32_t sb = SUB_PER_T * tid + j;
+      if (sb < nsub) { w.u_uniq_off[u0 + sb] = ex; w.u_bytes_off[u0 + sb] = ey; }
+      ex += v[j];
+      ey += y[j];
+    }
     if (tid == 0) { w.b_uniq[b] = tot; w.b_bytes[b] = btot; }
   }
   // long-table slice b
