@@ -1976,6 +1976,8 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
   __shared__ uint16_t idx[SMALL_CAP];     // records grouped by bin
   __shared__ uint16_t idx2[SMALL_CAP];    // records in (h32, key) order
   __shared__ uint32_t bins[SR_BINS / 2];  // u16 pairs: counts, then exclusive starts
+  __shared__ uint8_t mixed[SR_BINS];      // bin holds more than one distinct key
+  __shared__ uint16_t hp[SMALL_CAP + 1];  // sorted position of the o-th run head
   __shared__ uint32_t wsa[SR_THREADS / 64], wsb[SR_THREADS / 64];
   __shared__ uint32_t sbytes;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1989,6 +1991,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
   if (tid == 0) { dring[0] = load_desc(w, u, U); dring[1] = load_desc(w, u + G, U); sbytes = 0; }
   bins[tid] = 0;
   bins[tid + SR_THREADS] = 0;
+  for (int i = tid; i < SR_BINS; i += SR_THREADS) mixed[i] = 0;
   lds_barrier();
   SmallIn in;
   {
@@ -2059,6 +2062,22 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
         if (i < n) idx[bin16[hbits(hh[i], shift, SR_BIN_BITS)] + rk[i]] = (uint16_t)i;
       }
       lds_barrier();
+      // a bin is "mixed" when a member differs from its first member; in the
+      // others (one key, possibly repeated ~70 times in C4) the arrival rank rk
+      // is already a valid order
+#pragma unroll
+      for (int j = 0; j < SR_PER; j++) {
+        const uint32_t i = tid + j * SR_THREADS;
+        if (i < n) {
+          const uint32_t bn = hbits(hh[i], shift, SR_BIN_BITS);
+          const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
+          if (hi - lo > 1) {
+            const uint32_t f = idx[lo];
+            if (f != i && (hh[f] != hh[i] || !key_eq16(key[f], key[i]))) mixed[bn] = 1;
+          }
+        }
+      }
+      lds_barrier();
       // final position of each record: its bin start + its (h32, key) rank among
       // the bin's records, ties between equal keys broken by record index (they
       // are summed, so their order is immaterial).  O(bin size) per record, so a
@@ -2071,7 +2090,9 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
           const uint32_t bn = hbits(hx, shift, SR_BIN_BITS);
           const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
           uint32_t r = 0;
-          if (hi - lo > 1) {
+          if (hi - lo > 1 && !mixed[bn]) {
+            r = rk[i];
+          } else if (hi - lo > 1) {
             const uint4 kx = key[i];
             const uint64_t x0 = ((uint64_t)kx.y << 32) | kx.x, x1 = ((uint64_t)kx.w << 32) | kx.z;
             // batches of 2 with branch-free bodies: the LDS reads of a batch are
@@ -2098,8 +2119,9 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
       SR_MARK(1);
       lds_barrier();
       SR_MARK(2);
-      bins[tid] = 0;  // bin starts are dead after the sort: zero for the next unit
+      bins[tid] = 0;  // bin starts and flags are dead after the sort: zero for the next unit
       bins[tid + SR_THREADS] = 0;
+      for (int i = tid; i < SR_BINS; i += SR_THREADS) mixed[i] = 0;
       // run heads at sorted positions 4t..4t+3 -> output index by scan
       uint32_t hm = 0, nh = 0;
 #pragma unroll
@@ -2112,6 +2134,17 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
       lds_barrier();
       uint32_t o = incl - nh, nu = 0;
       for (int k = 0; k < SR_THREADS / 64; k++) { if (k < wv) o += wsb[k]; nu += wsb[k]; }
+      // run lengths from the next head's position (all counts are 1 in a unit
+      // without weighted records); units with weighted records sum their runs
+      const bool ones = d.win_n == 0;
+      if (ones) {
+        uint32_t oo = o;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if ((hm >> j) & 1u) hp[oo++] = (uint16_t)(4 * tid + j);
+        if (tid == 0) hp[nu] = (uint16_t)n;
+        lds_barrier();
+      }
       uint32_t lb = 0;
 #pragma unroll 1
       for (int j = 0; j < 4; j++) {
@@ -2119,8 +2152,9 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
         const uint32_t p = 4 * tid + j;
         const uint4 k = key[idx2[p]];
         unsigned long long c = cnt[idx2[p]];
+        if (ones) c = (unsigned long long)(hp[o + 1] - p);
         // the run of equal keys after p, in batches of 2 (reads issued together)
-        for (uint32_t q0 = p + 1; q0 < n; q0 += 2) {
+        else for (uint32_t q0 = p + 1; q0 < n; q0 += 2) {
           uint32_t y[2];
 #pragma unroll
           for (int t = 0; t < 2; t++) y[t] = idx2[q0 + t < n ? q0 + t : p];
