@@ -170,6 +170,9 @@ __device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint
     if (cur == h) {
       unsigned long long r = atomicAdd(&s->ref, 0ull);
       if (r == 0) continue;  // claimant still publishing: retry this slot
+      // acquire: the claimant's arena bytes (written before its release fence,
+      // possibly from another XCD's L2) must be seen before they are compared
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);
       unsigned long long l = atomicAdd(&s->len, 0ull);
       if (l == len && long_equal(base, w.arena, r - 1, ref, len)) {
         atomicAdd(&s->count, (unsigned long long)cnt);
