@@ -52,6 +52,8 @@ extern "C" {
 #define MOX_F_NO_DICT 0x1u      /* disable the hot-word dictionary (all tokens take the cold path) */
 #define MOX_F_SORT_BYTES 0x2u   /* fetch returns words sorted bytewise (Rust String Ord) instead of hash order */
 #define MOX_F_TIMING 0x4u       /* record per-kernel HIP-event timings into mox_stats */
+#define MOX_F_TIMING_MAP 0x8u   /* HIP events around the map kernel only (ms_map): each event record idles
+                                   the stream ~5.6 us, so timed loops bracket just the dominant kernel */
 
 typedef struct mox_config {
   int device;             /* HIP device ordinal; -1 = current device */
@@ -106,6 +108,8 @@ const char* mox_last_error(void);
 int mox_abi_version(void);
 
 int mox_engine_create(const mox_config* cfg, mox_engine** out);
+/* Replace the engine's MOX_F_* flags (e.g. switch timing modes between runs). */
+int mox_set_flags(mox_engine* e, uint32_t flags);
 void mox_engine_destroy(mox_engine* e);
 
 /* ---- drop-in for main.rs:16-22 ---- */

@@ -310,9 +310,9 @@ float ev_ms(mox_engine* e, int a, int b) {
 struct Seq {
   mox_engine* e;
   hipStream_t s;
-  bool timing, sync_each;
-  void rec(int i) const {
-    if (timing) (void)hipEventRecord(e->ev[i], s);
+  bool timing, sync_each, map_only;
+  void rec(int i) const {  // map_only: events 1 and 2 (around k_map) only
+    if (timing || (map_only && (i == 1 || i == 2))) (void)hipEventRecord(e->ev[i], s);
   }
   void step(const char* name) const {
     if (!sync_each) return;
@@ -321,7 +321,10 @@ struct Seq {
   }
 };
 
-Seq seq_of(mox_engine* e) { return Seq{e, e->stream, (e->flags & MOX_F_TIMING) != 0, e->sync_each}; }
+Seq seq_of(mox_engine* e) {
+  const bool full = (e->flags & MOX_F_TIMING) != 0;
+  return Seq{e, e->stream, full, e->sync_each, !full && (e->flags & MOX_F_TIMING_MAP) != 0};
+}
 
 // Stages 4-5 of a pass (shared by the corpus pass and the exchange pass):
 // shuffle directory + bucket reduce, then the dense table.
@@ -359,6 +362,10 @@ int finish_pass(mox_engine* e, const Seq& q) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(e->h_ctl, e->w.ctl, sizeof(Ctl), hipMemcpyDeviceToHost, e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (q.map_only && !q.sync_each) {
+    e->stats.ms_dict = e->stats.ms_lanes = e->stats.ms_reduce = e->stats.ms_finalize = e->stats.ms_run = 0;
+    e->stats.ms_map = ev_ms(e, 1, 2);
+  }
   if (q.timing) {
     e->stats.ms_dict = ev_ms(e, 0, 1);
     e->stats.ms_map = ev_ms(e, 1, 2);
@@ -794,6 +801,12 @@ extern "C" {
 
 const char* mox_last_error(void) { return g_err.c_str(); }
 int mox_abi_version(void) { return MOX_ABI_VERSION; }
+
+int mox_set_flags(mox_engine* e, uint32_t flags) {
+  if (!e) return fail(MOX_EINVAL, "NULL engine");
+  e->flags = flags;
+  return MOX_OK;
+}
 
 int mox_engine_create(const mox_config* cfg, mox_engine** out) {
   if (!out) return fail(MOX_EINVAL, "out is NULL");

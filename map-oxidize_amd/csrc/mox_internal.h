@@ -180,7 +180,7 @@ struct Work {  // device buffers of one engine
   Ctl* ctl;
   // dictionary
   WRec* cand;                     // GC_SLOTS candidates (key claimed with claim16, count)
-  uint32_t* dict_hist;            // [256] candidate count histogram, [256] picked words
+  uint32_t* dict_hist;            // [256] candidate count histogram, [256] picked words (classes >= T), [257] class T - 1 words
   WRec* dict_list;                // DICT_MAX_WORDS picked words
   uint32_t* dict_tag;             // DICT_SLOTS key hashes (0 = empty), bucket b = slots 4b..4b+3
   uint4* dict_key;                // DICT_SLOTS lowered 16-byte keys

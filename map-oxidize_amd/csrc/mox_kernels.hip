@@ -999,7 +999,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_hist(Work w) {
 }
 
 extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t max_words) {
-  __shared__ uint32_t T, h[256];
+  __shared__ uint32_t T, ST, h[256];
   if (threadIdx.x < 256) h[threadIdx.x] = w.dict_hist[threadIdx.x];
   __syncthreads();
   // T = smallest count class cc >= 2 whose suffix sum S(cc) = sum_{c >= cc} h[c]
@@ -1011,10 +1011,11 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
     const int cc = 255 - (int)threadIdx.x;
     const uint64_t x = threadIdx.x < 256 ? h[cc] : 0;
     const uint64_t ex = block_exscan(x, wsum, tot);
-    if (threadIdx.x == 0) T = 256;
+    if (threadIdx.x == 0) { T = 256; ST = 0; }
     __syncthreads();
     if (threadIdx.x < 254 && ex + x <= max_words) atomicMin(&T, (uint32_t)cc);  // cc in [2, 255]
     __syncthreads();
+    if (threadIdx.x < 256 && cc == (int)T) ST = (uint32_t)(ex + x);  // S(T): words picked whole
     if (threadIdx.x == 0) {
       if (T > 255) T = 256;  // nothing fits: pick nothing
       if (blockIdx.x == 0) w.ctl->dict_thresh = T;
@@ -1023,21 +1024,40 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
   }
   // one slot per thread (grid = GC_SLOTS / 1024): rank picked entries in the
   // workgroup, reserve the workgroup's range with one global atomic
-  __shared__ uint32_t wn[16], base;
-  const uint32_t t = T;
+  // Classes >= T fill dict_list[0, S(T)) (they fit whole).  The room left
+  // (max_words - S(T)) goes to class T - 1 (if >= 2) at [S(T), ...), first
+  // come first served: its words are equally hot by the sample, and k_dict_build
+  // places them last.
+  __shared__ uint32_t wn[2][16], base[2];
+  const uint32_t t = T, t1 = T - 1;
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const WRec r = w.cand[i];
-  const bool pick = r.count >= t && r.w0 != 0 && r.w1 != 0;
-  const uint64_t bm = __ballot(pick);
+  const bool real = r.w0 != 0 && r.w1 != 0;
+  const bool pick = real && r.count >= t;
+  const bool fill = real && t1 >= 2 && t1 < 255 && r.count == t1;
+  const uint64_t bm = __ballot(pick), bf = __ballot(fill);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (lane == 0) wn[wv] = (uint32_t)__popcll(bm);
+  if (lane == 0) { wn[0][wv] = (uint32_t)__popcll(bm); wn[1][wv] = (uint32_t)__popcll(bf); }
   __syncthreads();
-  uint32_t pre = (uint32_t)__popcll(bm & ((1ull << lane) - 1ull)), tot = 0;
-  for (int k = 0; k < 16; k++) { if (k < wv) pre += wn[k]; tot += wn[k]; }
-  if (threadIdx.x == 0) base = tot ? atomicAdd(&w.dict_hist[256], tot) : 0u;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  uint32_t pre = (uint32_t)__popcll(bm & lt), pref = (uint32_t)__popcll(bf & lt), tot = 0, totf = 0;
+  for (int k = 0; k < 16; k++) {
+    if (k < wv) { pre += wn[0][k]; pref += wn[1][k]; }
+    tot += wn[0][k];
+    totf += wn[1][k];
+  }
+  if (threadIdx.x == 0) {
+    base[0] = tot ? atomicAdd(&w.dict_hist[256], tot) : 0u;
+    base[1] = totf ? atomicAdd(&w.dict_hist[257], totf) : 0u;
+  }
   __syncthreads();
-  const uint32_t o = base + pre;
-  if (pick && o < max_words) w.dict_list[o] = WRec{r.w0, r.w1 & ~(1ull << 63), r.count};
+  if (pick) {
+    const uint32_t o = base[0] + pre;
+    if (o < max_words) w.dict_list[o] = WRec{r.w0, r.w1 & ~(1ull << 63), r.count};
+  } else if (fill) {
+    const uint32_t o = ST + base[1] + pref;
+    if (o < max_words) w.dict_list[o] = WRec{r.w0, r.w1 & ~(1ull << 63), r.count};
+  }
 }
 
 extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
@@ -1051,7 +1071,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
   for (int i = tid; i < DICT_SLOTS; i += 1024) { ltag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
   if (tid < 32) { ccnt[tid] = 0; cfill[tid] = 0; }
   if (tid == 0) nsel = 0;
-  uint32_t n = w.dict_hist[256];
+  uint32_t n = w.dict_hist[256] + w.dict_hist[257];  // classes >= T, then the partial class T - 1
   if (n > max_words) n = max_words;
   __syncthreads();
   for (uint32_t i = tid; i < n; i += 1024) {

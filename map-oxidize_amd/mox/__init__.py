@@ -30,6 +30,7 @@ MOX_EHALO = -8
 
 MOX_F_NO_DICT = 0x1
 MOX_F_TIMING = 0x4
+MOX_F_TIMING_MAP = 0x8  # HIP events around the map kernel only
 
 UNIQUE_ID_BYTES = 128
 
@@ -118,6 +119,7 @@ def lib():
             "mox_abi_version": ([], I),
             "mox_engine_create": ([P(Config), P(VP)], I),
             "mox_engine_destroy": ([VP], None),
+            "mox_set_flags": ([VP, ctypes.c_uint32], I),
             "mox_count": ([VP, VP, sz, P(P(_Table))], I),
             "mox_count_file": ([VP, ctypes.c_char_p, P(P(_Table))], I),
             "mox_table_free": ([P(_Table)], None),
@@ -216,6 +218,9 @@ class Engine:
         h = ctypes.c_void_p()
         _check(lib().mox_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+
+    def set_flags(self, flags):
+        _check(lib().mox_set_flags(self._h, flags))
 
     # -- drop-in for main.rs:16-22
     def count(self, data):
