@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dict", action="store_true")
+    ap.add_argument("--sample-pieces", type=int, default=0, help="dictionary sample pieces (0 = engine default)")
     ap.add_argument("--xport", default="rccl", choices=["rccl", "host"],
                     help="exchange transport for N > 1 (host: gloo-staged, for ranks sharing one GPU)")
     ap.add_argument("--device", type=int, default=-1, help="override the GPU (default LOCAL_RANK)")
@@ -116,7 +117,7 @@ def main():
     # timed steps: HIP events around k_map only (each event record idles the
     # stream ~5.6 us); one diagnostic step after the timed region has them all
     eng = mox.Engine(device=local if a.device < 0 else a.device, flags=base_flags | mox.MOX_F_TIMING_MAP,
-                     reserve_bytes=per_rank)
+                     sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
     host = corpus.fill(kind, seed, lo, hi - lo)
     d_buf = eng.alloc(hi - lo)
     eng.h2d(d_buf, host)

@@ -970,9 +970,24 @@ extern "C" __global__ __launch_bounds__(256) void k_sample(Corpus c, Work w, uin
     }
   }
   __syncthreads();
+  // compact the local words first, so that each thread runs at most a couple of
+  // (dependent) global claim chains instead of one per slot it scans
+  __shared__ uint16_t lw[SAMPLE_SLOTS];
+  __shared__ uint32_t nlw;
+  if (tid == 0) nlw = 0;
+  __syncthreads();
   for (int i = tid; i < SAMPLE_SLOTS; i += 256) {
+    const bool used = scnt[i] != 0 && sk0[i] != 0 && sk1[i] != 0;
+    const uint64_t bm = __ballot(used);
+    uint32_t b0 = 0;
+    if ((tid & 63) == 0 && bm) b0 = atomicAdd(&nlw, (uint32_t)__popcll(bm));
+    b0 = __shfl(b0, 0);
+    if (used) lw[b0 + (uint32_t)__popcll(bm & ((1ull << (tid & 63)) - 1ull))] = (uint16_t)i;
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < nlw; j += 256) {
+    const uint32_t i = lw[j];
     const uint32_t n = scnt[i];
-    if (n == 0 || sk0[i] == 0 || sk1[i] == 0) continue;
     const uint64_t w0 = sk0[i], w1 = sk1[i] & ~(1ull << 63);
     uint32_t g = key_hash(w0, w1) & (GC_SLOTS - 1);
     for (int pr = 0; pr < 16; pr++) {  // bounded: a full table (high-cardinality input) just drops words
