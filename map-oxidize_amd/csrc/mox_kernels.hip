@@ -149,7 +149,8 @@ __device__ bool long_equal(const uint8_t* base, const uint8_t* arena, uint64_t r
 }
 // Exact insert into the long-word table; every access is an atomic (memory-side,
 // coherent across XCDs).  Keys: (hash, len) + byte compare on hash equality.
-__device__ void long_insert(const Work& w, const uint8_t* base, uint64_t h, uint64_t ref, uint64_t len, uint64_t cnt) {
+template <class W>  // Work, or the kernarg-segment Work of k_map's rare paths
+__device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_t ref, uint64_t len, uint64_t cnt) {
   h |= 1;
   uint64_t mask = w.long_cap - 1, slot = h & mask;
   uint32_t spins = 0;
@@ -227,12 +228,24 @@ struct MapLds {
   uint4* masktab;   // [17]: byte masks keeping the first len bytes of a 16-byte key
 };
 
+typedef const __attribute__((address_space(4))) Work* KWork;  // constant (kernarg) address space: scalar loads
 struct MapCtx {
   Corpus c;
-  Work w;
+  Work w;            // hot path: cold, cold_cap only
+  KWork wk;          // the kernel argument itself (kernarg segment), for the rare paths
   MapLds s;
   uint32_t dict_n;
 };
+// Work fields of the rare paths (spills, Unicode lane, long words, error
+// flags), loaded where they are used: the opaque pointer keeps the compiler from
+// hoisting these loads to the kernel entry, where ~20 more SGPRs would stay live
+// across the row loop and spill into VGPR lanes (v_readlane in the hot path).
+__device__ __forceinline__ KWork rare_ptr(const MapCtx& m) {
+  KWork p = m.wk;
+  asm volatile("" : "+s"(p));
+  return p;
+}
+#define rare(m) (*rare_ptr(m))
 
 __device__ __forceinline__ bool key_eq(uint4 k, uint64_t w0, uint64_t w1) {
   return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && k.w == (uint32_t)(w1 >> 32);
@@ -275,11 +288,11 @@ __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_
 // hash partition (the shuffle write), no global atomics.
 __device__ __forceinline__ void cold_spill(const MapCtx& m, uint4 key) {
   const uint32_t sp = atomicAdd(&m.s.misc[0], 1u);
-  if (sp < m.w.spill_cap) {
-    m.w.spill[(uint64_t)blockIdx.x * m.w.spill_cap + sp] = key;
+  if (sp < rare(m).spill_cap) {
+    rare(m).spill[(uint64_t)blockIdx.x * rare(m).spill_cap + sp] = key;
     return;
   }
-  atomicOr(&m.w.ctl->overflow, OVF_POOL);
+  atomicOr(&rare(m).ctl->overflow, OVF_POOL);
 }
 __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
   const uint32_t b = bucket_of(h);
@@ -301,7 +314,7 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
   bool nonascii = false, nul = false;
   for (;;) {
     if (q >= c.hi) {
-      if (!c.at_end) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - c.lo));
+      if (!c.at_end) atomicMin(&rare(m).ctl->halo_err, (unsigned long long)(p - c.lo));
       break;
     }
     const uint8_t b = c.base[q];
@@ -317,9 +330,9 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
   }
   const uint64_t len = q - p;
   if (nonascii) {
-    const unsigned long long i = atomicAdd(&m.w.ctl->u_n, 1ull);
-    if (i < m.w.u_cap) m.w.u[i] = URec{p, len};
-    else atomicOr(&m.w.ctl->overflow, OVF_U);
+    const unsigned long long i = atomicAdd(&rare(m).ctl->u_n, 1ull);
+    if (i < rare(m).u_cap) rare(m).u[i] = URec{p, len};
+    else atomicOr(&rare(m).ctl->overflow, OVF_U);
     return;
   }
   if (len <= 16 && !nul) {
@@ -333,8 +346,8 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
   }
   uint64_t h = FNV0;
   for (uint64_t i = 0; i < len; i++) h = fnv_step(h, ascii_lower(c.base[p + i]));
-  atomicAdd(&m.w.ctl->long_n, 1ull);
-  long_insert(m.w, c.base, h, p, len, 1);
+  atomicAdd(&rare(m).ctl->long_n, 1ull);
+  long_insert(rare(m), c.base, h, p, len, 1);
 }
 
 // Clamped aligned 16-byte load: the block always overlaps [lo, hi), so it never
@@ -405,8 +418,8 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
     const uint64_t p = p0 + j;
     if (p < m.c.own_lo || p >= m.c.own_hi) continue;
     const int v = utf8_check(m.c, p);
-    if (v == 1) atomicMin(&m.w.ctl->err_utf8, (unsigned long long)(p - m.c.lo));
-    else if (v == 2) atomicMin(&m.w.ctl->halo_err, (unsigned long long)(p - m.c.lo));
+    if (v == 1) atomicMin(&rare(m).ctl->err_utf8, (unsigned long long)(p - m.c.lo));
+    else if (v == 2) atomicMin(&rare(m).ctl->halo_err, (unsigned long long)(p - m.c.lo));
     if (in_ws(m.c, p)) continue;
     const bool start = (p == m.c.lo) ? true : in_ws(m.c, p - 1);
     if (start && (m.c.base[p] & 0xC0) != 0x80) st |= 1u << j;
@@ -682,6 +695,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   MapCtx m;
   m.c = c;
   m.w = w;
+  // w's copy in the kernarg segment (k_map(Corpus, Work, ...): natural
+  // alignment after c); taking &w instead would copy it to scratch
+  m.wk = (KWork)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
+                 ((sizeof(Corpus) + alignof(Work) - 1) & ~(alignof(Work) - 1)));
   uint8_t* sp = smem;
   m.s.dtag4 = (uint4*)sp; sp += DICT_SLOTS * 4;
   m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
