@@ -146,7 +146,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
-        map_ms.append(eng.stats()["ms_map"])
+        map_ms.append(eng.ms_map())
     eng.synchronize()
     if dist:
         dist.barrier()

@@ -251,6 +251,14 @@ class Engine:
         _check(lib().mox_get_stats(self._h, ctypes.byref(s)))
         return s.as_dict()
 
+    def ms_map(self):
+        """Map-kernel milliseconds of the last pass (cheap: for timed loops)."""
+        if not hasattr(self, "_st"):
+            self._st = Stats()
+            self._st_ref = ctypes.byref(self._st)
+        _check(lib().mox_get_stats(self._h, self._st_ref))
+        return self._st.ms_map
+
     def alloc(self, nbytes):
         p = ctypes.c_void_p()
         _check(lib().mox_device_alloc(self._h, nbytes, ctypes.byref(p)))
