@@ -613,6 +613,14 @@ struct Transport {
   virtual int counts(const XCnt* d_send, XCnt* d_recv, XCnt* h_send, XCnt* h_recv) = 0;
   virtual int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
                         const uint64_t* rlen) = 0;
+  // two independent all-to-alls (short records, long-word blobs); a transport
+  // may move both in one round
+  virtual int alltoallv_pair(const uint8_t* send_a, const uint64_t* soff_a, const uint64_t* slen_a, uint8_t* recv_a,
+                             const uint64_t* roff_a, const uint64_t* rlen_a, const uint8_t* send_b, const uint64_t* soff_b,
+                             const uint64_t* slen_b, uint8_t* recv_b, const uint64_t* roff_b, const uint64_t* rlen_b) {
+    int rc = alltoallv(send_a, soff_a, slen_a, recv_a, roff_a, rlen_a);
+    return rc ? rc : alltoallv(send_b, soff_b, slen_b, recv_b, roff_b, rlen_b);
+  }
 };
 
 struct RcclTransport : Transport {
@@ -641,6 +649,26 @@ struct RcclTransport : Transport {
       if (p == me) continue;
       if (slen[p]) RCCLCHK(ncclSend(send + soff[p], slen[p], ncclUint8, p, e->comm, e->stream));
       if (rlen[p]) RCCLCHK(ncclRecv(recv + roff[p], rlen[p], ncclUint8, p, e->comm, e->stream));
+    }
+    RCCLCHK(ncclGroupEnd());
+    return MOX_OK;
+  }
+  // both payloads inside ONE ncclGroupStart/End: one RCCL launch and one round
+  // of peer handshakes per exchange instead of two
+  int alltoallv_pair(const uint8_t* send_a, const uint64_t* soff_a, const uint64_t* slen_a, uint8_t* recv_a,
+                     const uint64_t* roff_a, const uint64_t* rlen_a, const uint8_t* send_b, const uint64_t* soff_b,
+                     const uint64_t* slen_b, uint8_t* recv_b, const uint64_t* roff_b, const uint64_t* rlen_b) override {
+    const int P = e->nranks, me = e->rank;
+    if (slen_a[me]) HIPCHK(hipMemcpyAsync(recv_a + roff_a[me], send_a + soff_a[me], slen_a[me], hipMemcpyDeviceToDevice, e->stream));
+    if (slen_b[me]) HIPCHK(hipMemcpyAsync(recv_b + roff_b[me], send_b + soff_b[me], slen_b[me], hipMemcpyDeviceToDevice, e->stream));
+    if (P == 1) return MOX_OK;
+    RCCLCHK(ncclGroupStart());
+    for (int p = 0; p < P; p++) {
+      if (p == me) continue;
+      if (slen_a[p]) RCCLCHK(ncclSend(send_a + soff_a[p], slen_a[p], ncclUint8, p, e->comm, e->stream));
+      if (rlen_a[p]) RCCLCHK(ncclRecv(recv_a + roff_a[p], rlen_a[p], ncclUint8, p, e->comm, e->stream));
+      if (slen_b[p]) RCCLCHK(ncclSend(send_b + soff_b[p], slen_b[p], ncclUint8, p, e->comm, e->stream));
+      if (rlen_b[p]) RCCLCHK(ncclRecv(recv_b + roff_b[p], rlen_b[p], ncclUint8, p, e->comm, e->stream));
     }
     RCCLCHK(ncclGroupEnd());
     return MOX_OK;
@@ -757,10 +785,9 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   HIPCHK(hipGetLastError());
   (void)me;
   // 3. payload all-to-alls
-  if ((rc = T.alltoallv((const uint8_t*)e->x_send_short.p, s_short_off, s_short_len, (uint8_t*)e->x_recv_short.p, r_short_off,
-                        r_short_len)))
-    return rc;
-  if ((rc = T.alltoallv((const uint8_t*)e->x_send_blob.p, s_blob_off, s_blob_len, (uint8_t*)e->x_recv_blob.p, r_blob_off, r_blob_len)))
+  if ((rc = T.alltoallv_pair((const uint8_t*)e->x_send_short.p, s_short_off, s_short_len, (uint8_t*)e->x_recv_short.p,
+                             r_short_off, r_short_len, (const uint8_t*)e->x_send_blob.p, s_blob_off, s_blob_len,
+                             (uint8_t*)e->x_recv_blob.p, r_blob_off, r_blob_len)))
     return rc;
   // 4. reduce-only pass over the received partials (the local table is no
   //    longer needed: buffers may be regrown)
