@@ -59,6 +59,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dict", action="store_true")
     ap.add_argument("--sample-pieces", type=int, default=0, help="dictionary sample pieces (0 = engine default)")
+    ap.add_argument("--sync-passes", action="store_true", help="N = 1: synchronous passes (no async enqueue)")
     ap.add_argument("--xport", default="rccl", choices=["rccl", "host"],
                     help="exchange transport for N > 1 (host: gloo-staged, for ranks sharing one GPU)")
     ap.add_argument("--device", type=int, default=-1, help="override the GPU (default LOCAL_RANK)")
@@ -129,7 +130,17 @@ def main():
         eng.comm_init(world, rank, obj[0])
     a2a = mdist.gloo_alltoallv() if world > 1 and a.xport == "host" else None
 
-    def step():
+    # N = 1: passes are enqueued asynchronously (mox_run_range_async): each call
+    # enqueues its pass, then completes (checks) the previous one, so the GPU
+    # runs the passes back to back with no host round trip between them.
+    # N > 1: the exchange needs the local result on the host side, so passes
+    # run synchronously.
+    use_async = world == 1 and not a.sync_passes
+
+    def step(sync=False):
+        if use_async and not sync:
+            eng.run_range_async(d_buf, hi - lo, own_b, own_e, at_end)
+            return
         eng.run_range(d_buf, hi - lo, own_b, own_e, at_end)
         if world > 1:
             if a2a:
@@ -139,20 +150,23 @@ def main():
 
     for _ in range(a.warmup):
         step()
+    eng.synchronize()  # completes (and checks) every queued pass
     if dist:
         dist.barrier()
-    eng.synchronize()
     map_ms = []
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
         step()
-        map_ms.append(eng.ms_map())
+        if not use_async or i > 0:  # async: the call completed the previous pass
+            map_ms.append(eng.ms_map())
     eng.synchronize()
+    if use_async:
+        map_ms.append(eng.ms_map())  # the last pass, completed by synchronize
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     eng.set_flags(base_flags | mox.MOX_F_TIMING)  # untimed diagnostic step: per-phase events
-    step()
+    step(sync=True)
     eng.synchronize()
     phases = [eng.stats()]
     if dist:
@@ -219,6 +233,7 @@ def main():
                 "avg_launch_ms": round(map_avg, 4),
             },
             "phases_note": "phases_ms: one untimed diagnostic step with per-phase HIP events",
+            "pass_mode": "async (mox_run_range_async: back-to-back passes, each completed and checked)" if use_async else "sync",
             "phases_ms": {k: round(statistics.mean(p[k] for p in phases), 4)
                           for k in ("ms_run", "ms_dict", "ms_map", "ms_lanes", "ms_reduce", "ms_finalize",
                                     "ms_exchange")},

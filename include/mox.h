@@ -130,6 +130,16 @@ int mox_run_device(mox_engine* e, const void* d_text, size_t len);
  * end is an error (MOX_EHALO). */
 int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
                   int at_corpus_end);
+/* Asynchronous mox_run_range: enqueues the pass and returns; the pass queued
+ * by the previous async call is completed (checked, and re-run synchronously
+ * if a buffer overflowed) after this one is enqueued, so back-to-back passes
+ * leave no host round trip between them on the GPU.  A pass's error is
+ * returned by the call that completes it: the next mox_run_range_async, or
+ * mox_run_wait.  Every other entry point completes pending passes first. */
+int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
+                        int at_corpus_end);
+/* Complete every pending async pass; the last one's table is the result. */
+int mox_run_wait(mox_engine* e);
 /* Copy the table of the last run (or of the last exchange) to the host. */
 int mox_fetch_table(mox_engine* e, mox_table** out);
 int mox_get_stats(const mox_engine* e, mox_stats* out);

@@ -32,6 +32,7 @@ using namespace mox;
 extern "C" {
 __global__ void k_map(Corpus c, Work w, uint64_t ntiles);
 __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags);
+__global__ void k_ctl_out(const Ctl* src, Ctl* dst);
 __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
 __global__ void k_dict_hist(Work w);
 __global__ void k_dict_pick(Work w, uint32_t max_words);
@@ -115,6 +116,16 @@ struct mox_engine {
   Corpus last_corpus{};
   mox_stats stats{};
   hipEvent_t ev[12]{};
+  // mox_run_range_async: two pass slots (the newest pass is enqueued before the
+  // previous one is completed, so the GPU runs them back to back)
+  struct AsyncSlot {
+    bool pending = false;
+    bool rerun = false;  // a pass before it was re-run synchronously: its result is stale
+    Corpus c{};
+    Ctl* h_ctl = nullptr;                  // pinned copy of this pass's control block
+    hipEvent_t ev_map0 = nullptr, ev_map1 = nullptr, ev_done = nullptr;
+  } aslot[2];
+  int anext = 0;
   // multi-GPU
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
@@ -311,7 +322,12 @@ struct Seq {
   mox_engine* e;
   hipStream_t s;
   bool timing, sync_each, map_only;
+  hipEvent_t map_ev[2] = {nullptr, nullptr};  // async passes: their own map events
   void rec(int i) const {  // map_only: events 1 and 2 (around k_map) only
+    if ((i == 1 || i == 2) && map_ev[0]) {
+      if (timing || map_only) (void)hipEventRecord(map_ev[i - 1], s);
+      return;
+    }
     if (timing || (map_only && (i == 1 || i == 2))) (void)hipEventRecord(e->ev[i], s);
   }
   void step(const char* name) const {
@@ -379,10 +395,9 @@ int finish_pass(mox_engine* e, const Seq& q) {
 
 // One attempt of the whole device pipeline.  Returns MOX_OK after the control
 // block has been read back into e->h_ctl (caller inspects overflow / errors).
-int pipeline_once(mox_engine* e, const Corpus& c) {
+void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q) {
   Work& w = e->w;
   hipStream_t s = e->stream;
-  const Seq q = seq_of(e);
   q.rec(0);
   const bool dict = !(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo;
   // control block, partition counters, long table, sampling buffers: one launch
@@ -415,6 +430,11 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   q.rec(3);
   // 4-5. shuffle directory + bucket reduce, table
   launch_reduce_tail(e, c, q);
+}
+
+int pipeline_once(mox_engine* e, const Corpus& c) {
+  const Seq q = seq_of(e);
+  enqueue_pass(e, c, q);
   return finish_pass(e, q);
 }
 
@@ -442,6 +462,8 @@ Caps grow_for(mox_engine* e, const Ctl& h) {
   if (h.overflow & OVF_TABLE) need.bytes_cap = std::max(need.bytes_cap, need.table_cap * 16);
   return need;
 }
+
+void commit_result(mox_engine* e, const Corpus& c, const Ctl& h);
 
 int run_corpus(mox_engine* e, const Corpus& c) {
   e->have_result = false;
@@ -530,12 +552,19 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     e->stats.retries++;
     if ((rc = ensure_caps(e, need))) return rc;
   }
-  const Ctl& h = *e->h_ctl;
+  commit_result(e, c, *e->h_ctl);
+  return MOX_OK;
+}
+
+// The pass over c finished with control block h (no overflow, no error): its
+// table is the engine's result.
+void commit_result(mox_engine* e, const Corpus& c, const Ctl& h) {
+  if (&h != e->h_ctl) std::memcpy(e->h_ctl, &h, sizeof(Ctl));  // an async pass: fetch reads e->h_ctl
   // spills are correct but slow (atomic scatter): size the regions for the
   // next run of this engine from what this one needed
   // (applied at the start of the next run: the buffers hold this run's table)
   if (h.spill_need) e->next_cold_cap = std::max<uint64_t>(e->next_cold_cap, h.cold_need + h.cold_need / 8 + 16);
-  e->stats.bytes = n;
+  e->stats.bytes = c.own_hi - c.own_lo;
   e->stats.tokens = h.tokens;
   e->stats.uniques = h.n_total;
   e->stats.dict_words = h.dict_n;
@@ -549,7 +578,50 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   e->stats.split_partitions = h.n_split;
   e->last_corpus = c;
   e->have_result = true;
-  return MOX_OK;
+}
+
+// ---- asynchronous passes (mox_run_range_async / mox_run_wait)
+// Completes async slot k: waits for its control block, then either commits its
+// result, or (overflow / stale) re-runs its corpus synchronously with grown
+// buffers.  A synchronous re-run overwrites the device state, so a later
+// pending pass is marked to be re-run as well.
+int complete_async(mox_engine* e, int k) {
+  auto& a = e->aslot[k];
+  if (!a.pending) return MOX_OK;
+  a.pending = false;
+  HIPCHK(hipEventSynchronize(a.ev_done));
+  const Ctl& h = *a.h_ctl;
+  auto& later = e->aslot[k ^ 1];
+  if (!a.rerun) {
+    if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
+    if (h.halo_err != ~0ull)
+      return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
+    if (!h.overflow) {
+      const bool map_only = (e->flags & (MOX_F_TIMING | MOX_F_TIMING_MAP)) != 0;
+      if (map_only) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, a.ev_map0, a.ev_map1) == hipSuccess) e->stats.ms_map = ms;
+      }
+      e->stats.retries = 0;
+      commit_result(e, a.c, h);
+      if (later.pending) e->have_result = false;  // the later pass is overwriting this table
+      return MOX_OK;
+    }
+  }
+  // overflowed or stale: drain, then the synchronous path (retry loop)
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (later.pending) later.rerun = true;
+  int rc = run_corpus(e, a.c);
+  if (later.pending) e->have_result = false;
+  return rc;
+}
+
+int drain_async(mox_engine* e) {
+  // the older pending slot first
+  const int first = e->anext;  // slot written least recently
+  int rc = complete_async(e, first);
+  const int rc2 = complete_async(e, first ^ 1);
+  return rc ? rc : rc2;
 }
 
 // Internal coordinates: c.base is the buffer address rounded down to 16 B,
@@ -727,6 +799,7 @@ int exchange_pass_once(mox_engine* e, uint64_t r_short, uint64_t blob_bytes, con
 }
 
 int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
+  if (int rc = drain_async(e)) return rc;
   if (!e->have_result) return fail(MOX_ESTATE, "no local result: mox_run_range first");
   if (P > MAX_RANKS) return fail(MOX_EINVAL, "at most %d ranks", MAX_RANKS);
   HIPCHK(hipSetDevice(e->device));
@@ -893,6 +966,10 @@ void mox_engine_destroy(mox_engine* e) {
   if (!e) return;
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
+  for (auto& a : e->aslot) {
+    if (a.h_ctl) (void)hipHostFree(a.h_ctl);
+    for (hipEvent_t ev : {a.ev_map0, a.ev_map1, a.ev_done}) if (ev) (void)hipEventDestroy(ev);
+  }
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
   void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
@@ -918,8 +995,56 @@ void mox_engine_destroy(mox_engine* e) {
   delete e;
 }
 
+int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
+                        int at_corpus_end) {
+  if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (!d_buf && buf_len) return fail(MOX_EINVAL, "buffer is NULL");
+  if (own_begin > own_end || own_end > buf_len) return fail(MOX_EINVAL, "bad own range [%zu, %zu) of %zu", own_begin, own_end, buf_len);
+  if (own_begin > 0 && own_begin < 4) return fail(MOX_EINVAL, "own_begin must be 0 (corpus start) or >= 4 (left context)");
+  HIPCHK(hipSetDevice(e->device));
+  const Corpus c = make_corpus(buf_len ? d_buf : (const void*)e->w.ctl, buf_len, own_begin, own_end, at_corpus_end);
+  const int k = e->anext;
+  auto& a = e->aslot[k];
+  if (a.pending) {  // two passes already queued: complete the older one first
+    int rc = complete_async(e, k);
+    if (rc) return rc;
+  }
+  if (!a.h_ctl) {
+    HIPCHK(hipHostMalloc((void**)&a.h_ctl, sizeof(Ctl), hipHostMallocDefault));
+    HIPCHK(hipEventCreate(&a.ev_map0));
+    HIPCHK(hipEventCreate(&a.ev_map1));
+    HIPCHK(hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming));
+  }
+  Caps want = initial_caps(c.own_hi - c.own_lo, e->n_cu);
+  want.cold_cap = std::max<uint64_t>(want.cold_cap, e->next_cold_cap);
+  int rc = ensure_caps(e, want);  // a regrow synchronises the device: pending passes finish first
+  if (rc) return rc;
+  e->have_result = false;
+  Seq q = seq_of(e);
+  q.map_ev[0] = a.ev_map0;
+  q.map_ev[1] = a.ev_map1;
+  enqueue_pass(e, c, q);
+  HIPCHK(hipGetLastError());
+  static_assert(sizeof(Ctl) / 8 <= 256, "k_ctl_out: one workgroup");
+  hipLaunchKernelGGL(k_ctl_out, dim3(1), dim3(256), 0, e->stream, (const Ctl*)e->w.ctl, a.h_ctl);
+  HIPCHK(hipEventRecord(a.ev_done, e->stream));
+  a.pending = true;
+  a.rerun = false;
+  a.c = c;
+  e->anext = k ^ 1;
+  // the previous pass, if any, completes while this one is already queued
+  return complete_async(e, k ^ 1);
+}
+
+int mox_run_wait(mox_engine* e) {
+  if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  HIPCHK(hipSetDevice(e->device));
+  return drain_async(e);
+}
+
 int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end, int at_corpus_end) {
   if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (int rc = drain_async(e)) return rc;
   if (!d_buf && buf_len) return fail(MOX_EINVAL, "buffer is NULL");
   if (own_begin > own_end || own_end > buf_len) return fail(MOX_EINVAL, "bad own range [%zu, %zu) of %zu", own_begin, own_end, buf_len);
   if (own_begin > 0 && own_begin < 4) return fail(MOX_EINVAL, "own_begin must be 0 (corpus start) or >= 4 (left context)");
@@ -935,6 +1060,7 @@ int mox_run_device(mox_engine* e, const void* d_text, size_t len) { return mox_r
 int mox_fetch_table(mox_engine* e, mox_table** out) {
   if (!e || !out) return fail(MOX_EINVAL, "NULL argument");
   *out = nullptr;
+  if (int rc = drain_async(e)) return rc;
   if (!e->have_result) return fail(MOX_ESTATE, "no result: run first");
   HIPCHK(hipSetDevice(e->device));
   const bool timing = (e->flags & MOX_F_TIMING) != 0;
@@ -997,6 +1123,7 @@ int mox_count(mox_engine* e, const uint8_t* text, size_t len, mox_table** out) {
   if (!e || !out || (!text && len)) return fail(MOX_EINVAL, "NULL argument");
   *out = nullptr;
   HIPCHK(hipSetDevice(e->device));
+  if (int rc = drain_async(e)) return rc;
   int rc = stage_host(e, text, len);
   if (rc) return rc;
   if ((rc = mox_run_range(e, len ? (const void*)e->d_text : nullptr, len, 0, len, 1))) return rc;
@@ -1067,6 +1194,7 @@ int mox_count_file(mox_engine* e, const char* path, mox_table** out) {
   if (!e || !path || !out) return fail(MOX_EINVAL, "NULL argument");
   *out = nullptr;
   HIPCHK(hipSetDevice(e->device));
+  if (int rc = drain_async(e)) return rc;
   int fd = open(path, O_RDONLY);
   if (fd < 0) return fail(MOX_EIO, "cannot open %s: %s", path, strerror(errno));
   struct stat st;
@@ -1108,6 +1236,7 @@ int mox_memcpy_d2h(mox_engine* e, void* h_dst, const void* d_src, size_t bytes) 
 }
 int mox_synchronize(mox_engine* e) {
   if (!e) return fail(MOX_EINVAL, "NULL argument");
+  if (int rc = drain_async(e)) return rc;  // queued passes complete (and are checked) first
   HIPCHK(hipStreamSynchronize(e->stream));
   return MOX_OK;
 }

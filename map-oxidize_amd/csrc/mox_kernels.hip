@@ -861,6 +861,15 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
   }
 }
 
+// Control block -> pinned host memory (device-visible): the readback of an
+// async pass as a kernel, so that enqueueing it never blocks the host the way a
+// small hipMemcpyAsync to host may.
+extern "C" __global__ void k_ctl_out(const Ctl* __restrict__ src, Ctl* __restrict__ dst) {
+  constexpr int CW = sizeof(Ctl) / 8;
+  const int t = threadIdx.x;
+  if (t < CW) reinterpret_cast<volatile unsigned long long*>(dst)[t] = reinterpret_cast<const unsigned long long*>(src)[t];
+}
+
 // ------------------------------------------------------------------ pass init
 // One launch instead of a control-block copy and five memsets: the control
 // block (zero, no UTF-8 / halo error, w_n), the partition counters, the long

@@ -125,6 +125,8 @@ def lib():
             "mox_table_free": ([P(_Table)], None),
             "mox_run_device": ([VP, VP, sz], I),
             "mox_run_range": ([VP, VP, sz, sz, sz, I], I),
+            "mox_run_range_async": ([VP, VP, sz, sz, sz, I], I),
+            "mox_run_wait": ([VP], I),
             "mox_fetch_table": ([VP, P(P(_Table))], I),
             "mox_get_stats": ([VP, P(Stats)], I),
             "mox_device_alloc": ([VP, sz, P(VP)], I),
@@ -240,6 +242,13 @@ class Engine:
 
     def run_range(self, d_ptr, buf_len, own_begin, own_end, at_end):
         _check(lib().mox_run_range(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
+
+    def run_range_async(self, d_ptr, buf_len, own_begin, own_end, at_end):
+        """Enqueue a pass; completes the previously enqueued one (include/mox.h)."""
+        _check(lib().mox_run_range_async(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
+
+    def run_wait(self):
+        _check(lib().mox_run_wait(self._h))
 
     def fetch(self):
         t = ctypes.POINTER(_Table)()

@@ -296,3 +296,50 @@ def test_count_file_streamed_chunks(tmp_path, eng):
         t.close()
     with pytest.raises(mox.MoxError):
         eng.count_file(str(tmp_path / "missing.txt"))
+
+
+def test_async_passes():
+    """mox_run_range_async: back-to-back passes, each completed by the next call
+    (or run_wait / fetch); the table is the last pass's; overflow retries and
+    errors are handled by the completing call (include/mox.h)."""
+    a = corpus.fill(corpus.ZIPF, 21, 0, 6 << 20).tobytes()
+    b = corpus.fill(corpus.UNICODE, 22, 0, 3 << 20).tobytes()
+    h = corpus.fill(corpus.HICARD, 23, 0, 24 << 20).tobytes()  # grows buffers: retries inside async completion
+    bad = a[: 1 << 20] + b"\xc0\x80" + a[1 << 20: 2 << 20]
+    want = {k: coracle.count(x)[0] for k, x in (("a", a), ("b", b), ("h", h))}
+    e = mox.Engine(device=0, flags=mox.MOX_F_TIMING_MAP)  # fresh: no reserve, so the first passes overflow
+    bufs = {}
+    try:
+        for k, x in (("a", a), ("b", b), ("h", h), ("bad", bad)):
+            bufs[k] = e.alloc(len(x))
+            e.h2d(bufs[k], x)
+        lens = {"a": len(a), "b": len(b), "h": len(h), "bad": len(bad)}
+
+        def run(k):
+            e.run_range_async(bufs[k], lens[k], 0, lens[k], True)
+
+        def table():
+            t = e.fetch()  # completes pending passes
+            try:
+                return t.sorted_items()
+            finally:
+                t.close()
+
+        for seq in (["h", "a"], ["a", "h"], ["a", "b", "a", "b"], ["h", "h", "b"]):
+            for k in seq:
+                run(k)
+            assert table() == want[seq[-1]], seq
+        run("a")
+        e.run_wait()
+        assert e.stats()["ms_map"] > 0
+        assert table() == want["a"]
+        # an invalid pass reports its error from the call that completes it
+        run("bad")
+        with pytest.raises(mox.Utf8Error):
+            run("b")
+        e.run_wait()
+        assert table() == want["b"]
+    finally:
+        for d in bufs.values():
+            e.free(d)
+        e.close()
