@@ -488,7 +488,8 @@ int run_corpus(mox_engine* e, const Corpus& c) {
       FILE* g = fopen("gpurun_out/mapcyc.csv", "w");
       if (g) {
         for (uint32_t i = 0; i < e->w.map_grid * MAP_WAVES; i++)
-          fprintf(g, "%u,%llu,%llu,%llu,%llu,%llu,%llu\n", i, mc[8 * i], mc[8 * i + 1], mc[8 * i + 2], mc[8 * i + 3], mc[8 * i + 4], mc[8 * i + 5]);
+          fprintf(g, "%u,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, mc[8 * i], mc[8 * i + 1], mc[8 * i + 2], mc[8 * i + 3], mc[8 * i + 4],
+                  mc[8 * i + 5], mc[8 * i + 6]);
         fclose(g);
       }
       FILE* f = fopen("gpurun_out/stamps.csv", "w");

@@ -820,6 +820,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Wor
     if (lane == 0 && w.stamps) {
       unsigned long long* o = w.stamps + 8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8;
       o[0] = cyc.wait; o[1] = cyc.byte; o[2] = cyc.pa; o[3] = cyc.pb; o[4] = cyc.miss; o[5] = cyc.rows;
+      o[6] = __builtin_amdgcn_s_memrealtime();  // this wave's finish (100 MHz)
     }
 #endif
   }
