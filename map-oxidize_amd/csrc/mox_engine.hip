@@ -769,6 +769,9 @@ struct HostTransport : Transport {
                 const uint64_t* rlen) override {
     const uint64_t stot = soff[P - 1] + slen[P - 1], rtot = roff[P - 1] + rlen[P - 1];
     int rc;
+    // a previous call's H2D from hx_recv may still be in flight on the stream:
+    // drain it before a regrow frees the pinned buffer under it
+    if (e->hx_send.cap < stot + 8 || e->hx_recv.cap < rtot + 8) HIPCHK(hipStreamSynchronize(e->stream));
     if ((rc = grow_pinned(e->hx_send, stot + 8)) || (rc = grow_pinned(e->hx_recv, rtot + 8))) return rc;
     if (stot) HIPCHK(hipMemcpyAsync(e->hx_send.p, send, stot, hipMemcpyDeviceToHost, e->stream));
     HIPCHK(hipStreamSynchronize(e->stream));
