@@ -176,6 +176,14 @@ int mox_write_final_result(const mox_table* t, const char* path);
  * ties in table order (the reference's tie order is HashMap-random). */
 int mox_print_top_words(const mox_table* t, size_t n);
 
+/* ---- intermediate (spill) files, SURVEY.md §8(f) rank 4 ---- */
+/* reduce_phase over parsed map files (replaces main.rs:111-150; the parse of
+ * read_map_result main.rs:152-168 is host text work): n (word, count) pairs,
+ * word i = bytes[offs[i], offs[i+1]) taken verbatim (not lowercased), are
+ * summed by word with the GPU reduce; the result is then fetched with
+ * mox_fetch_table like a run's.  Duplicate words are summed. */
+int mox_reduce_pairs(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n);
+
 #ifdef __cplusplus
 }
 #endif

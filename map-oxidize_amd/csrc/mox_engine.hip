@@ -802,6 +802,9 @@ int exchange_pass_once(mox_engine* e, uint64_t r_short, uint64_t blob_bytes, con
   return finish_pass(e, q);
 }
 
+int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, const XDir& rdir, const mox_stats& local,
+                    std::chrono::steady_clock::time_point t0);
+
 int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   if (int rc = drain_async(e)) return rc;
   if (!e->have_result) return fail(MOX_ESTATE, "no local result: mox_run_range first");
@@ -868,7 +871,17 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
     return rc;
   // 4. reduce-only pass over the received partials (the local table is no
   //    longer needed: buffers may be regrown)
-  Caps need = caps_of(w);
+  return reduce_received(e, rs, rb, r_long, rdir, local, t0);
+}
+
+// Reduce-only pass over partial (word, count) records already in
+// x_recv_short (rs WRecs) and x_recv_blob (long-word blobs described by rdir):
+// the exchange's final reduce and mox_reduce_pairs (spill files) share it.
+int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, const XDir& rdir, const mox_stats& local,
+                    std::chrono::steady_clock::time_point t0) {
+  Work& w = e->w;
+  int rc;
+  Caps need = w.cold ? caps_of(w) : initial_caps(1 << 20, e->n_cu);
   need.w_cap = std::max<uint64_t>(need.w_cap, rs + rs / 8 + 1024);
   need.table_cap = std::max<uint64_t>(need.table_cap, rs + r_long + 1024);
   need.bytes_cap = std::max<uint64_t>(need.bytes_cap, rs * 16 + rb + 65536);
@@ -896,6 +909,65 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   e->last_corpus.base = (const uint8_t*)w.ctl;
   e->have_result = true;
   return MOX_OK;
+}
+
+// Host (word, count) pairs -> the exchange's receive layout (one source):
+// words of 1..16 bytes without a NUL byte become 16-byte zero-padded WRec keys,
+// every other word an XHdr + its bytes (padded to 8) in the long blob.  Words
+// are taken as given (no lowercasing: reduce_phase sums parts[0] verbatim,
+// main.rs:160-162,131-134).
+int reduce_pairs_impl(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n) {
+  if (int rc = drain_async(e)) return rc;
+  HIPCHK(hipSetDevice(e->device));
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<WRec> shorts;
+  std::vector<XHdr> hdrs;
+  std::vector<uint8_t> lbytes;
+  shorts.reserve(n);
+  for (uint64_t i = 0; i < n; i++) {
+    const uint64_t a = offs[i], len = offs[i + 1] - offs[i];
+    if (offs[i + 1] < a) return fail(MOX_EINVAL, "offs not ascending at %llu", (unsigned long long)i);
+    if (len == 0) return fail(MOX_EINVAL, "empty word at %llu (split_whitespace never yields one)", (unsigned long long)i);
+    const bool nul = memchr(bytes + a, 0, len) != nullptr;
+    if (len <= 16 && !nul) {
+      uint8_t k[16] = {0};
+      memcpy(k, bytes + a, len);
+      WRec r;
+      memcpy(&r.w0, k, 8);
+      memcpy(&r.w1, k + 8, 8);
+      r.count = counts[i];
+      shorts.push_back(r);
+    } else {
+      uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a 64 (any hash works: all long words of this pass use it)
+      for (uint64_t j = 0; j < len; j++) h = (h ^ bytes[a + j]) * 0x100000001b3ull;
+      hdrs.push_back(XHdr{h, len, counts[i], (uint64_t)lbytes.size()});
+      lbytes.insert(lbytes.end(), bytes + a, bytes + a + len);
+      lbytes.resize((lbytes.size() + 7) & ~size_t(7), 0);
+    }
+  }
+  const uint64_t rs = shorts.size(), r_long = hdrs.size();
+  const uint64_t rb = r_long * sizeof(XHdr) + lbytes.size();
+  int rc;
+  if ((rc = grow_dev(e->x_recv_short, rs * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_recv_blob, rb + 64))) return rc;
+  if (rs) HIPCHK(hipMemcpyAsync(e->x_recv_short.p, shorts.data(), rs * sizeof(WRec), hipMemcpyHostToDevice, e->stream));
+  if (r_long) {
+    HIPCHK(hipMemcpyAsync(e->x_recv_blob.p, hdrs.data(), r_long * sizeof(XHdr), hipMemcpyHostToDevice, e->stream));
+    if (!lbytes.empty())
+      HIPCHK(hipMemcpyAsync((uint8_t*)e->x_recv_blob.p + r_long * sizeof(XHdr), lbytes.data(), lbytes.size(),
+                            hipMemcpyHostToDevice, e->stream));
+  }
+  // pageable sources: complete the copies before the vectors go away
+  HIPCHK(hipStreamSynchronize(e->stream));
+  XDir rdir{};
+  rdir.P = 1;
+  rdir.blob[0] = 0;
+  rdir.blob[1] = rb;
+  rdir.nlong[0] = r_long;
+  rdir.hpre[0] = 0;
+  rdir.hpre[1] = r_long;
+  mox_stats local{};
+  local.weighted_records = rs + r_long;
+  return reduce_received(e, rs, rb, r_long, rdir, local, t0);
 }
 
 }  // namespace
@@ -1320,6 +1392,11 @@ int mox_exchange_host(mox_engine* e, int nranks, int rank, mox_alltoallv_fn fn, 
   if (nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad rank %d of %d", rank, nranks);
   HostTransport t(e, nranks, fn, user);
   return exchange_impl(e, nranks, rank, t);
+}
+
+int mox_reduce_pairs(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n) {
+  if (!e || (n && (!bytes || !offs || !counts))) return fail(MOX_EINVAL, "NULL argument");
+  return reduce_pairs_impl(e, bytes, offs, counts, n);
 }
 
 }  // extern "C"

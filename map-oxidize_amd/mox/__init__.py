@@ -140,6 +140,7 @@ def lib():
             "mox_exchange_host": ([VP, I, I, _A2A_FN, VP], I),
             "mox_write_final_result": ([P(_Table), ctypes.c_char_p], I),
             "mox_print_top_words": ([P(_Table), sz], I),
+            "mox_reduce_pairs": ([VP, VP, VP, VP, U64], I),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
@@ -322,6 +323,20 @@ class Engine:
         if err:
             raise err[0]
         _check(rc)
+
+    # -- spill files (mox/spill.py): reduce_phase over parsed map files
+    def reduce_pairs(self, words, counts):
+        """Sum counts by word (bytes, taken verbatim) on the GPU; returns the
+        Table (main.rs:111-150 over read_map_result's maps)."""
+        from . import spill
+
+        data, offs, cnt = spill.pack_pairs(list(words), list(counts))
+        if len(cnt) != len(offs) - 1:
+            raise ValueError("words and counts differ in length")
+        buf = ctypes.create_string_buffer(data, max(1, len(data)))
+        _check(lib().mox_reduce_pairs(self._h, buf, ctypes.c_void_p(offs.ctypes.data),
+                                      ctypes.c_void_p(cnt.ctypes.data), len(cnt)))
+        return self.fetch()
 
     def close(self):
         if getattr(self, "_h", None):
