@@ -3,14 +3,17 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
+# kernels: the scheduler that groups memory instructions into clauses measured
+# ~1.5-2 % faster on the C2 bench (k_map 1.16 -> 1.14 ms)
+KERNEL_FLAGS ?= -mllvm -amdgpu-sched-strategy=max-memory-clause
 PKG := map-oxidize_amd
 CSRC := $(PKG)/csrc
 OUT := $(PKG)/mox
 
 all: $(OUT)/libmox.so $(OUT)/libmox_corpus.so $(OUT)/meduce-gpu oracle
 
-$(OUT)/mox_kernels.o: $(CSRC)/mox_kernels.hip $(CSRC)/mox_internal.h
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+$(OUT)/mox_kernels.o: $(CSRC)/mox_kernels.hip $(CSRC)/mox_internal.h Makefile
+	$(HIPCC) $(HIPFLAGS) $(KERNEL_FLAGS) -c $< -o $@
 
 $(OUT)/mox_engine.o: $(CSRC)/mox_engine.hip $(CSRC)/mox_internal.h $(CSRC)/mox_unicode_tables.h include/mox.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
