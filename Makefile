@@ -10,16 +10,32 @@ PKG := map-oxidize_amd
 CSRC := $(PKG)/csrc
 OUT := $(PKG)/mox
 
-all: $(OUT)/libmox.so $(OUT)/libmox_corpus.so $(OUT)/meduce-gpu oracle
+all: $(OUT)/libmox.so $(OUT)/libmox_corpus.so $(OUT)/meduce-gpu $(OUT)/libmox_check.so oracle
 
 $(OUT)/mox_kernels.o: $(CSRC)/mox_kernels.hip $(CSRC)/mox_internal.h Makefile
 	$(HIPCC) $(HIPFLAGS) $(KERNEL_FLAGS) -c $< -o $@
 
-$(OUT)/mox_engine.o: $(CSRC)/mox_engine.hip $(CSRC)/mox_internal.h $(CSRC)/mox_unicode_tables.h include/mox.h
+$(OUT)/mox_engine.o: $(CSRC)/mox_engine.hip $(CSRC)/mox_internal.h $(CSRC)/mox_unicode_tables.h $(CSRC)/mox_table.h include/mox.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(OUT)/libmox.so: $(OUT)/mox_kernels.o $(OUT)/mox_engine.o
+$(OUT)/mox_table.o: $(CSRC)/mox_table.cpp $(CSRC)/mox_table.h
+	g++ -O3 -std=c++17 -fPIC -Wall -Wextra -c $< -o $@
+
+$(OUT)/libmox.so: $(OUT)/mox_kernels.o $(OUT)/mox_engine.o $(OUT)/mox_table.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+# check build: device bounds checks on every derived index (MOX_CHK, mox_internal.h);
+# tests load it with MOX_LIB=.../libmox_check.so
+$(OUT)/mox_kernels_check.o: $(CSRC)/mox_kernels.hip $(CSRC)/mox_internal.h Makefile
+	$(HIPCC) $(HIPFLAGS) $(KERNEL_FLAGS) -DMOX_CHECK -c $< -o $@
+
+$(OUT)/mox_engine_check.o: $(CSRC)/mox_engine.hip $(CSRC)/mox_internal.h $(CSRC)/mox_unicode_tables.h $(CSRC)/mox_table.h include/mox.h
+	$(HIPCC) $(HIPFLAGS) -DMOX_CHECK -c $< -o $@
+
+$(OUT)/libmox_check.so: $(OUT)/mox_kernels_check.o $(OUT)/mox_engine_check.o $(OUT)/mox_table.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+check: $(OUT)/libmox_check.so
 
 $(OUT)/libmox_corpus.so: $(CSRC)/mox_corpus.c
 	gcc -O3 -fPIC -shared -Wall -Wextra -o $@ $< -lpthread -lm
@@ -34,4 +50,4 @@ clean:
 	rm -f $(OUT)/*.o $(OUT)/*.so $(OUT)/meduce-gpu
 	$(MAKE) -C oracle clean
 
-.PHONY: all clean oracle
+.PHONY: all clean oracle check

@@ -23,7 +23,10 @@
  * Conventions: every entry point returns an int status (0 = MOX_OK); no
  * exception crosses the ABI; mox_last_error() holds a thread-local message.
  * An engine is bound to one HIP device and is not thread-safe (one host thread
- * per engine).  Calls are synchronous: they return after the result is ready.
+ * per engine).  Every call except mox_run_range_async is synchronous: it
+ * returns after its work (and any pending asynchronous pass) is complete.
+ * mox_run_range_async returns once its pass is queued; see its comment for
+ * the lifetime rule of the device buffer it reads.
  */
 #ifndef MOX_H
 #define MOX_H
@@ -35,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MOX_ABI_VERSION 1
+#define MOX_ABI_VERSION 2
 
 /* status codes */
 #define MOX_OK 0
@@ -50,7 +53,8 @@ extern "C" {
 
 /* mox_config.flags */
 #define MOX_F_NO_DICT 0x1u      /* disable the hot-word dictionary (all tokens take the cold path) */
-#define MOX_F_SORT_BYTES 0x2u   /* fetch returns words sorted bytewise (Rust String Ord) instead of hash order */
+#define MOX_F_SORT_BYTES 0x2u   /* mox_fetch_table returns the words sorted bytewise ascending (Rust String Ord,
+                                   = mox_table_sort_bytes on the fetched table) instead of engine order */
 #define MOX_F_TIMING 0x4u       /* record per-kernel HIP-event timings into mox_stats */
 #define MOX_F_TIMING_MAP 0x8u   /* HIP events around the map kernel only (ms_map): each event record idles
                                    the stream ~5.6 us, so timed loops bracket just the dominant kernel */
@@ -66,9 +70,15 @@ typedef struct mox_config {
 
 typedef struct mox_engine mox_engine;
 
-/* Result table: one entry per distinct lowercased word.  Order: ascending
- * (64-bit word hash, word bytes) -- deterministic -- or bytewise ascending with
- * MOX_F_SORT_BYTES.  Memory is owned by the library until mox_table_free. */
+/* Result table: one entry per distinct lowercased word.  Engine order
+ * (deterministic for a given input and engine configuration): words of at most
+ * 16 bytes without a NUL byte first, ascending by (32-bit key hash, the word's
+ * 16-byte zero-padded key), then longer words in long-table slot order.  With
+ * MOX_F_SORT_BYTES (or after mox_table_sort_bytes): bytewise ascending, Rust
+ * String Ord.  The reference's own order is HashMap-random
+ * (/root/reference/src/main.rs:177-179).  After mox_gather the root's table
+ * is the ranks' tables one after another (rank order), each in engine order.
+ * Memory is owned by the library until mox_table_free. */
 typedef struct mox_table {
   uint64_t n;              /* distinct words */
   uint64_t tokens;         /* total tokens counted (== sum of counts) */
@@ -101,7 +111,12 @@ typedef struct mox_stats {
   double ms_exchange;      /* multi-GPU all-to-all + final reduce */
   uint64_t reduce_units;   /* reduce work units (partitions, or their sub-buckets when split) */
   uint32_t split_partitions; /* partitions split by the high-cardinality path */
-  uint32_t pad0;
+  uint32_t async_reruns;   /* async passes re-run synchronously (overflow), cumulative over the engine */
+  /* multi-GPU (last mox_exchange / mox_gather of this rank) */
+  uint64_t x_bytes_sent;   /* exchange payload bytes this rank sent (records + long-word blobs, self included) */
+  uint64_t x_bytes_recv;   /* exchange payload bytes this rank received */
+  uint64_t gather_bytes;   /* table bytes this rank sent to the gather root (root: received) */
+  double ms_gather;        /* wall time of the last mox_gather on this rank */
 } mox_stats;
 
 const char* mox_last_error(void);
@@ -118,6 +133,8 @@ int mox_count(mox_engine* e, const uint8_t* text, size_t len, mox_table** out);
 /* Count words of a file (reference: split_file(path) .. reduce_phase). */
 int mox_count_file(mox_engine* e, const char* path, mox_table** out);
 void mox_table_free(mox_table* t);
+/* Reorder a fetched table bytewise ascending (Rust String Ord) in place. */
+int mox_table_sort_bytes(mox_table* t);
 
 /* ---- device-resident path (bench / pipelines): corpus already in HBM ---- */
 /* One full pass: HBM corpus -> HBM table.  No host copy of the result. */
@@ -135,7 +152,11 @@ int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_b
  * if a buffer overflowed) after this one is enqueued, so back-to-back passes
  * leave no host round trip between them on the GPU.  A pass's error is
  * returned by the call that completes it: the next mox_run_range_async, or
- * mox_run_wait.  Every other entry point completes pending passes first. */
+ * mox_run_wait.  Every other entry point completes pending passes first.
+ * Buffer lifetime: an overflowed pass is re-run later from d_buf, so d_buf
+ * must stay valid and unmodified until the call that completes the pass has
+ * returned (the next mox_run_range_async, mox_run_wait, or any other entry
+ * point of this engine). */
 int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
                         int at_corpus_end);
 /* Complete every pending async pass; the last one's table is the result. */
@@ -167,6 +188,15 @@ int mox_exchange(mox_engine* e);
 typedef int (*mox_alltoallv_fn)(void* user, const void* send, const uint64_t* send_bytes, void* recv,
                                 const uint64_t* recv_bytes);
 int mox_exchange_host(mox_engine* e, int nranks, int rank, mox_alltoallv_fn fn, void* user);
+/* After mox_exchange on every rank: gather the ranks' final tables into the
+ * root's engine (RCCL send/recv, device to device).  Ranks own disjoint words
+ * after the exchange, so the root's table afterwards is the whole corpus's
+ * table (fetch it with mox_fetch_table; MOX_F_SORT_BYTES gives bytewise order).
+ * Other ranks keep their own table.  Replaces the reference's single-process
+ * result (main.rs:22) for one process per GPU. */
+int mox_gather(mox_engine* e, int root);
+/* The same over the host-staged transport of mox_exchange_host. */
+int mox_gather_host(mox_engine* e, int nranks, int rank, int root, mox_alltoallv_fn fn, void* user);
 
 /* ---- output layer (reference L5: main.rs:170-192) ---- */
 /* final_result.txt: one "{word} {count}\n" line per word.  Truncates on open

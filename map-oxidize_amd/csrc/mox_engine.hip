@@ -25,6 +25,7 @@
 
 #include "../../include/mox.h"
 #include "mox_internal.h"
+#include "mox_table.h"
 #include "mox_unicode_tables.h"
 
 using namespace mox;
@@ -54,6 +55,7 @@ __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
 __global__ void k_xpack_short(Work w, WRec* out);
 __global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob);
 __global__ void k_xingest(Work w, XDir dir, uint64_t n_short);
+__global__ void k_gather_offs(const uint8_t* recv, GDir d, uint64_t* out);
 }
 
 namespace {
@@ -101,6 +103,7 @@ struct mox_engine {
   uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 192;
   int n_cu = 256;
   bool sync_each = false;
+  int test_fail_alloc = 0;     // MOX_TEST_FAIL_ALLOC=k: the k-th sized allocation fails once (tests)
   uint64_t next_cold_cap = 0;  // region capacity learnt from spills of an earlier run
   Work w{};
   Tables tables{};
@@ -113,6 +116,15 @@ struct mox_engine {
   uint8_t* file_pin[8][2]{};
   // last run
   bool have_result = false;
+  // where the result table lives (the pass's t_* buffers, or the gather buffers)
+  struct Res {
+    const uint64_t* counts = nullptr;
+    const uint64_t* offs = nullptr;
+    const uint8_t* bytes = nullptr;
+    uint64_t n = 0, nb = 0, tokens = 0;
+    bool pass = false;  // true: the t_* buffers of the last pass (an exchange can start from it)
+  } res;
+  DevBuf g_counts, g_offs, g_bytes, g_recv;  // mox_gather (root)
   Corpus last_corpus{};
   mox_stats stats{};
   hipEvent_t ev[12]{};
@@ -120,7 +132,6 @@ struct mox_engine {
   // previous one is completed, so the GPU runs them back to back)
   struct AsyncSlot {
     bool pending = false;
-    bool rerun = false;  // a pass before it was re-run synchronously: its result is stale
     Corpus c{};
     Ctl* h_ctl = nullptr;                  // pinned copy of this pass's control block
     hipEvent_t ev_map0 = nullptr, ev_map1 = nullptr, ev_done = nullptr;
@@ -181,40 +192,59 @@ Caps initial_caps(uint64_t n, int map_grid) {
     e->w.f = nullptr; \
   } while (0)
 
-int realloc_sized(mox_engine* e, const Caps& c) {
-  (void)hipDeviceSynchronize();
+void free_sized(mox_engine* e) {
   FREE_FIELD(cold); FREE_FIELD(spill);
   FREE_FIELD(w); FREE_FIELD(w_sorted); FREE_FIELD(u); FREE_FIELD(arena); FREE_FIELD(ltab); FREE_FIELD(lpos);
   FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
   FREE_FIELD(split_k); FREE_FIELD(split_w);
   Work& w = e->w;
-  w.cold_cap = (uint32_t)std::min<uint64_t>(c.cold_cap, 0xFFFFFFF0u);
-  w.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
-  w.w_cap = c.w_cap;
-  w.u_cap = c.u_cap;
-  w.arena_cap = c.arena_cap;
-  w.long_cap = next_pow2(c.long_cap);
-  w.uniq_cap = (uint64_t)w.map_grid * NB * w.cold_cap + c.w_cap;
-  w.table_cap = c.table_cap;
-  w.bytes_cap = c.bytes_cap;
-  w.split_k_cap = c.split_k_cap;
-  w.split_w_cap = c.split_w_cap;
-  int rc;
-  if ((rc = dalloc(e, (void**)&w.cold, (uint64_t)w.map_grid * NB * w.cold_cap * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.spill, (uint64_t)w.map_grid * w.spill_cap * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.w, w.w_cap * sizeof(WRec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.w_sorted, w.w_cap * sizeof(WRec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.u, w.u_cap * sizeof(URec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.arena, w.arena_cap))) return rc;
-  if ((rc = dalloc(e, (void**)&w.ltab, w.long_cap * sizeof(LSlot)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.lpos, (w.long_cap + 1) * 8))) return rc;
-  if ((rc = dalloc(e, (void**)&w.uk, w.uniq_cap * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.uc, w.uniq_cap * 8))) return rc;
-  if ((rc = dalloc(e, (void**)&w.t_counts, w.table_cap * 8))) return rc;
-  if ((rc = dalloc(e, (void**)&w.t_offs, (w.table_cap + 1) * 8))) return rc;
-  if ((rc = dalloc(e, (void**)&w.t_bytes, w.bytes_cap))) return rc;
-  if ((rc = dalloc(e, (void**)&w.split_k, w.split_k_cap * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.split_w, w.split_w_cap * sizeof(WRec)))) return rc;
+  w.cold_cap = w.spill_cap = 0;
+  w.w_cap = w.u_cap = w.arena_cap = w.long_cap = w.uniq_cap = w.table_cap = w.bytes_cap = 0;
+  w.split_k_cap = w.split_w_cap = 0;
+}
+
+// Allocates every size-dependent buffer for capacities c.  The new capacities
+// are committed to e->w only after every allocation succeeded: on a failure
+// everything is freed and the capacities are zero (w.cold == nullptr), so the
+// next ensure_caps reallocates instead of launching kernels on null buffers
+// with a stale recorded capacity.
+int realloc_sized(mox_engine* e, const Caps& c) {
+  (void)hipDeviceSynchronize();
+  free_sized(e);
+  Work n = e->w;
+  n.cold_cap = (uint32_t)std::min<uint64_t>(c.cold_cap, 0xFFFFFFF0u);
+  n.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
+  n.w_cap = c.w_cap;
+  n.u_cap = c.u_cap;
+  n.arena_cap = c.arena_cap;
+  n.long_cap = next_pow2(c.long_cap);
+  n.uniq_cap = (uint64_t)n.map_grid * NB * n.cold_cap + c.w_cap;
+  n.table_cap = c.table_cap;
+  n.bytes_cap = c.bytes_cap;
+  n.split_k_cap = c.split_k_cap;
+  n.split_w_cap = c.split_w_cap;
+  struct { void** p; uint64_t bytes; } plan[] = {
+      {(void**)&n.cold, (uint64_t)n.map_grid * NB * n.cold_cap * 16}, {(void**)&n.spill, (uint64_t)n.map_grid * n.spill_cap * 16},
+      {(void**)&n.w, n.w_cap * sizeof(WRec)}, {(void**)&n.w_sorted, n.w_cap * sizeof(WRec)},
+      {(void**)&n.u, n.u_cap * sizeof(URec)}, {(void**)&n.arena, n.arena_cap},
+      {(void**)&n.ltab, n.long_cap * sizeof(LSlot)}, {(void**)&n.lpos, (n.long_cap + 1) * 8},
+      {(void**)&n.uk, n.uniq_cap * 16}, {(void**)&n.uc, n.uniq_cap * 8},
+      {(void**)&n.t_counts, n.table_cap * 8}, {(void**)&n.t_offs, (n.table_cap + 1) * 8},
+      {(void**)&n.t_bytes, n.bytes_cap}, {(void**)&n.split_k, n.split_k_cap * 16},
+      {(void**)&n.split_w, n.split_w_cap * sizeof(WRec)}};
+  for (auto& a : plan) *a.p = nullptr;
+  for (auto& a : plan) {
+    int rc = (e->test_fail_alloc && --e->test_fail_alloc == 0)
+                 ? fail(MOX_ENOMEM, "hipMalloc(%llu) failed: injected (MOX_TEST_FAIL_ALLOC)", (unsigned long long)a.bytes)
+                 : dalloc(e, a.p, a.bytes);
+    if (rc) {
+      const std::string msg = g_err;
+      for (auto& b : plan) dfree(*b.p);
+      g_err = msg;
+      return rc;  // e->w keeps null buffers and zero capacities
+    }
+  }
+  e->w = n;
   return MOX_OK;
 }
 
@@ -465,6 +495,31 @@ Caps grow_for(mox_engine* e, const Ctl& h) {
 
 void commit_result(mox_engine* e, const Corpus& c, const Ctl& h);
 
+// The table of the pass whose control block is h (in the t_* buffers) becomes
+// the engine's result.
+void set_result(mox_engine* e, const Ctl& h) {
+  e->res.counts = e->w.t_counts;
+  e->res.offs = e->w.t_offs;
+  e->res.bytes = e->w.t_bytes;
+  e->res.n = h.n_total;
+  e->res.nb = h.bytes_total;
+  e->res.tokens = h.tokens;
+  e->res.pass = true;
+  e->have_result = true;
+}
+
+// Check builds (-DMOX_CHECK): a device bounds check failed during the pass
+// (mox_internal.h, MOX_CHK).  Production builds never fail here.
+int check_failed(const Ctl& h) {
+#ifdef MOX_CHECK
+  if (h.dbg_cnt[0])
+    return fail(MOX_EHIP, "device bounds check failed %llu times (largest site id %llu)", h.dbg_cnt[0], h.dbg_cnt[1]);
+#else
+  (void)h;
+#endif
+  return MOX_OK;
+}
+
 int run_corpus(mox_engine* e, const Corpus& c) {
   e->have_result = false;
   uint64_t n = c.own_hi - c.own_lo;
@@ -542,6 +597,7 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     }
     if (getenv("MOX_VERBOSE"))
       fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu\n", h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3]);
+    if ((rc = check_failed(h))) return rc;
     if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
     if (h.halo_err != ~0ull)
       return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
@@ -578,14 +634,14 @@ void commit_result(mox_engine* e, const Corpus& c, const Ctl& h) {
   e->stats.reduce_units = h.n_units;
   e->stats.split_partitions = h.n_split;
   e->last_corpus = c;
-  e->have_result = true;
+  set_result(e, h);
 }
 
 // ---- asynchronous passes (mox_run_range_async / mox_run_wait)
 // Completes async slot k: waits for its control block, then either commits its
-// result, or (overflow / stale) re-runs its corpus synchronously with grown
-// buffers.  A synchronous re-run overwrites the device state, so a later
-// pending pass is marked to be re-run as well.
+// result, or (overflow) re-runs its corpus synchronously with grown buffers.
+// A synchronous re-run overwrites the device state, so a later pending pass is
+// re-run synchronously right after it.
 int complete_async(mox_engine* e, int k) {
   auto& a = e->aslot[k];
   if (!a.pending) return MOX_OK;
@@ -593,27 +649,38 @@ int complete_async(mox_engine* e, int k) {
   HIPCHK(hipEventSynchronize(a.ev_done));
   const Ctl& h = *a.h_ctl;
   auto& later = e->aslot[k ^ 1];
-  if (!a.rerun) {
-    if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
-    if (h.halo_err != ~0ull)
-      return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
-    if (!h.overflow) {
-      const bool map_only = (e->flags & (MOX_F_TIMING | MOX_F_TIMING_MAP)) != 0;
-      if (map_only) {
-        float ms = 0;
-        if (hipEventElapsedTime(&ms, a.ev_map0, a.ev_map1) == hipSuccess) e->stats.ms_map = ms;
-      }
-      e->stats.retries = 0;
-      commit_result(e, a.c, h);
-      if (later.pending) e->have_result = false;  // the later pass is overwriting this table
-      return MOX_OK;
+  if (int rc = check_failed(h)) return rc;
+  if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
+  if (h.halo_err != ~0ull)
+    return fail(MOX_EHALO, "token at byte %llu runs past the end of a non-final shard buffer", h.halo_err);
+  if (!h.overflow) {
+    const bool map_only = (e->flags & (MOX_F_TIMING | MOX_F_TIMING_MAP)) != 0;
+    if (map_only) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, a.ev_map0, a.ev_map1) == hipSuccess) e->stats.ms_map = ms;
     }
+    e->stats.retries = 0;
+    commit_result(e, a.c, h);
+    if (later.pending) e->have_result = false;  // the later pass is overwriting this table
+    return MOX_OK;
   }
-  // overflowed or stale: drain, then the synchronous path (retry loop)
+  // overflowed: drain, then the synchronous path (retry loop)
   HIPCHK(hipStreamSynchronize(e->stream));
-  if (later.pending) later.rerun = true;
+  e->stats.async_reruns++;
   int rc = run_corpus(e, a.c);
-  if (later.pending) e->have_result = false;
+  if (later.pending) {
+    // The re-run overwrote the device state the later pass had written, so
+    // that pass is stale: re-run it now as well.  Left queued as stale, it
+    // would be re-run by the call that completes it, which by then has queued
+    // a newer pass that it would make stale in turn -- every following pass
+    // would run twice.  The first error is the one returned.
+    later.pending = false;
+    e->stats.async_reruns++;
+    const std::string msg = g_err;
+    const int rc2 = run_corpus(e, later.c);
+    if (rc == MOX_OK) rc = rc2;
+    else g_err = msg;
+  }
   return rc;
 }
 
@@ -807,7 +874,7 @@ int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, co
 
 int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   if (int rc = drain_async(e)) return rc;
-  if (!e->have_result) return fail(MOX_ESTATE, "no local result: mox_run_range first");
+  if (!e->have_result || !e->res.pass) return fail(MOX_ESTATE, "no local result: mox_run_range first");
   if (P > MAX_RANKS) return fail(MOX_EINVAL, "at most %d ranks", MAX_RANKS);
   HIPCHK(hipSetDevice(e->device));
   Work& w = e->w;
@@ -871,7 +938,100 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
     return rc;
   // 4. reduce-only pass over the received partials (the local table is no
   //    longer needed: buffers may be regrown)
-  return reduce_received(e, rs, rb, r_long, rdir, local, t0);
+  if ((rc = reduce_received(e, rs, rb, r_long, rdir, local, t0))) return rc;
+  e->stats.x_bytes_sent = ns * sizeof(WRec) + sb + P * sizeof(XCnt);
+  e->stats.x_bytes_recv = rs * sizeof(WRec) + rb + P * sizeof(XCnt);
+  return MOX_OK;
+}
+
+// ============================================================== gather (mox_gather)
+// Every rank sends its final table [counts (8 n) | offs (8 n) | bytes (nb,
+// padded to 8)] to the root; the root concatenates the blocks in rank order
+// (counts and bytes by device copies, offsets rebased by k_gather_offs) into
+// its gather buffers, which then become its result.  Ranks own disjoint words
+// after the exchange, so the concatenation is the whole corpus's table.
+int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
+  if (int rc = drain_async(e)) return rc;
+  if (!e->have_result) return fail(MOX_ESTATE, "no result to gather: run (and exchange) first");
+  if (P > MAX_RANKS || root < 0 || root >= P) return fail(MOX_EINVAL, "bad root %d of %d ranks", root, P);
+  HIPCHK(hipSetDevice(e->device));
+  hipStream_t s = e->stream;
+  int rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!e->d_xcnt) {
+    if ((rc = dalloc(e, (void**)&e->d_xcnt, 2 * MAX_RANKS * sizeof(XCnt)))) return rc;
+    if ((rc = dalloc(e, (void**)&e->d_xcur, 2 * MAX_RANKS * 8))) return rc;
+    HIPCHK(hipHostMalloc((void**)&e->h_xcnt, 2 * MAX_RANKS * sizeof(XCnt), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&e->h_ctl_x, sizeof(Ctl), hipHostMallocDefault));
+  }
+  const mox_engine::Res r = e->res;
+  const uint64_t n = r.n, nb = r.nb, nb8 = (nb + 7) & ~7ull, block = 16 * n + nb8;
+  // 1. sizes: every rank's (n, nb, tokens) row to every peer (only the root uses them)
+  XCnt* d_send = e->d_xcnt;
+  XCnt* d_recv = e->d_xcnt + MAX_RANKS;
+  XCnt* h_send = e->h_xcnt;
+  XCnt* h_recv = e->h_xcnt + MAX_RANKS;
+  for (int d = 0; d < P; d++) h_send[d] = XCnt{n, nb, r.tokens, 0};
+  HIPCHK(hipMemcpyAsync(d_send, h_send, P * sizeof(XCnt), hipMemcpyHostToDevice, s));
+  if ((rc = T.counts(d_send, d_recv, h_send, h_recv))) return rc;
+  // 2. this rank's block -> the root
+  if ((rc = grow_dev(e->x_send_blob, block + 64))) return rc;
+  uint8_t* sb = (uint8_t*)e->x_send_blob.p;
+  if (n) {
+    HIPCHK(hipMemcpyAsync(sb, r.counts, 8 * n, hipMemcpyDeviceToDevice, s));
+    HIPCHK(hipMemcpyAsync(sb + 8 * n, r.offs, 8 * n, hipMemcpyDeviceToDevice, s));
+    if (nb) HIPCHK(hipMemcpyAsync(sb + 16 * n, r.bytes, nb, hipMemcpyDeviceToDevice, s));
+  }
+  uint64_t soff[MAX_RANKS], slen[MAX_RANKS], roff[MAX_RANKS], rlen[MAX_RANKS];
+  uint64_t so = 0, ro = 0, N = 0, NB = 0, tok = 0;
+  GDir gd{};
+  gd.P = (uint32_t)P;
+  for (int d = 0; d < P; d++) {
+    soff[d] = so;
+    slen[d] = d == root ? block : 0;
+    so += slen[d];
+    const uint64_t bn = h_recv[d].n_short, bb = h_recv[d].n_long;  // rank d's n, nb
+    roff[d] = ro;
+    rlen[d] = me == root ? 16 * bn + ((bb + 7) & ~7ull) : 0;
+    gd.roff[d] = ro + 8 * bn;  // rank d's offs block
+    gd.base_n[d] = N;
+    gd.base_b[d] = NB;
+    ro += rlen[d];
+    N += bn;
+    NB += bb;
+    tok += h_recv[d].long_bytes;
+  }
+  gd.base_n[P] = N;
+  gd.base_b_total = NB;
+  if (me == root && (rc = grow_dev(e->g_recv, ro + 64))) return rc;
+  if ((rc = T.alltoallv(sb, soff, slen, (uint8_t*)(me == root ? e->g_recv.p : e->x_send_blob.p), roff, rlen))) return rc;
+  e->stats.gather_bytes = me == root ? ro : block;
+  if (me == root) {
+    // 3. root: concatenate in rank order
+    if ((rc = grow_dev(e->g_counts, 8 * N + 64)) || (rc = grow_dev(e->g_offs, 8 * (N + 1) + 64)) ||
+        (rc = grow_dev(e->g_bytes, NB + 64)))
+      return rc;
+    const uint8_t* rb = (const uint8_t*)e->g_recv.p;
+    for (int d = 0; d < P; d++) {
+      const uint64_t bn = h_recv[d].n_short, bb = h_recv[d].n_long;
+      if (bn) HIPCHK(hipMemcpyAsync((uint64_t*)e->g_counts.p + gd.base_n[d], rb + roff[d], 8 * bn, hipMemcpyDeviceToDevice, s));
+      if (bb) HIPCHK(hipMemcpyAsync((uint8_t*)e->g_bytes.p + gd.base_b[d], rb + roff[d] + 16 * bn, bb, hipMemcpyDeviceToDevice, s));
+    }
+    hipLaunchKernelGGL(k_gather_offs, dim3(256), dim3(256), 0, s, rb, gd, (uint64_t*)e->g_offs.p);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipStreamSynchronize(s));
+    e->res.counts = (const uint64_t*)e->g_counts.p;
+    e->res.offs = (const uint64_t*)e->g_offs.p;
+    e->res.bytes = (const uint8_t*)e->g_bytes.p;
+    e->res.n = N;
+    e->res.nb = NB;
+    e->res.tokens = tok;
+    e->res.pass = false;
+  } else {
+    HIPCHK(hipStreamSynchronize(s));  // the send buffer is reused by the next exchange
+  }
+  e->stats.ms_gather = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return MOX_OK;
 }
 
 // Reduce-only pass over partial (word, count) records already in
@@ -892,6 +1052,7 @@ int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, co
   for (int attempt = 0;; attempt++) {
     if ((rc = exchange_pass_once(e, rs, rb, rdir))) return rc;
     const Ctl& h = *e->h_ctl;
+    if ((rc = check_failed(h))) return rc;
     if (!h.overflow) break;
     if (h.overflow & OVF_REDUCE) return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
     if (attempt >= 4) return fail(MOX_ENOMEM, "exchange buffer growth did not converge (overflow mask 0x%x)", h.overflow);
@@ -907,7 +1068,7 @@ int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, co
   e->stats.ms_exchange = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   e->last_corpus = Corpus{};
   e->last_corpus.base = (const uint8_t*)w.ctl;
-  e->have_result = true;
+  set_result(e, h);
   return MOX_OK;
 }
 
@@ -1026,6 +1187,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
   if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096 + 8 * 8 * 1024 * MAP_WAVES);
   e->sync_each = getenv("MOX_SYNC_EACH") != nullptr;
+  if (const char* f = getenv("MOX_TEST_FAIL_ALLOC")) e->test_fail_alloc = atoi(f);
   int rc = alloc_fixed(e);
   if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));
   if (rc != MOX_OK) {
@@ -1054,7 +1216,9 @@ void mox_engine_destroy(mox_engine* e) {
                   w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.u_uniq, w.u_uniq_off,
                   w.u_bytes, w.u_bytes_off, w.b_bytes, w.split_k, w.split_w};
   for (void* p : ptrs) dfree(p);
-  for (DevBuf* b : {&e->x_send_short, &e->x_send_blob, &e->x_recv_short, &e->x_recv_blob}) dfree(b->p);
+  for (DevBuf* b : {&e->x_send_short, &e->x_send_blob, &e->x_recv_short, &e->x_recv_blob, &e->g_counts, &e->g_offs,
+                    &e->g_bytes, &e->g_recv})
+    dfree(b->p);
   for (DevBuf* b : {&e->hx_send, &e->hx_recv}) if (b->p) (void)hipHostFree(b->p);
   dfree(e->d_xcnt);
   dfree(e->d_xcur);
@@ -1093,7 +1257,12 @@ int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t
   }
   Caps want = initial_caps(c.own_hi - c.own_lo, e->n_cu);
   want.cold_cap = std::max<uint64_t>(want.cold_cap, e->next_cold_cap);
-  int rc = ensure_caps(e, want);  // a regrow synchronises the device: pending passes finish first
+  if (!(e->w.cold && caps_cover(caps_of(e->w), want))) {
+    // a regrow frees the buffers a pending pass wrote its table into: complete
+    // (check, commit) pending passes first
+    if (int rc = drain_async(e)) return rc;
+  }
+  int rc = ensure_caps(e, want);
   if (rc) return rc;
   e->have_result = false;
   Seq q = seq_of(e);
@@ -1105,7 +1274,6 @@ int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t
   hipLaunchKernelGGL(k_ctl_out, dim3(1), dim3(256), 0, e->stream, (const Ctl*)e->w.ctl, a.h_ctl);
   HIPCHK(hipEventRecord(a.ev_done, e->stream));
   a.pending = true;
-  a.rerun = false;
   a.c = c;
   e->anext = k ^ 1;
   // the previous pass, if any, completes while this one is already queued
@@ -1141,8 +1309,8 @@ int mox_fetch_table(mox_engine* e, mox_table** out) {
   HIPCHK(hipSetDevice(e->device));
   const bool timing = (e->flags & MOX_F_TIMING) != 0;
   if (timing) HIPCHK(hipEventRecord(e->ev[6], e->stream));
-  const Ctl& h = *e->h_ctl;
-  uint64_t n = h.n_total, nb = h.bytes_total;
+  const mox_engine::Res& r = e->res;
+  uint64_t n = r.n, nb = r.nb;
   size_t bytes = sizeof(mox_table) + (n + 1) * 8 * 2 + nb + 16;
   uint8_t* mem = (uint8_t*)malloc(bytes);
   if (!mem) return fail(MOX_ENOMEM, "host allocation of %zu bytes failed", bytes);
@@ -1151,25 +1319,43 @@ int mox_fetch_table(mox_engine* e, mox_table** out) {
   uint64_t* offs = counts + n + 1;
   uint8_t* wb = (uint8_t*)(offs + n + 1);
   t->n = n;
-  t->tokens = h.tokens;
+  t->tokens = r.tokens;
   t->counts = counts;
   t->offs = offs;
   t->bytes = wb;
   if (n) {
-    HIPCHK(hipMemcpyAsync(counts, e->w.t_counts, n * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(offs, e->w.t_offs, (n + 1) * 8, hipMemcpyDeviceToHost, e->stream));
-    if (nb) HIPCHK(hipMemcpyAsync(wb, e->w.t_bytes, nb, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(counts, r.counts, n * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipMemcpyAsync(offs, r.offs, (n + 1) * 8, hipMemcpyDeviceToHost, e->stream));
+    if (nb) HIPCHK(hipMemcpyAsync(wb, r.bytes, nb, hipMemcpyDeviceToHost, e->stream));
   } else {
     offs[0] = 0;
   }
   if (timing) HIPCHK(hipEventRecord(e->ev[7], e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   if (timing) e->stats.ms_d2h = ev_ms(e, 6, 7);
+  if (e->flags & MOX_F_SORT_BYTES) {
+    if (int rc = mox_table_sort_bytes(t)) {
+      free(mem);
+      return rc;
+    }
+  }
   *out = t;
   return MOX_OK;
 }
 
 void mox_table_free(mox_table* t) { free(t); }
+
+int mox_table_sort_bytes(mox_table* t) {
+  if (!t) return fail(MOX_EINVAL, "NULL argument");
+  try {
+    if (mox_host::sort_table_bytes(t->n, const_cast<uint64_t*>(t->counts), const_cast<uint64_t*>(t->offs),
+                                   const_cast<uint8_t*>(t->bytes)) != 0)
+      return fail(MOX_ENOMEM, "host allocation failed while sorting the table");
+  } catch (const std::exception& ex) {
+    return fail(MOX_ENOMEM, "sorting the table failed: %s", ex.what());
+  }
+  return MOX_OK;
+}
 
 int mox_get_stats(const mox_engine* e, mox_stats* out) {
   if (!e || !out) return fail(MOX_EINVAL, "NULL argument");
@@ -1392,6 +1578,20 @@ int mox_exchange_host(mox_engine* e, int nranks, int rank, mox_alltoallv_fn fn, 
   if (nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad rank %d of %d", rank, nranks);
   HostTransport t(e, nranks, fn, user);
   return exchange_impl(e, nranks, rank, t);
+}
+
+int mox_gather(mox_engine* e, int root) {
+  if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (!e->comm) return fail(MOX_ESTATE, "mox_comm_init first");
+  RcclTransport t(e);
+  return gather_impl(e, e->nranks, e->rank, root, t);
+}
+
+int mox_gather_host(mox_engine* e, int nranks, int rank, int root, mox_alltoallv_fn fn, void* user) {
+  if (!e || !fn) return fail(MOX_EINVAL, "NULL argument");
+  if (nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad rank %d of %d", rank, nranks);
+  HostTransport t(e, nranks, fn, user);
+  return gather_impl(e, nranks, rank, root, t);
 }
 
 int mox_reduce_pairs(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n) {

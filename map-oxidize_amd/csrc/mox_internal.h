@@ -60,6 +60,20 @@ constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points 
 #endif
 enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u,
                   DBG_RED_NOSORT = 32u, DBG_RED_NOINSERT = 64u, DBG_RED_NOSLOW = 128u, DBG_COUNT = 256u, DBG_RED_PLAINADD = 512u, DBG_STAMP = 1024u };
+// Bounds checks of derived indices (UnitDesc ranges, scatter cursors, table
+// offsets), compiled in only with -DMOX_CHECK (libmox_check.so, `make check`):
+// a failed check counts into ctl->dbg_cnt[0], records the largest site id in
+// dbg_cnt[1], and skips the access; the host then fails the call with MOX_EHIP.
+// Production builds evaluate to true and emit nothing.
+enum : uint32_t {
+  CHK_SMALL_DESC = 1u, CHK_SMALL_OUT = 2u, CHK_RED_OUT = 3u, CHK_SPLIT_K = 4u, CHK_SPLIT_W = 5u, CHK_UNIT = 6u,
+  CHK_MAT_ROW = 7u, CHK_MAT_BYTES = 8u, CHK_SCATTER = 9u, CHK_RED_IN = 10u, CHK_GATHER = 11u
+};
+#ifdef MOX_CHECK
+#define MOX_CHK(w, ok, site) (::mox::chk_record((w).ctl, (ok), (site)))
+#else
+#define MOX_CHK(w, ok, site) (true)
+#endif
 enum : uint32_t {
   OVF_POOL = 1u, OVF_W = 2u, OVF_U = 4u, OVF_LONG = 8u, OVF_ARENA = 16u, OVF_PROBE = 32u,
   OVF_TABLE = 64u, OVF_BYTES = 128u, OVF_REDUCE = 256u, OVF_SPLIT = 512u,
@@ -100,6 +114,16 @@ struct Ctl {
   unsigned long long n_big;       // entries of big_units (k_reduce work list)
   unsigned long long short_bytes; // table bytes of the short words (long words follow)
 };
+
+#ifdef MOX_CHECK
+__device__ __forceinline__ bool chk_record(Ctl* ctl, bool ok, uint32_t site) {
+  if (!ok) {
+    atomicAdd(&ctl->dbg_cnt[0], 1ull);
+    atomicMax(&ctl->dbg_cnt[1], (unsigned long long)site);
+  }
+  return ok;
+}
+#endif
 
 // Weighted record: a key with a count (dictionary totals, spills, Unicode-lane
 // short words, received partials).
@@ -147,6 +171,16 @@ struct XDir {
   uint64_t blob[MAX_RANKS + 1];   // byte offset of peer d's long blob
   uint64_t nlong[MAX_RANKS];      // headers in peer d's blob
   uint64_t hpre[MAX_RANKS + 1];   // prefix of nlong (receive side)
+};
+
+// mox_gather: where source rank s's offsets sit in the root's receive buffer,
+// and the row / byte base of its part of the gathered table.
+struct GDir {
+  uint32_t P;
+  uint64_t roff[MAX_RANKS];
+  uint64_t base_n[MAX_RANKS + 1];
+  uint64_t base_b[MAX_RANKS];
+  uint64_t base_b_total;
 };
 
 struct Tables {  // Unicode case data in device memory

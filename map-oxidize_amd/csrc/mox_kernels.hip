@@ -1379,7 +1379,10 @@ __device__ __forceinline__ void scatter_sub(const Work& w, uint32_t* lh, uint32_
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < SCT_PER; j++)
-    if (bk[j] != 0xFFFFFFFFu) w.w_sorted[w.w_off[bk[j]] + base[bk[j]] + li[j]] = WRec{r0[j], r1[j], rc[j]};
+    if (bk[j] != 0xFFFFFFFFu) {
+      const uint64_t q = w.w_off[bk[j]] + base[bk[j]] + li[j];
+      if (MOX_CHK(w, q < w.w_off[bk[j] + 1] && q < w.w_cap, CHK_SCATTER)) w.w_sorted[q] = WRec{r0[j], r1[j], rc[j]};
+    }
   __syncthreads();
 }
 extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {
@@ -1692,8 +1695,11 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
     const uint32_t sb = SUB_PER_T * tid + j;
     if (sb < nsub) {
       const uint32_t u = u0 + sb;
-      w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + ec + ew, c[j], d[j], b, kk};
-      if (c[j] + d[j] > SMALL_CAP) w.big_units[atomicAdd(&w.ctl->n_big, 1ull)] = u;
+      if (MOX_CHK(w, u < U_MAX, CHK_UNIT)) w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + ec + ew, c[j], d[j], b, kk};
+      if (c[j] + d[j] > SMALL_CAP) {
+        const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
+        if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
+      }
       cc[sb] = (uint32_t)ec;
       cw[sb] = (uint32_t)ew;
     }
@@ -1704,14 +1710,14 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   uint4* ok = w.split_k + kb;
   for_partition_cold(w, b, [&](uint4 k) {
     const uint32_t p = atomicAdd(&cc[hbits(hash32(k.x, k.y, k.z, k.w), NB_LOG2, kk)], 1u);
-    ok[p] = k;
+    if (MOX_CHK(w, p < tc && kb + p < w.split_k_cap, CHK_SPLIT_K)) ok[p] = k;
   });
   const uint64_t w0 = w.w_off[b], w1 = w.w_off[b + 1];
   WRec* ow = w.split_w + wb;
   for (uint64_t i = w0 + tid; i < w1; i += blockDim.x) {
     const WRec r = w.w_sorted[i];
     const uint32_t p = atomicAdd(&cw[hbits(key_hash(r.w0, r.w1), NB_LOG2, kk)], 1u);
-    ow[p] = r;
+    if (MOX_CHK(w, p < tw && wb + p < w.split_w_cap, CHK_SPLIT_W)) ow[p] = r;
   }
 }
 
@@ -1937,8 +1943,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       for (uint32_t i = tid; i < nu; i += RED_THREADS) {
         const uint16_t sl = s.idx[i];
         const uint4 kk4 = s.key[sl];
-        w.uk[out0 + written + i] = kk4;
-        w.uc[out0 + written + i] = s.cnt[sl];
+        // check builds: the unit's distinct keys stay inside its record range
+        if (MOX_CHK(w, written + i < (split ? (uint64_t)ud.in_n + ud.win_n : w.rec_off[b + 1] - w.rec_off[b]) &&
+                           out0 + written + i < w.uniq_cap, CHK_RED_OUT)) {
+          w.uk[out0 + written + i] = kk4;
+          w.uc[out0 + written + i] = s.cnt[sl];
+        }
         lb += key_len16(kk4);
       }
       if (lb) atomicAdd(&s.misc[3], lb);
@@ -2072,18 +2082,10 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
   for (uint32_t it = 0; u < U; u += G, it++) {
     const UnitDesc d = dring[it & 1], dn = dring[(it + 1) & 1];
     bool cur_small = small_unit(d);
-#ifdef MOX_SR_CHECK
-    if (cur_small && (d.in_off + d.in_n > w.split_k_cap || d.win_off + d.win_n > w.split_w_cap ||
-                      d.rec_off + d.in_n + d.win_n > w.uniq_cap)) {
-      if (tid == 0) {
-        atomicAdd(&w.ctl->dbg_cnt[0], 1ull);
-        atomicMax(&w.ctl->dbg_cnt[1], (unsigned long long)u);
-        atomicMax(&w.ctl->dbg_cnt[2], (unsigned long long)d.in_off + d.in_n);
-        atomicMax(&w.ctl->dbg_cnt[3], (unsigned long long)d.rec_off + d.in_n + d.win_n);
-      }
+    // check builds: the unit's input and output ranges lie inside their buffers
+    if (cur_small && !MOX_CHK(w, d.in_off + d.in_n <= w.split_k_cap && d.win_off + d.win_n <= w.split_w_cap &&
+                                     d.rec_off + d.in_n + d.win_n <= w.uniq_cap, CHK_SMALL_DESC))
       cur_small = false;
-    }
-#endif
     const uint32_t n = d.in_n + d.win_n, shift = NB_LOG2 + d.kk;
     // this unit's records into LDS + bin counts (bins were zeroed by the previous unit)
     if (cur_small) {
@@ -2231,13 +2233,24 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
           }
           if (!go) break;
         }
-        w.uk[d.rec_off + o] = k;
-        w.uc[d.rec_off + o] = c;
+        if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {  // distinct keys <= records
+          w.uk[d.rec_off + o] = k;
+          w.uc[d.rec_off + o] = c;
+        }
         lb += key_len16(k);
         o++;
       }
       if (lb) atomicAdd(&sbytes, lb);
       if (tid == 0) w.u_uniq[u] = nu;  // summed per partition by k_unit_uniq_scan
+    } else {
+      // A unit this kernel skips (whole partition or > SMALL_CAP records) has
+      // no barrier above: without this one, wave 0 could overwrite
+      // dring[it & 1] before a lagging wave has read it as d at the top of
+      // this iteration.  That wave would then take unit u + 2G for u, disagree
+      // with the others on cur_small, pair its barriers with theirs and write
+      // its scan results to wrong (possibly out-of-range) uk / uc positions:
+      // the intermittent illegal-address faults of round 1.
+      lds_barrier();
     }
     if (tid == 0) dring[it & 1] = dnn;
     lds_barrier();  // LDS reused by the next unit
@@ -2378,7 +2391,7 @@ extern "C" __global__ __launch_bounds__(256) void k_mat(Work w, Corpus c) {
       // (bytes at the partial first/last line one by one: neighbours share them)
       const uint64_t gbase = boff & ~15ull;
       const uint32_t sh = (uint32_t)(boff - gbase);
-      if (i < n) {
+      if (i < n && MOX_CHK(w, dst0 + i < w.table_cap && boff + ex + len <= w.bytes_cap, CHK_MAT_ROW)) {
         const uint64_t o = boff + ex;
         w.t_counts[dst0 + i] = w.uc[src0 + i];
         w.t_offs[dst0 + i] = o;
@@ -2510,6 +2523,23 @@ extern "C" __global__ void k_xingest(Work w, XDir dir, uint64_t n_short) {
   if ((threadIdx.x & 63) == 0 && tok) atomicAdd(&s_tok, tok);
   __syncthreads();
   if (threadIdx.x == 0 && s_tok) atomicAdd(&w.ctl->tokens, s_tok);  // one global atomic per workgroup
+}
+
+// ------------------------------------------------------------------ gather
+// Root of mox_gather: offsets of the concatenated table.  Row t of the
+// gathered table belongs to source s with base_n[s] <= t < base_n[s + 1];
+// its offset is the source's own offset plus the bytes of the sources before
+// it.  Row N (the end) gets the total.
+extern "C" __global__ void k_gather_offs(const uint8_t* recv, GDir d, uint64_t* out) {
+  const uint64_t N = d.base_n[d.P];
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t <= N; t += stride) {
+    if (t == N) { out[N] = d.base_b_total; continue; }
+    uint32_t a = 0, b = d.P - 1;  // last source with base_n[s] <= t
+    while (a < b) { const uint32_t m = (a + b + 1) >> 1; if (d.base_n[m] <= t) a = m; else b = m - 1; }
+    const uint64_t* offs = reinterpret_cast<const uint64_t*>(recv + d.roff[a]);
+    out[t] = offs[t - d.base_n[a]] + d.base_b[a];
+  }
 }
 
 }  // namespace mox

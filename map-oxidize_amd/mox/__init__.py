@@ -29,6 +29,7 @@ MOX_ESTATE = -7
 MOX_EHALO = -8
 
 MOX_F_NO_DICT = 0x1
+MOX_F_SORT_BYTES = 0x2  # fetch returns the words bytewise ascending (Rust String Ord)
 MOX_F_TIMING = 0x4
 MOX_F_TIMING_MAP = 0x8  # HIP events around the map kernel only
 
@@ -90,7 +91,11 @@ class Stats(ctypes.Structure):
         ("ms_exchange", ctypes.c_double),
         ("reduce_units", ctypes.c_uint64),
         ("split_partitions", ctypes.c_uint32),
-        ("pad0", ctypes.c_uint32),
+        ("async_reruns", ctypes.c_uint32),
+        ("x_bytes_sent", ctypes.c_uint64),
+        ("x_bytes_recv", ctypes.c_uint64),
+        ("gather_bytes", ctypes.c_uint64),
+        ("ms_gather", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -123,6 +128,7 @@ def lib():
             "mox_count": ([VP, VP, sz, P(P(_Table))], I),
             "mox_count_file": ([VP, ctypes.c_char_p, P(P(_Table))], I),
             "mox_table_free": ([P(_Table)], None),
+            "mox_table_sort_bytes": ([P(_Table)], I),
             "mox_run_device": ([VP, VP, sz], I),
             "mox_run_range": ([VP, VP, sz, sz, sz, I], I),
             "mox_run_range_async": ([VP, VP, sz, sz, sz, I], I),
@@ -138,6 +144,8 @@ def lib():
             "mox_comm_init": ([VP, I, I, ctypes.c_char_p], I),
             "mox_exchange": ([VP], I),
             "mox_exchange_host": ([VP, I, I, _A2A_FN, VP], I),
+            "mox_gather": ([VP, I], I),
+            "mox_gather_host": ([VP, I, I, I, _A2A_FN, VP], I),
             "mox_write_final_result": ([P(_Table), ctypes.c_char_p], I),
             "mox_print_top_words": ([P(_Table), sz], I),
             "mox_reduce_pairs": ([VP, VP, VP, VP, U64], I),
@@ -194,6 +202,11 @@ class Table:
     def sorted_items(self):
         """Deterministic key sort (bytewise, Rust String Ord) used for parity."""
         return sorted(self.items(), key=lambda kv: kv[0])
+
+    def sort_bytes(self):
+        """Reorder this table bytewise ascending in place (mox_table_sort_bytes)."""
+        _check(lib().mox_table_sort_bytes(self._p))
+        return self
 
     def write_final_result(self, path):
         _check(lib().mox_write_final_result(self._p, path.encode()))
@@ -300,6 +313,17 @@ class Engine:
         """The same exchange over a host transport.  ``alltoallv(send, send_sizes,
         recv_sizes)`` gets the send bytes (memoryview, blocks for ranks 0..n-1)
         and must return the received bytes (blocks from ranks 0..n-1)."""
+        self._host_call(lambda fn: lib().mox_exchange_host(self._h, nranks, rank, fn, None), nranks, alltoallv)
+
+    def gather(self, root=0):
+        """Gather every rank's final table into root's engine over RCCL (mox_gather)."""
+        _check(lib().mox_gather(self._h, root))
+
+    def gather_host(self, nranks, rank, alltoallv, root=0):
+        """mox_gather over a host transport (same callback as exchange_host)."""
+        self._host_call(lambda fn: lib().mox_gather_host(self._h, nranks, rank, root, fn, None), nranks, alltoallv)
+
+    def _host_call(self, call, nranks, alltoallv):
         err = []
 
         def cb(_user, send, send_bytes, recv, recv_bytes):
@@ -319,7 +343,7 @@ class Engine:
                 return 1
 
         fn = _A2A_FN(cb)
-        rc = lib().mox_exchange_host(self._h, nranks, rank, fn, None)
+        rc = call(fn)
         if err:
             raise err[0]
         _check(rc)

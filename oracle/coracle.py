@@ -31,6 +31,15 @@ def lib():
         L.moxo_count_range.restype = ctypes.c_int
         L.moxo_utf8_invalid_at.argtypes = [ctypes.c_void_p, ctypes.c_uint64]
         L.moxo_utf8_invalid_at.restype = ctypes.c_int64
+        VP, U64, P64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)
+        L.moxo_count_digest.argtypes = [VP, U64, ctypes.c_int, VP, P64]
+        L.moxo_count_digest.restype = ctypes.c_int
+        L.moxo_table_digest.argtypes = [U64, VP, VP, VP, ctypes.c_int, VP]
+        L.moxo_table_digest.restype = None
+        L.moxo_count_tokens.argtypes = [VP, U64, ctypes.c_int]
+        L.moxo_count_tokens.restype = U64
+        L.moxo_count_words.argtypes = [VP, U64, ctypes.c_int, VP, VP, U64, VP]
+        L.moxo_count_words.restype = None
         _lib = L
     return _lib
 
@@ -101,3 +110,60 @@ def count_range(data, own_begin, own_end):
         return [(raw[offs[i]:offs[i + 1]], int(counts[i])) for i in range(nn)], int(t.tokens)
     finally:
         lib().moxo_free(ctypes.byref(t))
+
+
+def _ptr(data):
+    import numpy as np
+    if isinstance(data, np.ndarray):
+        return data, data.ctypes.data, data.nbytes
+    keep = bytes(data)
+    return keep, ctypes.cast(ctypes.c_char_p(keep), ctypes.c_void_p).value, len(keep)
+
+
+def count_digest(data, nthreads=16):
+    """(digest tuple (distinct, sum of counts, sum1, sum2), tokens) of the word
+    count of ``data`` -- the order-independent fingerprint of the table that
+    count() would return, computed without sorting it (for multi-GiB corpora)."""
+    import numpy as np
+    keep, ptr, n = _ptr(data)
+    out = np.zeros(4, np.uint64)
+    tok = ctypes.c_uint64()
+    rc = lib().moxo_count_digest(ptr, n, nthreads, out.ctypes.data, ctypes.byref(tok))
+    del keep
+    if rc == EUTF8:
+        raise InvalidUtf8(-1)
+    return tuple(int(x) for x in out), int(tok.value)
+
+
+def table_digest(counts, offs, raw, nthreads=16):
+    """The same fingerprint of a (counts, offs, bytes) table, e.g. the GPU's."""
+    import numpy as np
+    counts = np.ascontiguousarray(counts, dtype=np.uint64)
+    offs = np.ascontiguousarray(offs, dtype=np.uint64)
+    buf = np.frombuffer(raw, dtype=np.uint8) if len(raw) else np.zeros(1, np.uint8)
+    out = np.zeros(4, np.uint64)
+    lib().moxo_table_digest(counts.size, counts.ctypes.data, offs.ctypes.data, buf.ctypes.data, nthreads, out.ctypes.data)
+    return tuple(int(x) for x in out)
+
+
+def count_tokens(data, nthreads=16):
+    """Token count only (valid UTF-8 assumed): split_whitespace without counting words."""
+    keep, ptr, n = _ptr(data)
+    r = int(lib().moxo_count_tokens(ptr, n, nthreads))
+    del keep
+    return r
+
+
+def count_words(data, words, nthreads=16):
+    """Counts of the given distinct lowercased words (bytes) in ``data``."""
+    import numpy as np
+    words = list(words)
+    assert len(set(words)) == len(words), "distinct words only"
+    keep, ptr, n = _ptr(data)
+    wb = np.frombuffer(b"".join(words) or b"\0", dtype=np.uint8)
+    wo = np.zeros(len(words) + 1, np.uint64)
+    wo[1:] = np.cumsum([len(w) for w in words])
+    out = np.zeros(max(1, len(words)), np.uint64)
+    lib().moxo_count_words(ptr, n, nthreads, wb.ctypes.data, wo.ctypes.data, len(words), out.ctypes.data)
+    del keep
+    return [int(x) for x in out[:len(words)]]

@@ -383,3 +383,226 @@ void moxo_free(moxo_table* t) {
   free(t->counts); free(t->offs); free(t->bytes);
   memset(t, 0, sizeof(*t));
 }
+
+/* ---- property checks for corpora too large for a full sorted table ----
+ * (tests/test_gpu_scale.py: C4 at >= 4 GiB, C4/C5 at 16 GiB).  Same
+ * tokenizer, case folding and counting rules as moxo_count above. */
+
+static uint64_t mix64(uint64_t x) { /* splitmix64 finaliser */
+  x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27; x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+static uint64_t fnv_full(const uint8_t* s, uint64_t n) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  for (uint64_t i = 0; i < n; i++) { h ^= s[i]; h *= 0x100000001b3ull; }
+  return h;
+}
+/* Order-independent digest of one (word, count) entry, summed over a table. */
+static void digest_add(uint64_t d[4], const uint8_t* w, uint64_t len, uint64_t cnt) {
+  const uint64_t x = mix64(fnv_full(w, len) ^ (cnt * 0x9E3779B97F4A7C15ull) ^ (len << 56));
+  d[0] += 1; d[1] += cnt; d[2] += x; d[3] += mix64(x + 0x632BE59BD9B4E019ull);
+}
+
+/* Cuts of s[0, n) into at most nt pieces at '\n' bytes (cuts[0..nt]). */
+static int cut_lines(const uint8_t* s, uint64_t n, int nthreads, uint64_t* cuts) {
+  int nt = 0;
+  cuts[0] = 0;
+  for (int t = 1; t < nthreads; t++) {
+    uint64_t p = n / (uint64_t)nthreads * (uint64_t)t;
+    if (p < cuts[nt]) p = cuts[nt];
+    while (p < n && s[p] != '\n') p++;
+    if (p < n && p > cuts[nt]) cuts[++nt] = p;
+  }
+  cuts[++nt] = n;
+  return nt;
+}
+
+/* Calls f(ctx, lowered word, len) for every token of s[0, n) (valid UTF-8). */
+typedef void (*tok_fn)(void* ctx, const uint8_t* w, uint64_t len);
+static uint64_t for_tokens(const uint8_t* s, uint64_t n, tok_fn f, void* ctx) {
+  uint64_t i = 0, tokens = 0, bcap = 0;
+  uint8_t* buf = NULL;
+  while (i < n) {
+    uint64_t p = i;
+    uint32_t c = dec(s, &p);
+    if (moxo_is_whitespace(c)) { i = p; continue; }
+    uint64_t start = i;
+    i = p;
+    while (i < n) {
+      uint64_t q = i;
+      uint32_t d = dec(s, &q);
+      if (moxo_is_whitespace(d)) break;
+      i = q;
+    }
+    tokens++;
+    if (!f) continue;
+    uint64_t len = i - start;
+    if (len * 2 + 8 > bcap) { bcap = len * 2 + 8; buf = (uint8_t*)realloc(buf, bcap); }
+    f(ctx, buf, moxo_lowercase(s + start, len, buf));
+  }
+  free(buf);
+  return tokens;
+}
+
+typedef struct { uint8_t* p; uint64_t n, cap; } bytevec;
+static void bv_put(bytevec* v, const void* x, uint64_t k) {
+  if (v->n + k > v->cap) {
+    v->cap = v->cap ? v->cap * 2 : 1 << 20;
+    while (v->n + k > v->cap) v->cap *= 2;
+    v->p = (uint8_t*)realloc(v->p, v->cap);
+  }
+  memcpy(v->p + v->n, x, k);
+  v->n += k;
+}
+
+typedef struct {
+  const uint8_t* s; uint64_t n; int T; int t;
+  bytevec* out;      /* [T] words routed to their owner thread: u32 len + bytes */
+  uint64_t tokens;
+  void* all;         /* the job array (phase 2 reads every job's out[t]) */
+  uint64_t d[4];
+} djob;
+static void route(void* ctx, const uint8_t* w, uint64_t len) {
+  djob* j = (djob*)ctx;
+  const uint32_t owner = (uint32_t)(((fnv_full(w, len) >> 32) * (uint64_t)j->T) >> 32);
+  const uint32_t l32 = (uint32_t)len;
+  bv_put(&j->out[owner], &l32, 4);
+  bv_put(&j->out[owner], w, len);
+}
+static void* dphase1(void* a) { djob* j = (djob*)a; j->tokens = for_tokens(j->s, j->n, route, j); return NULL; }
+static void* dphase2(void* a) {
+  djob* j = (djob*)a;
+  djob* all = (djob*)j->all;
+  cmap m;
+  cmap_init(&m);
+  for (int t = 0; t < j->T; t++) {
+    bytevec* v = &all[t].out[j->t];
+    for (uint64_t o = 0; o < v->n;) {
+      uint32_t len;
+      memcpy(&len, v->p + o, 4);
+      cmap_add(&m, v->p + o + 4, len, 1);
+      o += 4 + len;
+    }
+  }
+  memset(j->d, 0, sizeof j->d);
+  for (uint64_t i = 0; i < m.cap; i++)
+    if (m.slots[i].h) digest_add(j->d, m.arena + m.slots[i].off, m.slots[i].len, m.slots[i].count);
+  cmap_free(&m);
+  return NULL;
+}
+
+/* Digest {distinct words, total count, sum1, sum2} of the word count of
+ * s[0, n), without building the sorted table: tokens are routed to T owner
+ * threads by hash, each owner counts its words.  Returns MOXO_EUTF8 on invalid
+ * input, else 0; out[4] = digest, *tokens = token count. */
+int moxo_count_digest(const uint8_t* s, uint64_t n, int nthreads, uint64_t out[4], uint64_t* tokens) {
+  memset(out, 0, 4 * sizeof(uint64_t));
+  *tokens = 0;
+  if (moxo_utf8_invalid_at(s, n) >= 0) return MOXO_EUTF8;
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  uint64_t cuts[65];
+  const int nt = cut_lines(s, n, nthreads, cuts);
+  djob* jobs = (djob*)calloc((size_t)nt, sizeof(djob));
+  pthread_t th[64];
+  for (int t = 0; t < nt; t++) {
+    jobs[t] = (djob){s + cuts[t], cuts[t + 1] - cuts[t], nt, t, (bytevec*)calloc((size_t)nt, sizeof(bytevec)), 0, jobs, {0, 0, 0, 0}};
+    pthread_create(&th[t], NULL, dphase1, &jobs[t]);
+  }
+  for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+  for (int t = 0; t < nt; t++) pthread_create(&th[t], NULL, dphase2, &jobs[t]);
+  for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+  for (int t = 0; t < nt; t++) {
+    for (int k = 0; k < 4; k++) out[k] += jobs[t].d[k];
+    *tokens += jobs[t].tokens;
+    for (int d = 0; d < nt; d++) free(jobs[t].out[d].p);
+    free(jobs[t].out);
+  }
+  free(jobs);
+  return 0;
+}
+
+/* The same digest of a table (counts[n], offs[n+1], bytes), e.g. the GPU's. */
+typedef struct { const uint64_t* c; const uint64_t* o; const uint8_t* b; uint64_t lo, hi; uint64_t d[4]; } tdjob;
+static void* tdmain(void* a) {
+  tdjob* j = (tdjob*)a;
+  for (uint64_t i = j->lo; i < j->hi; i++) digest_add(j->d, j->b + j->o[i], j->o[i + 1] - j->o[i], j->c[i]);
+  return NULL;
+}
+void moxo_table_digest(uint64_t n, const uint64_t* counts, const uint64_t* offs, const uint8_t* bytes, int nthreads,
+                       uint64_t out[4]) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  tdjob jobs[64];
+  pthread_t th[64];
+  const uint64_t per = (n + (uint64_t)nthreads - 1) / (uint64_t)nthreads;
+  for (int t = 0; t < nthreads; t++) {
+    uint64_t lo = per * (uint64_t)t, hi = lo + per;
+    if (lo > n) lo = n;
+    if (hi > n) hi = n;
+    jobs[t] = (tdjob){counts, offs, bytes, lo, hi, {0, 0, 0, 0}};
+    pthread_create(&th[t], NULL, tdmain, &jobs[t]);
+  }
+  memset(out, 0, 4 * sizeof(uint64_t));
+  for (int t = 0; t < nthreads; t++) {
+    pthread_join(th[t], NULL);
+    for (int k = 0; k < 4; k++) out[k] += jobs[t].d[k];
+  }
+}
+
+/* Token count of s[0, n) (valid UTF-8 assumed): the cheap pass. */
+typedef struct { const uint8_t* s; uint64_t n, tokens; } tcjob;
+static void* tcmain(void* a) { tcjob* j = (tcjob*)a; j->tokens = for_tokens(j->s, j->n, NULL, NULL); return NULL; }
+uint64_t moxo_count_tokens(const uint8_t* s, uint64_t n, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  uint64_t cuts[65];
+  const int nt = cut_lines(s, n, nthreads, cuts);
+  tcjob jobs[64];
+  pthread_t th[64];
+  for (int t = 0; t < nt; t++) {
+    jobs[t] = (tcjob){s + cuts[t], cuts[t + 1] - cuts[t], 0};
+    pthread_create(&th[t], NULL, tcmain, &jobs[t]);
+  }
+  uint64_t tok = 0;
+  for (int t = 0; t < nt; t++) { pthread_join(th[t], NULL); tok += jobs[t].tokens; }
+  return tok;
+}
+
+/* Counts of k given (lowercased) words in s[0, n): a spot check of a table. */
+typedef struct { const uint8_t* s; uint64_t n; const cmap* set; uint64_t* cnt; } wcjob;
+static void wc_tok(void* ctx, const uint8_t* w, uint64_t len) {
+  wcjob* j = (wcjob*)ctx;
+  const cmap* m = j->set;
+  const uint64_t h = fnv(w, len);
+  for (uint64_t k = h & (m->cap - 1);; k = (k + 1) & (m->cap - 1)) {
+    const slot_t* sl = &m->slots[k];
+    if (!sl->h) return;
+    if (sl->h == h && sl->len == len && memcmp(m->arena + sl->off, w, len) == 0) { j->cnt[sl->count]++; return; }
+  }
+}
+static void* wcmain(void* a) { wcjob* j = (wcjob*)a; for_tokens(j->s, j->n, wc_tok, j); return NULL; }
+void moxo_count_words(const uint8_t* s, uint64_t n, int nthreads, const uint8_t* wbytes, const uint64_t* woffs, uint64_t k,
+                      uint64_t* out) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 64) nthreads = 64;
+  cmap set;  /* word -> its index (in the count field) */
+  cmap_init(&set);
+  for (uint64_t i = 0; i < k; i++) cmap_add(&set, wbytes + woffs[i], woffs[i + 1] - woffs[i], i);
+  uint64_t cuts[65];
+  const int nt = cut_lines(s, n, nthreads, cuts);
+  wcjob jobs[64];
+  pthread_t th[64];
+  for (int t = 0; t < nt; t++) {
+    jobs[t] = (wcjob){s + cuts[t], cuts[t + 1] - cuts[t], &set, (uint64_t*)calloc(k + 1, 8)};
+    pthread_create(&th[t], NULL, wcmain, &jobs[t]);
+  }
+  memset(out, 0, k * 8);
+  for (int t = 0; t < nt; t++) {
+    pthread_join(th[t], NULL);
+    for (uint64_t i = 0; i < k; i++) out[i] += jobs[t].cnt[i];
+    free(jobs[t].cnt);
+  }
+  cmap_free(&set);
+}

@@ -24,6 +24,13 @@ void moxo_free(moxo_table* t);
 int64_t moxo_utf8_invalid_at(const uint8_t* s, uint64_t n);
 int moxo_is_whitespace(uint32_t c);
 uint64_t moxo_lowercase(const uint8_t* s, uint64_t n, uint8_t* out);
+/* property checks for big corpora (no sorted table) */
+int moxo_count_digest(const uint8_t* s, uint64_t n, int nthreads, uint64_t out[4], uint64_t* tokens);
+void moxo_table_digest(uint64_t n, const uint64_t* counts, const uint64_t* offs, const uint8_t* bytes, int nthreads,
+                       uint64_t out[4]);
+uint64_t moxo_count_tokens(const uint8_t* s, uint64_t n, int nthreads);
+void moxo_count_words(const uint8_t* s, uint64_t n, int nthreads, const uint8_t* wbytes, const uint64_t* woffs, uint64_t k,
+                      uint64_t* out);
 
 #ifdef __cplusplus
 }

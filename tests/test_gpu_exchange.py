@@ -32,8 +32,10 @@ def mixed_corpus(n, seed):
     return z[: n // 2] + b" " + u + b"\n" + extra + b" " + z[n // 2:]
 
 
-def run_ranks(data, world, use_threads=True):
-    """Each rank: engine on device 0, its shard, exchange over ThreadAlltoall."""
+def run_ranks(data, world, gather_root=None):
+    """Each rank: engine on device 0, its shard, exchange over ThreadAlltoall;
+    with gather_root, then the gather of every table into that rank's engine
+    (out[root] is then the gathered table, the others their own)."""
     x = mdist.ThreadAlltoall(world)
     out, errs = [None] * world, []
 
@@ -49,6 +51,8 @@ def run_ranks(data, world, use_threads=True):
                         e.h2d(d, buf)
                     e.run_range(d, len(buf), ob, oe, at_end)
                     e.exchange_host(world, r, x.fn(r))
+                    if gather_root is not None:
+                        e.gather_host(world, r, x.fn(r), root=gather_root)
                     t = e.fetch()
                     out[r] = (t.sorted_items(), t.tokens)
                     t.close()
@@ -151,3 +155,83 @@ def test_host_exchange_zipf_many_records():
     wc, wo, wraw, wtok = coracle.count_arrays(np.frombuffer(data, np.uint8), nthreads=16)
     assert sum(tok for _, tok in out) == wtok
     assert_tables_equal((counts, offs, b"".join(words)), (wc, wo, wraw))
+
+
+def test_host_gather_threads():
+    """mox_gather over the host transport: after the exchange every rank's
+    table goes to the root, whose table is then the whole corpus's."""
+    data = mixed_corpus(6 << 20, 51)
+    want, wtok = coracle.count(data)
+    for world, root in ((2, 0), (3, 2)):
+        out = run_ranks(data, world, gather_root=root)
+        items, tok = out[root]
+        assert tok == wtok
+        assert sorted(items) == want
+        others = [o for r, o in enumerate(out) if r != root]
+        assert all(sum(c for _, c in it) == t for it, t in others)
+
+
+def test_rccl_gather_world1():
+    data = mixed_corpus(3 << 20, 19)
+    e = mox.Engine(device=0, flags=mox.MOX_F_SORT_BYTES)
+    try:
+        e.comm_init(1, 0, mox.comm_unique_id())
+        d = e.alloc(len(data))
+        try:
+            e.h2d(d, data)
+            e.run_range(d, len(data), 0, len(data), True)
+            e.exchange()
+            e.gather(0)
+            t = e.fetch()
+            got = list(t.items())  # MOX_F_SORT_BYTES: table order is bytewise
+            t.close()
+            st = e.stats()
+        finally:
+            e.free(d)
+    finally:
+        e.close()
+    assert got == coracle.count(data)[0]
+    assert st["x_bytes_sent"] > 0 and st["x_bytes_sent"] == st["x_bytes_recv"] and st["gather_bytes"] > 0
+
+
+def c3_like_corpus(world, per_rank, seed):
+    """world x per_rank bytes of Zipf text with Unicode tokens and long words
+    mixed in, and at every shard cut (a multiple of the 1 MiB generator block)
+    an item straddling the cut: a token, a 3-byte or a 2-byte Unicode
+    whitespace, a Greek token with a final sigma, CR LF and VT.  The base text
+    is ASCII and planted items never overlap, so the corpus stays valid UTF-8."""
+    import numpy as np
+    n = world * per_rank
+    buf = bytearray(corpus.fill(corpus.ZIPF, seed, 0, n).tobytes())
+    rng = np.random.default_rng(seed)
+    items = ["日本語ΣΑΣ".encode(), "İstanbul".encode(), "ΟΔΟΣ".encode(), "\u212aelvin".encode(),
+             b"Supercalifragilisticexpialidocious", b"Antidisestablishmentarianism_" * 3]
+    cuts = {r * per_rank for r in range(1, world)}
+    for k in range(n // 4096 - 1):  # one item per 4 KiB slot, away from the cuts
+        it = items[int(rng.integers(len(items)))]
+        p = k * 4096 + 1 + int(rng.integers(0, 4096 - 200))
+        if any(abs(p - c) < 256 for c in cuts):
+            continue
+        buf[p - 1:p + len(it) + 1] = b" " + it + b"\n"
+    plants = [b"xx STRADDLING yy", " a\u3000b ".encode(), " c\u00a0d ".encode(), " ΣΙΣΥΦΟΣ ".encode(),
+              b"\r\n\r\nWORD\x0b"]
+    for r in range(1, world):
+        it = plants[(r - 1) % len(plants)]
+        p = r * per_rank - len(it) // 2
+        buf[p:p + len(it)] = it
+    return bytes(buf)
+
+
+def test_world8_threads_c3_path():
+    """C3's data path at P = 8 (threads sharing device 0, host transport):
+    8 x 32 MiB shards cut at 1 MiB generator-block boundaries, with tokens and
+    multi-byte whitespace straddling the cuts; part_owner / long_owner /
+    owner_first_part at NB = 1024 / 8; exact against the oracle, and the
+    gather at rank 0 gives the whole table."""
+    world, per = 8, 32 << 20
+    data = c3_like_corpus(world, per, 0x5EED0003)
+    assert all(mdist.shard_range(len(data), world, r)[2] in (0, 64) for r in range(world))
+    out = run_ranks(data, world, gather_root=0)
+    want, wtok = coracle.count(data, nthreads=16)
+    assert out[0][1] == wtok
+    assert out[0][0] == want

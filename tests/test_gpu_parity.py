@@ -198,6 +198,12 @@ def test_count_file_and_cli(tmp_path, eng):
     assert r.returncode == 0, r.stderr
     lines = r.stdout.decode().splitlines()
     assert lines[0] == "Top 10 words:" and len(lines) == 11
+    # print_top_words (main.rs:184-192): the 10 largest counts, descending;
+    # ties may print in any order (the reference's order is HashMap-random)
+    want = dict(coracle.count(data)[0])
+    top = [line.encode().rsplit(b": ", 1) for line in lines[1:]]
+    assert [int(c) for _, c in top] == sorted(want.values(), reverse=True)[:10]
+    assert all(want[w] == int(c) for w, c in top)
     final = {}
     for line in (tmp_path / "final_result.txt").read_bytes().split(b"\n"):
         if line:
@@ -343,3 +349,95 @@ def test_async_passes():
         for d in bufs.values():
             e.free(d)
         e.close()
+
+
+def test_sort_bytes_flag():
+    """MOX_F_SORT_BYTES: the fetched table is in bytewise order (Rust String
+    Ord), i.e. exactly the oracle's list, not only the same multiset."""
+    e = mox.Engine(device=0, flags=mox.MOX_F_SORT_BYTES)
+    try:
+        for data in (corpus.fill(corpus.UNICODE, 7, 0, 3 << 20).tobytes() + b" " + b"z" * 40 + b" " + b"a" * 17,
+                     b"b a B \xc3\x89 \x00x x\x00 " + b"k" * 20, b""):
+            t = e.count(data)
+            got = list(t.items())
+            t.close()
+            assert got == coracle.count(data)[0]
+    finally:
+        e.close()
+
+
+def test_async_overflow_reruns_once():
+    """An overflowing async pass is re-run once, and so is the pass queued
+    behind it; later passes are not re-run (no stale-rerun cascade)."""
+    h = corpus.fill(corpus.HICARD, 23, 0, 24 << 20).tobytes()
+    a = corpus.fill(corpus.ZIPF, 24, 0, 4 << 20).tobytes()
+    e = mox.Engine(device=0)  # fresh: no reserve, so the first high-cardinality pass overflows
+    try:
+        dh, da = e.alloc(len(h)), e.alloc(len(a))
+        e.h2d(dh, h)
+        e.h2d(da, a)
+        e.run_range_async(dh, len(h), 0, len(h), True)
+        for _ in range(6):
+            e.run_range_async(da, len(a), 0, len(a), True)
+        e.run_wait()
+        assert e.stats()["async_reruns"] <= 2
+        t = e.fetch()
+        assert t.sorted_items() == coracle.count(a)[0]
+        t.close()
+        e.free(dh)
+        e.free(da)
+    finally:
+        e.close()
+
+
+def test_allocation_failure_recovers(monkeypatch):
+    """A device allocation failing half-way through a regrow returns MOX_ENOMEM
+    and leaves the engine usable: the next call reallocates."""
+    monkeypatch.setenv("MOX_TEST_FAIL_ALLOC", "5")
+    e = mox.Engine(device=0)
+    monkeypatch.delenv("MOX_TEST_FAIL_ALLOC")
+    try:
+        data = corpus.fill(corpus.ZIPF, 4, 0, 2 << 20).tobytes()
+        with pytest.raises(mox.MoxError) as ex:
+            e.count(data)
+        assert ex.value.code == mox.MOX_ENOMEM
+        assert gpu_items(e, data) == oracle_items(data)
+    finally:
+        e.close()
+
+
+def test_bounds_check_build():
+    """The check build (libmox_check.so, -DMOX_CHECK: every derived index of
+    the split / reduce / scatter / table kernels is bounds-checked on the
+    device) runs the shapes of the round-1 faults clean: mixed small, big and
+    whole reduce units in one k_reduce_small sweep (C4-like text beside Zipf
+    text), and a two-rank exchange whose reduce-only pass splits partitions."""
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    code = r"""
+import sys, threading
+sys.path[:0] = [%r, %r, %r]
+import numpy as np, coracle, mox
+from mox import corpus
+from conftest import assert_tables_equal
+import test_gpu_exchange as X
+z = corpus.fill(corpus.ZIPF, 77, 0, 24 << 20)
+h = corpus.fill(corpus.HICARD, 78, 0, 72 << 20)
+data = np.concatenate([z, np.frombuffer(b" \n", np.uint8), h])
+e = mox.Engine(device=0)
+t = e.count(data.tobytes()); got = t.arrays(); t.close()
+st = e.stats(); e.close()
+assert st["split_partitions"] > 0, st
+assert_tables_equal(got, coracle.count_arrays(data, nthreads=16)[:3])
+hc = corpus.fill(corpus.HICARD, 91, 0, 48 << 20).tobytes()
+out = X.run_ranks(hc, 2)
+items = [w for part, _ in out for w in part]
+assert sorted(items) == coracle.count(hc, nthreads=16)[0]
+print("check build clean")
+""" % (os.path.join(ROOT, "map-oxidize_amd"), os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests"))
+    env = dict(os.environ, MOX_LIB=os.path.join(ROOT, "map-oxidize_amd", "mox", "libmox_check.so"))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    assert b"check build clean" in r.stdout

@@ -1,0 +1,84 @@
+"""GPU: the BASELINE configs at (or near) full size, where a sorted oracle
+table is too big to build, checked through size-independent properties.
+
+* C4 at 4 GiB (high cardinality, ~3.5e8 distinct words): the table's
+  order-independent digest (distinct words, sum of counts, two 64-bit sums of a
+  mix of (FNV-1a(word), count)) equals the oracle's, computed by routing tokens
+  to owner threads by hash (oracle/mox_oracle.c, moxo_count_digest).  This size
+  crosses the >2 GiB table-bytes fetch and splits partitions to kk >= 10.
+* C4 at 16 GiB (1.4e9 distinct): sum of counts == tokens == the oracle's token
+  count (a tokenize-only pass), every word distinct and NUL-free, and a spot
+  check: the oracle's counts of 4,000 random table words equal the table's.
+* C5 at 16 GiB (heavy skew, ~1e6 distinct): the full sorted table against the
+  oracle's.
+Each test holds the corpus, its device copy and the fetched table: tens of GB
+of host memory for C4 16 GiB."""
+import numpy as np
+import pytest
+
+import coracle
+import mox
+from mox import corpus
+from conftest import assert_tables_equal
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+def gpu_table(data, **kw):
+    e = mox.Engine(device=0, reserve_bytes=data.nbytes, **kw)
+    d = e.alloc(data.nbytes)
+    try:
+        e.h2d(d, data)
+        e.run_device(d, data.nbytes)
+        t = e.fetch()
+        counts, offs, raw = t.arrays()
+        tokens = t.tokens
+        t.close()
+        st = e.stats()
+    finally:
+        e.free(d)
+        e.close()
+    return counts, offs, raw, tokens, st
+
+
+def test_c4_4gib_digest():
+    cfg = corpus.CONFIGS["C4"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, 4 << 30)
+    counts, offs, raw, tokens, st = gpu_table(data)
+    assert st["split_partitions"] > 900 and st["reduce_units"] > 1024 * 256, st
+    assert offs[-1] > (2 << 30)  # the table-bytes fetch crosses 2 GiB
+    assert int(counts.sum()) == tokens
+    got = coracle.table_digest(counts, offs, raw)
+    del counts, offs, raw
+    want, wtok = coracle.count_digest(data, nthreads=16)
+    assert tokens == wtok
+    assert got == want
+
+
+def spot_check(data, counts, offs, raw, k, seed):
+    rng = np.random.default_rng(seed)
+    idx = rng.choice(counts.size, size=min(k, counts.size), replace=False)
+    words = [raw[offs[i]:offs[i + 1]] for i in idx]
+    want = coracle.count_words(data, words, nthreads=16)
+    assert want == [int(counts[i]) for i in idx]
+
+
+def test_c4_full_16gib_properties():
+    cfg = corpus.CONFIGS["C4"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
+    counts, offs, raw, tokens, st = gpu_table(data)
+    assert int(counts.sum()) == tokens
+    assert tokens == coracle.count_tokens(data, nthreads=16)
+    assert counts.size > 1_000_000_000 and (counts > 0).all()
+    assert np.frombuffer(raw, np.uint8).min() > 0  # C4 words are [a-z0-9]: no NUL, lowercased
+    spot_check(data, counts, offs, raw, 4000, 1)
+
+
+def test_c5_full_16gib_exact():
+    cfg = corpus.CONFIGS["C5"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
+    counts, offs, raw, tokens, _ = gpu_table(data)
+    assert int(counts.sum()) == tokens
+    wc, wo, wraw, wtok = coracle.count_arrays(data, nthreads=16)
+    assert tokens == wtok
+    assert_tables_equal((counts, offs, raw), (wc, wo, wraw))
