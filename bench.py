@@ -11,8 +11,10 @@ copied to HBM before timing.
   torchrun --nproc-per-node N bench.py --gpus N ...
 
 Default workload (N = 1): config C2 of BASELINE.json, 1 GiB Zipf(1.1)
-English-like corpus.  N > 1: weak scaling, 1 GiB byte-range shard per GPU of the
-same corpus stream (rank r owns bytes [r GiB, (r+1) GiB)).
+English-like corpus.  N > 1: config C3, weak scaling with an 8 GiB byte-range
+shard per GPU of the C3 corpus stream (rank r owns bytes [8r GiB, 8(r+1) GiB);
+N = 8 is the 64 GiB corpus); a step is the local pass, the RCCL all-to-all
+exchange, the final per-owner reduce and the gather of the result at rank 0.
 Rank 0 prints ONE JSON line.
 """
 import argparse
@@ -53,7 +55,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="C2", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="", choices=[""] + sorted(WORKLOADS),
+                    help="default: C2 at N = 1, C3 (8 GiB shard per GPU) at N > 1")
+    ap.add_argument("--no-gather", action="store_true", help="N > 1: leave the final tables on their owner ranks")
+    ap.add_argument("--cpu-runs", type=int, default=3, help="CPU baseline: median of this many runs")
     ap.add_argument("--bytes-per-gpu", type=int, default=0, help="override the shard size")
     ap.add_argument("--cpu-sample-mib", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -68,33 +73,57 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(kind, seed, sample_bytes):
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, timeout=20).stdout.decode()
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    return None
+
+
+def cpu_baseline(kind, seed, sample_bytes, runs=3):
     """Faithful C++ restatement of the reference pipeline (oracle/build/meduce_ref),
-    timed on a bounded sample of the same corpus: 8 map threads, 4 reduce threads."""
+    timed on a bounded sample of the same corpus: 8 map threads, 4 reduce
+    threads (main.rs:12-13); median of ``runs`` runs."""
     exe = os.path.join(ROOT, "oracle", "build", "meduce_ref")
     if not os.path.exists(exe):
         return None
     data = corpus.fill(kind, seed, 0, sample_bytes)
     tmpdir = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    times = []
     with tempfile.TemporaryDirectory(dir=tmpdir) as d:
         path = os.path.join(d, "shakes.txt")
         data.tofile(path)
         del data
-        r = subprocess.run([exe, path, "--workdir", d, "--quiet", "--time"], capture_output=True, timeout=600)
-        if r.returncode != 0:
-            return None
-        t = json.loads(r.stderr.decode().strip().splitlines()[-1])
+        for _ in range(max(1, runs)):
+            r = subprocess.run([exe, path, "--workdir", d, "--quiet", "--time"], capture_output=True, timeout=600)
+            if r.returncode != 0:
+                return None
+            times.append(json.loads(r.stderr.decode().strip().splitlines()[-1])["hot_s"])
+    hot = statistics.median(times)
     return {
-        "value": round(sample_bytes / t["hot_s"] / 1e9, 4),
+        "value": round(sample_bytes / hot / 1e9, 4),
         "unit": "GB/s",
         "cores": 8,
         "kind": "port",
         "sample": "first %d MiB of the same corpus; oracle/build/meduce_ref (faithful C++ restatement of "
-                  "main.rs: line round-robin into 8 chunks, 8 map threads, spill files, 4 reduce threads "
-                  "behind one mutex), -O3, split+map+reduce wall time (main.rs:16-22)" % (sample_bytes >> 20),
-        "hot_s": t["hot_s"],
+                  "main.rs: line round-robin into 8 chunks, 8 map threads, spill files on tmpfs, 4 reduce "
+                  "threads behind one mutex), -O3, split+map+reduce wall time (main.rs:16-22), median of %d runs"
+                  % (sample_bytes >> 20, len(times)),
+        "hot_s_runs": [round(t, 4) for t in times],
+        "threads": {"map": 8, "reduce": 4},
         "host_nproc": os.cpu_count(),
+        "cpu_model": cpu_model(),
     }
+
+
+def local_tokens(eng, d_buf, n, own_b, own_e, at_end):
+    """Tokens of this rank's shard: one local pass (untimed, after the timed loop)."""
+    eng.run_range(d_buf, n, own_b, own_e, at_end)
+    return eng.stats()["tokens"]
 
 
 def main():
@@ -108,6 +137,8 @@ def main():
     if world > 1:
         import torch.distributed as dist  # control plane only (rendezvous, barrier, max-time)
         dist.init_process_group("gloo")
+    if not a.workload:
+        a.workload = "C2" if world == 1 else "C3"
     kind, seed, per_rank, desc = WORKLOADS[a.workload]
     if a.bytes_per_gpu:
         per_rank = a.bytes_per_gpu
@@ -137,6 +168,8 @@ def main():
     # run synchronously.
     use_async = world == 1 and not a.sync_passes
 
+    gather = world > 1 and not a.no_gather
+
     def step(sync=False):
         if use_async and not sync:
             eng.run_range_async(d_buf, hi - lo, own_b, own_e, at_end)
@@ -147,18 +180,27 @@ def main():
                 eng.exchange_host(world, rank, a2a)
             else:
                 eng.exchange()
+            if gather:  # the whole table at rank 0 (mox_gather: device to device)
+                if a2a:
+                    eng.gather_host(world, rank, a2a, root=0)
+                else:
+                    eng.gather(0)
 
     for _ in range(a.warmup):
         step()
     eng.synchronize()  # completes (and checks) every queued pass
     if dist:
         dist.barrier()
-    map_ms = []
+    map_ms, xms, gms = [], [], []
     t0 = time.perf_counter()
     for i in range(a.steps):
         step()
         if not use_async or i > 0:  # async: the call completed the previous pass
             map_ms.append(eng.ms_map())
+        if world > 1:
+            st = eng.stats()
+            xms.append(st["ms_exchange"])
+            gms.append(st["ms_gather"])
     eng.synchronize()
     if use_async:
         map_ms.append(eng.ms_map())  # the last pass, completed by synchronize
@@ -176,15 +218,37 @@ def main():
         elapsed = float(t.item())
     last = eng.stats()
     t = eng.fetch()
-    counts, _, _ = t.arrays()
+    counts, offs, _ = t.arrays()
     ok = int(counts.sum()) == t.tokens
+    table_n, table_bytes, table_tokens = t.n, int(offs[-1]) if t.n else 0, t.tokens
     t.close()
-    if dist:  # after the exchange every rank owns disjoint words: tokens add up to the whole corpus
+    xinfo = None
+    if dist:
         import torch
-        tk = torch.tensor([last["tokens"], int(ok)], dtype=torch.float64)
-        dist.all_reduce(tk)
-        tokens_all = int(tk[0].item())
-        ok = int(tk[1].item()) == world
+        # per-rank tokens of the local pass (the diagnostic step's stats are the
+        # exchange's; the local pass counted what this rank's shard holds)
+        loc = torch.tensor([float(local_tokens(eng, d_buf, hi - lo, own_b, own_e, at_end)), last["x_bytes_sent"],
+                            last["x_bytes_recv"], statistics.mean(xms) if xms else 0.0,
+                            statistics.mean(gms) if gms else 0.0], dtype=torch.float64)
+        rows = [torch.zeros_like(loc) for _ in range(world)]
+        dist.all_gather(rows, loc)
+        rows = [r.tolist() for r in rows]
+        tokens_all = int(sum(r[0] for r in rows))
+        if gather:  # rank 0 holds the whole table: its tokens are the corpus's
+            ok = ok and (rank != 0 or table_tokens == tokens_all)
+        okt = torch.tensor([int(ok)], dtype=torch.float64)
+        dist.all_reduce(okt)
+        ok = int(okt.item()) == world
+        xinfo = {
+            "per_rank_tokens": [int(r[0]) for r in rows],
+            "all_to_all_bytes": int(sum(r[1] for r in rows)),
+            "all_to_all_bytes_recv": int(sum(r[2] for r in rows)),
+            "exchange_ms_max_over_ranks": round(max(r[3] for r in rows), 4),
+            "gather_ms_max_over_ranks": round(max(r[4] for r in rows), 4) if gather else None,
+            "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens} if gather else None,
+            "note": "exchange = counts all-to-all + pack + payload all-to-all (RCCL send/recv in one group) + "
+                    "reduce-only pass; gather = every rank's final table to rank 0 (mox_gather)",
+        }
     else:
         tokens_all = last["tokens"]
 
@@ -202,6 +266,9 @@ def main():
                     traffic = tj.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        # algorithmic bytes per step = input read once + the output
+        # table written once (word bytes + a u64 count per distinct word)
+        b_alg = total + (table_bytes + 8 * table_n if (world == 1 or gather) else 0)
         line = {
             "metric": METRIC,
             "value": round(gbs, 3),
@@ -218,12 +285,18 @@ def main():
                     "copied to HBM before timing)" % (kind, seed, KIND_DESC.get(kind, "?")),
             "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
                        "parallelism": "dp%d byte-range shards%s" % (
-                           world, (" + %s all-to-all" % ("RCCL" if a.xport == "rccl" else "host/gloo")) if world > 1 else "")},
+                           world, (" + %s all-to-all%s" % ("RCCL" if a.xport == "rccl" else "host/gloo",
+                                                            " + gather at rank 0" if gather else "")) if world > 1 else "")},
             "words_per_s": round(tokens_all / (elapsed / a.steps), 1),
             "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * world), 2),
+            "algorithmic_bytes_per_step": b_alg,
+            "roofline_end_to_end": {"achieved": round(b_alg / (elapsed / a.steps) / 1e9, 1),
+                                    "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
+                                    "frac": round(b_alg / (elapsed / a.steps) / 1e9 / (HBM_PEAK_GBS * world), 4)},
             "roofline": {
                 "kernel": "k_map",
                 "bound": "hbm",
+                "limiter": "VALU issue + LDS latency at 3.5 consumer waves/SIMD, not HBM (SQ/PMC counters, DESIGN.md §4)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -236,15 +309,16 @@ def main():
             "pass_mode": "async (mox_run_range_async: back-to-back passes, each completed and checked)" if use_async else "sync",
             "phases_ms": {k: round(statistics.mean(p[k] for p in phases), 4)
                           for k in ("ms_run", "ms_dict", "ms_map", "ms_lanes", "ms_reduce", "ms_finalize",
-                                    "ms_exchange")},
+                                    "ms_exchange", "ms_gather")},
             "stats": {k: last[k] for k in ("tokens", "uniques", "dict_words", "cold_records", "weighted_records",
                                            "unicode_tokens", "long_tokens", "chunks", "max_subpasses", "retries",
                                            "reduce_units", "split_partitions")},
+            "multi_gpu": xinfo,
             "check_sum_counts_eq_tokens": ok,
             "cpu_baseline": None,
         }
         if world == 1 and not a.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(kind, seed, min(per_rank, a.cpu_sample_mib << 20))
+            line["cpu_baseline"] = cpu_baseline(kind, seed, min(per_rank, a.cpu_sample_mib << 20), a.cpu_runs)
         print(json.dumps(line), flush=True)
     eng.free(d_buf)
     eng.close()

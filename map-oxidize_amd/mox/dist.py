@@ -1,6 +1,7 @@
 """Host side of the multi-GPU path: byte-range sharding with
-word-boundary halos, a gloo all-to-all for the host-staged exchange transport,
-and the final gather of the per-rank tables.
+word-boundary halos, a gloo all-to-all for the host-staged exchange and
+gather transport (mox_exchange_host / mox_gather_host), and a checker-side
+merge of per-rank tables.  The gather itself is device side (mox_gather).
 
 The reference runs one process (main.rs:16-22); sharding is this engine's
 addition.  Every token belongs to the rank whose byte range holds its first
@@ -58,17 +59,6 @@ def merge_tables(parts):
             raise ValueError("word %r owned by two ranks" % (w,))
         out.append((w, c))
     return out
-
-
-def gather_items(items, group=None):
-    """Gather every rank's bytewise-sorted items on rank 0 and merge them
-    (None on the other ranks)."""
-    import torch.distributed as dist
-
-    world = dist.get_world_size(group)
-    parts = [None] * world if dist.get_rank(group) == 0 else None
-    dist.gather_object(items, parts, dst=0, group=group)
-    return merge_tables(parts) if parts is not None else None
 
 
 class ThreadAlltoall:

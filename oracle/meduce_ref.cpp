@@ -96,9 +96,18 @@ static Map read_map_result(const std::string& name) {  // :152-168
     std::vector<std::pair<size_t, size_t>> parts;
     split_whitespace(line, [&](size_t st, size_t len) { parts.emplace_back(st, len); });
     if (parts.size() == 2) {
+      // parts[1].parse::<usize>() (main.rs:161): an optional '+', then one or
+      // more ASCII digits, no overflow of u64; anything else is skipped
       std::string num = line.substr(parts[1].first, parts[1].second);
-      bool ok = !num.empty() && std::all_of(num.begin(), num.end(), [](char c) { return c >= '0' && c <= '9'; });
-      if (ok) m[line.substr(parts[0].first, parts[0].second)] = std::stoull(num);
+      size_t k = (!num.empty() && num[0] == '+') ? 1 : 0;
+      bool ok = num.size() > k;
+      unsigned long long v = 0;
+      for (size_t j = k; ok && j < num.size(); j++) {
+        const char c = num[j];
+        ok = c >= '0' && c <= '9' && v <= (~0ull - (unsigned)(c - '0')) / 10;
+        if (ok) v = v * 10 + (unsigned)(c - '0');
+      }
+      if (ok) m[line.substr(parts[0].first, parts[0].second)] = v;
     }
   }
   return m;

@@ -77,10 +77,12 @@ def _worker(rank, world, port, q):
         rs = [s + rank + 1 for s in range(world)]
         got = a2a(memoryview(send), ss, rs)
         want = b"".join(bytes([s * 16 + rank]) * rs[s] for s in range(world))
-        # disjoint per-rank tables, gathered and merged on rank 0
-        items = sorted((b"w%d_%d" % (rank, i), i + 1) for i in range(5))
-        merged = mdist.gather_items(items)
-        q.put((rank, got == want, merged))
+        # the gather's transport shape: every rank sends one block to rank 0 only
+        blk = b"r%d" % rank * (rank + 3)
+        gs = [len(blk) if d == 0 else 0 for d in range(world)]
+        sizes = [len(b"r%d" % s * (s + 3)) if rank == 0 else 0 for s in range(world)]
+        gathered = a2a(memoryview(blk), gs, sizes)
+        q.put((rank, got == want, gathered))
     finally:
         dist.destroy_process_group()
 
@@ -94,5 +96,4 @@ def test_gloo_alltoallv_and_gather_world2():
     res = dict((r, (ok, m)) for r, ok, m in (q.get(timeout=120) for _ in range(world)))
     [p.join(60) for p in ps]
     assert all(ok for ok, _ in res.values())
-    want = sorted((b"w%d_%d" % (r, i), i + 1) for r in range(world) for i in range(5))
-    assert res[0][1] == want and res[1][1] is None
+    assert res[0][1] == b"".join(b"r%d" % s * (s + 3) for s in range(world)) and res[1][1] == b""
