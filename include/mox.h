@@ -70,10 +70,12 @@ typedef struct mox_config {
 
 typedef struct mox_engine mox_engine;
 
-/* Result table: one entry per distinct lowercased word.  Engine order
- * (deterministic for a given input and engine configuration): words of at most
- * 16 bytes without a NUL byte first, ascending by (32-bit key hash, the word's
- * 16-byte zero-padded key), then longer words in long-table slot order.  With
+/* Result table: one entry per distinct lowercased word.  Engine order: words
+ * of at most 16 bytes without a NUL byte first, ascending by (32-bit key hash,
+ * second 32-bit key hash, the word's 16-byte zero-padded key) -- the same
+ * whichever reduce kernel grouped the word -- then longer words in long-table
+ * slot order (which can vary from run to run when two long words race for a
+ * slot).  With
  * MOX_F_SORT_BYTES (or after mox_table_sort_bytes): bytewise ascending, Rust
  * String Ord.  The reference's own order is HashMap-random
  * (/root/reference/src/main.rs:177-179).  After mox_gather the root's table

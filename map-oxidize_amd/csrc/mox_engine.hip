@@ -49,6 +49,7 @@ __global__ void k_unit_scan(Work w);
 __global__ void k_split_scatter(Work w);
 __global__ void k_unit_uniq_scan(Work w);
 __global__ void k_reduce_small(Work w);
+__global__ void k_reduce_sort1(Work w);
 __global__ void k_final_scan(Work w);
 __global__ void k_mat(Work w, Corpus c);
 __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
@@ -389,6 +390,9 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_unit_scan");
   hipLaunchKernelGGL(k_split_scatter, dim3(NB), dim3(1024), 0, s, w);
   q.step("k_split_scatter");
+  // count-1 small units first: its hash-collision fallbacks join k_reduce's work list
+  hipLaunchKernelGGL(k_reduce_sort1, dim3(4 * e->n_cu), dim3(256), 0, s, w);  // 4 waves per workgroup, one unit per wave
+  q.step("k_reduce_sort1");
   hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);  // workgroup b: partition b, then the work list
   q.step("k_reduce");
   hipLaunchKernelGGL(k_reduce_small, dim3(8 * e->n_cu), dim3(128), 0, s, w);  // persistent, 8 per CU (SR_THREADS)

@@ -191,7 +191,7 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 // a rotate/xor fold then a two-round multiply-xorshift finaliser.  Bit use:
 // partition = top NB_LOG2 bits, dictionary home slot = low 12 bits, second
 // dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
-// bits.  Final table order is (h32, key), so it is deterministic.
+// bits.  Final table order is (h32, hash32b, key) (key_less), so it is deterministic.
 __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t a = k0 ^ __builtin_rotateleft32(k1, 11) ^ __builtin_rotateleft32(k2, 21) ^ __builtin_rotateleft32(k3, 6);
   a *= 0x9E3779B1u;
@@ -1403,7 +1403,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {
 // contiguous region per map workgroup, streamed by one wave per region) and its
 // weighted records by exact 16-byte key in an LDS hash table of RED_BK buckets
 // x 4 slots (one ds_read_b128 of tags resolves a probe), sort the distinct keys
-// by (h32, key) with an LDS bitonic sort and write them out.  A partition with
+// in key_less order (bucket sort + insertion sort in LDS) and write them out.  A partition with
 // more distinct keys than RED_CAP is redone in 2^k sub-passes over the next
 // hash bits.
 constexpr int RED_BK = 608;    // 2 workgroups per CU: table + sort scratch <= 80 KiB
@@ -1500,15 +1500,30 @@ __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, ui
   return true;
 }
 
+// Table order of short words: (h32, hash32b, key).  Every reduce kernel uses
+// it (k_reduce, k_reduce_small, k_reduce_sort1), so the order does not depend
+// on which kernel a key's unit went to, nor on whether its partition was split.
+__device__ __forceinline__ uint32_t hash32b(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  uint32_t a = k1 ^ __builtin_rotateleft32(k0, 7) ^ __builtin_rotateleft32(k3, 17) ^ __builtin_rotateleft32(k2, 27);
+  a *= 0x2C1B3C6Du;
+  a ^= a >> 12;
+  a *= 0x297A2D39u;
+  a ^= a >> 15;
+  return a;
+}
+__device__ __forceinline__ bool key_less(uint32_t ha, uint4 ka, uint32_t hb, uint4 kb) {
+  if (ha != hb) return ha < hb;
+  const uint32_t ga = hash32b(ka.x, ka.y, ka.z, ka.w), gb = hash32b(kb.x, kb.y, kb.z, kb.w);
+  if (ga != gb) return ga < gb;
+  const uint64_t a0 = ((uint64_t)ka.y << 32) | ka.x, b0 = ((uint64_t)kb.y << 32) | kb.x;
+  if (a0 != b0) return a0 < b0;
+  return (((uint64_t)ka.w << 32) | ka.z) < (((uint64_t)kb.w << 32) | kb.z);
+}
 __device__ __forceinline__ bool red_less(const RedLds& s, uint16_t a, uint16_t b) {
   if (a == 0xFFFF) return false;
   if (b == 0xFFFF) return true;
   const uint32_t* tags = reinterpret_cast<const uint32_t*>(s.tag4);
-  if (tags[a] != tags[b]) return tags[a] < tags[b];
-  const uint4 ka = s.key[a], kb = s.key[b];
-  const uint64_t a0 = ((uint64_t)ka.y << 32) | ka.x, b0 = ((uint64_t)kb.y << 32) | kb.x;
-  if (a0 != b0) return a0 < b0;
-  return (((uint64_t)ka.w << 32) | ka.z) < (((uint64_t)kb.w << 32) | kb.z);
+  return key_less(tags[a], s.key[a], tags[b], s.key[b]);
 }
 
 // hash bits used: partition = top NB_LOG2 bits, then (split partitions) the
@@ -1895,8 +1910,8 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         wbytes = 0;
         continue;
       }
-      // deterministic order (h32, key): bucket sort by the hash bits below the
-      // unit and sub-pass bits, then (h32, key) insertion sort inside each bin
+      // deterministic order (key_less): bucket sort by the hash bits below the
+      // unit and sub-pass bits, then a key_less insertion sort inside each bin
       if (stamp) w.stamps[b * 8 + 2] = __builtin_amdgcn_s_memrealtime();  // all waves done inserting
       const uint32_t nu = s.misc[0];
       const uint32_t bsh = shift0 + kk;
@@ -1979,13 +1994,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 }
 
 // ------------------------------------------------------------------ small-unit reduce
-// Sub-buckets of split partitions with <= SMALL_CAP records (the common case
-// of high-cardinality input).  Persistent 256-thread workgroups (4 per CU) take
-// units grid-strided, no work queue.  Per unit: records into LDS, counting sort
-// by the 10 hash bits below the unit's bits (~0.7 records per bin), (h32, key)
-// insertion sort inside bins, so equal keys are adjacent; run heads are
-// compacted by a block scan and each head sums its run.  Output order (h32,
-// key), as k_reduce.
+// Geometry of k_reduce_small (small units with weighted records, below).
 constexpr int SR_THREADS = 128;
 constexpr int SR_PER = SMALL_CAP / SR_THREADS;  // records (and sorted positions) per thread
 constexpr int SR_BIN_BITS = 9;
@@ -2013,7 +2022,12 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
 struct SmallIn {  // prefetched keys (weighted counts are read at use: rare outside exchange passes)
   uint4 k[SR_PER];
 };
-__device__ __forceinline__ bool small_unit(const UnitDesc& d) { return d.in_n != UNIT_WHOLE && d.in_n + d.win_n <= SMALL_CAP; }
+// k_reduce_sort1 takes the split units of <= SMALL_CAP records that hold only
+// cold (count 1) records; k_reduce_small the small units with weighted records.
+__device__ __forceinline__ bool sort1_unit(const UnitDesc& d) { return d.in_n != UNIT_WHOLE && d.win_n == 0 && d.in_n <= SMALL_CAP; }
+__device__ __forceinline__ bool small_unit(const UnitDesc& d) {
+  return d.in_n != UNIT_WHOLE && d.win_n != 0 && d.in_n + d.win_n <= SMALL_CAP;
+}
 // Descriptor of unit min(u, U - 1): no select on the loaded value, so the load
 // stays in flight until first use (the caller checks u < U there).
 __device__ __forceinline__ UnitDesc load_desc(const Work& w, uint32_t u, uint32_t U) { return w.udesc[u < U ? u : U - 1]; }
@@ -2036,25 +2050,36 @@ __device__ __forceinline__ void load_small(const Work& w, const UnitDesc& d, boo
 }
 
 // Sub-buckets of split partitions with <= SMALL_CAP records (the common case of
-// high-cardinality input).  Persistent 256-thread workgroups (4 per CU) take
+// high-cardinality input).  Persistent 128-thread workgroups (8 per CU) take
 // units grid-strided (no work queue); the next unit's descriptor and records
 // are loaded into registers while the current one is processed.  Per unit:
-// records into LDS, counting sort by the 10 hash bits below the unit's bits
-// (~0.5 records per bin), (h32, key) insertion sort inside bins so equal keys
-// are adjacent, run heads compacted by a scan, each head sums its run.  Output
-// order (h32, key), as k_reduce.
+//  A. records into LDS (key, 32-bit hash, count);
+//  B. group by exact key in an LDS open-addressing table of record indices
+//     (SR_TSLOTS slots, linear probing, CAS claim): the first record of a key
+//     claims a slot and becomes its leader; every other record of that key adds
+//     its count to the leader's -- so a word repeated ~70 times in one unit
+//     (C4 at 16 GiB: every 4-letter word) costs 70 LDS adds, not the O(c^2)
+//     rank of a sort over all records;
+//  C. leaders into 512 bins by the 9 hash bits below the unit's bits (counting
+//     sort), each leader ranked by key_less among the few leaders of its bin;
+//  D. distinct keys written in key_less order, as k_reduce.
+// Barriers are LDS-only (s_waitcnt lgkmcnt(0); s_barrier), so pending global
+// stores are never waited for.
+constexpr int SR_TSLOTS = 1024;  // u16 record indices, two per LDS word; > SMALL_CAP: every record can lead
+constexpr uint32_t SR_EMPTY16 = 0xFFFFu;
+static_assert(SR_TSLOTS >= 2 * (int)SMALL_CAP && SR_TSLOTS == 8 * SR_THREADS, "k_reduce_small table");
+__device__ __forceinline__ uint32_t sr_slot(uint32_t h) { return (h * 0x9E3779B1u) >> (32 - 10); }  // SR_TSLOTS = 2^10
+
 extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work w) {  // 8 per CU (4 waves/SIMD): <= 128 VGPRs
   __shared__ uint4 key[SMALL_CAP];
-  __shared__ unsigned long long cnt[SMALL_CAP];
+  __shared__ unsigned long long acc[SMALL_CAP];  // record count; a leader's: its key's total
   __shared__ uint32_t hh[SMALL_CAP];
-  __shared__ uint16_t rk[SMALL_CAP];
-  __shared__ uint16_t idx[SMALL_CAP];     // records grouped by bin
-  __shared__ uint16_t idx2[SMALL_CAP];    // records in (h32, key) order
-  __shared__ uint32_t bins[SR_BINS / 2];  // u16 pairs: counts, then exclusive starts
-  __shared__ uint8_t mixed[SR_BINS];      // bin holds more than one distinct key
-  __shared__ uint16_t hp[SMALL_CAP + 1];  // sorted position of the o-th run head
-  __shared__ uint32_t wsa[SR_THREADS / 64], wsb[SR_THREADS / 64];
+  __shared__ uint32_t tab[SR_TSLOTS / 2];         // leader record index per slot, u16 pairs (0xFFFF = free)
+  __shared__ uint16_t idx2[SMALL_CAP];            // leaders in key_less order
+  __shared__ uint32_t bins[SR_BINS / 2];          // u16 pairs: leader counts, then exclusive starts
+  __shared__ uint32_t wsa[SR_THREADS / 64];
   __shared__ uint32_t sbytes;
+  uint16_t* idx = reinterpret_cast<uint16_t*>(tab);  // leaders grouped by bin (the table is dead by then)
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (w.ctl->overflow & OVF_RERUN) return;
   const uint32_t U = (uint32_t)w.ctl->n_units;
@@ -2066,7 +2091,8 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
   if (tid == 0) { dring[0] = load_desc(w, u, U); dring[1] = load_desc(w, u + G, U); sbytes = 0; }
   bins[tid] = 0;
   bins[tid + SR_THREADS] = 0;
-  for (int i = tid; i < SR_BINS; i += SR_THREADS) mixed[i] = 0;
+#pragma unroll
+  for (int q = 0; q < SR_TSLOTS / 2 / SR_THREADS; q++) tab[tid + q * SR_THREADS] = 0xFFFFFFFFu;
   lds_barrier();
   SmallIn in;
   {
@@ -2086,20 +2112,18 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
     if (cur_small && !MOX_CHK(w, d.in_off + d.in_n <= w.split_k_cap && d.win_off + d.win_n <= w.split_w_cap &&
                                      d.rec_off + d.in_n + d.win_n <= w.uniq_cap, CHK_SMALL_DESC))
       cur_small = false;
-    const uint32_t n = d.in_n + d.win_n, shift = NB_LOG2 + d.kk;
-    // this unit's records into LDS + bin counts (bins were zeroed by the previous unit)
+    const uint32_t n = d.in_n + d.win_n, nk = d.in_n, shift = NB_LOG2 + d.kk;
+    uint32_t h[SR_PER];
+    // A. this unit's records into LDS
     if (cur_small) {
 #pragma unroll
       for (int j = 0; j < SR_PER; j++) {
         const uint32_t i = tid + j * SR_THREADS;
+        h[j] = hash32(in.k[j].x, in.k[j].y, in.k[j].z, in.k[j].w);
         if (i < n) {
-          const uint32_t h = hash32(in.k[j].x, in.k[j].y, in.k[j].z, in.k[j].w);
-          const uint32_t bn = hbits(h, shift, SR_BIN_BITS);
           key[i] = in.k[j];
-          cnt[i] = i < d.in_n ? 1ull : w.split_w[d.win_off + (i - d.in_n)].count;
-          hh[i] = h;
-          const uint32_t old = atomicAdd(&bins[bn >> 1], 1u << (16 * (bn & 1)));
-          rk[i] = (uint16_t)((old >> (16 * (bn & 1))) & 0xFFFFu);
+          hh[i] = h[j];
+          acc[i] = i < nk ? 1ull : w.split_w[d.win_off + (i - nk)].count;
         }
       }
     }
@@ -2111,6 +2135,76 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
     if (cur_small) {
       lds_barrier();
       SR_MARK(0);
+      // B. group by key: claim a slot, or add to the leader holding this key.
+      // The thread's records are probed in one interleaved loop (one probe step
+      // per iteration, moving to its next record when one is placed), so a
+      // wave iterates max over lanes of the sum of its probe lengths rather
+      // than the sum over records of the wave's longest probe.
+      {
+        uint32_t j = 0, sl = sr_slot(h[0]);
+        uint32_t i = tid;
+        bool more = i < n;
+        while (__builtin_amdgcn_ballot_w64(more) != 0) {
+          if (more) {
+            uint4 k = in.k[0];
+            uint32_t hj = h[0];
+#pragma unroll
+            for (int q = 1; q < SR_PER; q++)
+              if (j == (uint32_t)q) { k = in.k[q]; hj = h[q]; }
+            const uint32_t wi = sl >> 1, sh = 16 * (sl & 1);
+            uint32_t v = __hip_atomic_load(&tab[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            uint32_t cur = (v >> sh) & 0xFFFFu;
+            bool placed = false;
+            if (cur == SR_EMPTY16) {
+              const uint32_t old = atomicCAS(&tab[wi], v, (v & ~(0xFFFFu << sh)) | (i << sh));
+              if (old == v) placed = true;   // this record leads its key
+              else cur = (old >> sh) & 0xFFFFu;  // lost the race (or the other half changed): look again
+            }
+            if (!placed && cur != SR_EMPTY16) {
+              if (hh[cur] == hj && key_eq16(key[cur], k)) {
+                atomicAdd(&acc[cur], acc[i]);
+                placed = true;
+              } else {
+                sl = (sl + 1) & (SR_TSLOTS - 1);
+              }
+            }
+            if (placed) {
+              j++;
+              i += SR_THREADS;
+              more = j < (uint32_t)SR_PER && i < n;
+              uint32_t hn = h[0];
+#pragma unroll
+              for (int q = 1; q < SR_PER; q++)
+                if (j == (uint32_t)q) hn = h[q];
+              sl = sr_slot(hn);
+            }
+          }
+        }
+      }
+      lds_barrier();
+      SR_MARK(1);
+      // C. leaders (table slots) into bins; arrival rank inside the bin.
+      // Thread t reads table words t, t + 128, t + 256, t + 384 (8 slots).
+      constexpr int SQ = SR_TSLOTS / SR_THREADS;  // slots per thread
+      uint32_t L[SQ], rkk[SQ], bnn[SQ];
+#pragma unroll
+      for (int q = 0; q < SQ / 2; q++) {
+        const uint32_t v = tab[tid + q * SR_THREADS];
+        L[2 * q] = v & 0xFFFFu;
+        L[2 * q + 1] = v >> 16;
+      }
+#pragma unroll
+      for (int q = 0; q < SQ; q++) {
+        rkk[q] = 0;
+        bnn[q] = 0;
+        if (L[q] != SR_EMPTY16) {
+          bnn[q] = hbits(hh[L[q]], shift, SR_BIN_BITS);
+          const uint32_t old = atomicAdd(&bins[bnn[q] >> 1], 1u << (16 * (bnn[q] & 1)));
+          rkk[q] = (old >> (16 * (bnn[q] & 1))) & 0xFFFFu;
+        }
+      }
+      lds_barrier();
+      uint32_t nu;
       {  // exclusive scan of the bin counts: bins 4t..4t+3 per thread
         const uint32_t p0 = bins[2 * tid], p1 = bins[2 * tid + 1];
         const uint32_t c0 = p0 & 0xFFFFu, c1 = p0 >> 16, c2 = p1 & 0xFFFFu, c3 = p1 >> 16;
@@ -2118,138 +2212,67 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
         if (lane == 63) wsa[wv] = incl;
         lds_barrier();
         uint32_t ex = incl - (c0 + c1 + c2 + c3);
-        for (int k = 0; k < wv; k++) ex += wsa[k];
+        nu = 0;
+        for (int k = 0; k < SR_THREADS / 64; k++) { if (k < wv) ex += wsa[k]; nu += wsa[k]; }
         bins[2 * tid] = ex | ((ex + c0) << 16);
         bins[2 * tid + 1] = (ex + c0 + c1) | ((ex + c0 + c1 + c2) << 16);
       }
       lds_barrier();
+      // leaders grouped by bin (idx overlays the table, read completely above)
 #pragma unroll
-      for (int j = 0; j < SR_PER; j++) {
-        const uint32_t i = tid + j * SR_THREADS;
-        if (i < n) idx[bin16[hbits(hh[i], shift, SR_BIN_BITS)] + rk[i]] = (uint16_t)i;
-      }
+      for (int q = 0; q < SQ; q++)
+        if (L[q] != SR_EMPTY16) idx[bin16[bnn[q]] + rkk[q]] = (uint16_t)L[q];
       lds_barrier();
-      // a bin is "mixed" when a member differs from its first member; in the
-      // others (one key, possibly repeated ~70 times in C4) the arrival rank rk
-      // is already a valid order
+      // final position: bin start + rank by (h32, hash32b, key) among the bin's leaders
+      // (distinct keys: the order is strict; bins hold ~0.6 leaders on average)
 #pragma unroll
-      for (int j = 0; j < SR_PER; j++) {
-        const uint32_t i = tid + j * SR_THREADS;
-        if (i < n) {
-          const uint32_t bn = hbits(hh[i], shift, SR_BIN_BITS);
-          const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
-          if (hi - lo > 1) {
-            const uint32_t f = idx[lo];
-            if (f != i && (hh[f] != hh[i] || !key_eq16(key[f], key[i]))) mixed[bn] = 1;
+      for (int q = 0; q < SQ; q++) {
+        if (L[q] == SR_EMPTY16) continue;
+        const uint32_t x = L[q];
+        const uint32_t lo = bin16[bnn[q]], hi = bnn[q] + 1 < SR_BINS ? bin16[bnn[q] + 1] : nu;
+        uint32_t r = 0;
+        if (hi - lo > 1) {
+          const uint32_t hx = hh[x];
+          const uint4 kx = key[x];
+          for (uint32_t m = lo; m < hi; m++) {
+            const uint32_t y = idx[m];
+            r += key_less(hh[y], key[y], hx, kx) ? 1u : 0u;
           }
         }
+        idx2[lo + r] = (uint16_t)x;
       }
-      lds_barrier();
-      // final position of each record: its bin start + its (h32, key) rank among
-      // the bin's records, ties between equal keys broken by record index (they
-      // are summed, so their order is immaterial).  O(bin size) per record, so a
-      // bin full of one repeated word costs no thread more than its own scan.
-#pragma unroll 1
-      for (int j = 0; j < SR_PER; j++) {
-        const uint32_t i = tid + j * SR_THREADS;
-        if (i < n) {
-          const uint32_t hx = hh[i];
-          const uint32_t bn = hbits(hx, shift, SR_BIN_BITS);
-          const uint32_t lo = bin16[bn], hi = bn + 1 < SR_BINS ? bin16[bn + 1] : n;
-          uint32_t r = 0;
-          if (hi - lo > 1 && !mixed[bn]) {
-            r = rk[i];
-          } else if (hi - lo > 1) {
-            const uint4 kx = key[i];
-            const uint64_t x0 = ((uint64_t)kx.y << 32) | kx.x, x1 = ((uint64_t)kx.w << 32) | kx.z;
-            // batches of 2 with branch-free bodies: the LDS reads of a batch are
-            // issued together (a bin of one repeated word costs ~c/2 latencies)
-            for (uint32_t q0 = lo; q0 < hi; q0 += 2) {
-              uint32_t y[2], hy[2];
-              uint4 ky[2];
-#pragma unroll
-              for (int t = 0; t < 2; t++) y[t] = idx[q0 + t < hi ? q0 + t : lo];
-#pragma unroll
-              for (int t = 0; t < 2; t++) { hy[t] = hh[y[t]]; ky[t] = key[y[t]]; }
-#pragma unroll
-              for (int t = 0; t < 2; t++) {
-                const uint64_t y0 = ((uint64_t)ky[t].y << 32) | ky[t].x, y1 = ((uint64_t)ky[t].w << 32) | ky[t].z;
-                const bool kl = y0 != x0 ? y0 < x0 : (y1 != x1 ? y1 < x1 : y[t] < i);
-                const bool less = hy[t] != hx ? hy[t] < hx : kl;
-                r += (q0 + t < hi && less) ? 1u : 0u;
-              }
-            }
-          }
-          idx2[lo + r] = (uint16_t)i;
-        }
-      }
-      SR_MARK(1);
       lds_barrier();
       SR_MARK(2);
-      bins[tid] = 0;  // bin starts and flags are dead after the sort: zero for the next unit
-      bins[tid + SR_THREADS] = 0;
-      for (int i = tid; i < SR_BINS; i += SR_THREADS) mixed[i] = 0;
-      // run heads at sorted positions 4t..4t+3 -> output index by scan
-      uint32_t hm = 0, nh = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) {
-        const uint32_t p = 4 * tid + j;
-        if (p < n && (p == 0 || !key_eq16(key[idx2[p]], key[idx2[p - 1]]))) { hm |= 1u << j; nh++; }
-      }
-      const uint32_t incl = wave_incl_scan(nh);
-      if (lane == 63) wsb[wv] = incl;
-      lds_barrier();
-      uint32_t o = incl - nh, nu = 0;
-      for (int k = 0; k < SR_THREADS / 64; k++) { if (k < wv) o += wsb[k]; nu += wsb[k]; }
-      // run lengths from the next head's position (all counts are 1 in a unit
-      // without weighted records); units with weighted records sum their runs
-      const bool ones = d.win_n == 0;
-      if (ones) {
-        uint32_t oo = o;
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          if ((hm >> j) & 1u) hp[oo++] = (uint16_t)(4 * tid + j);
-        if (tid == 0) hp[nu] = (uint16_t)n;
-        lds_barrier();
-      }
+      // D. distinct keys out; reset the table and the bins for the next unit
       uint32_t lb = 0;
-#pragma unroll 1
-      for (int j = 0; j < 4; j++) {
-        if (!((hm >> j) & 1u)) continue;
-        const uint32_t p = 4 * tid + j;
-        const uint4 k = key[idx2[p]];
-        unsigned long long c = cnt[idx2[p]];
-        if (ones) c = (unsigned long long)(hp[o + 1] - p);
-        // the run of equal keys after p, in batches of 2 (reads issued together)
-        else for (uint32_t q0 = p + 1; q0 < n; q0 += 2) {
-          uint32_t y[2];
 #pragma unroll
-          for (int t = 0; t < 2; t++) y[t] = idx2[q0 + t < n ? q0 + t : p];
-          bool go = true;
-#pragma unroll
-          for (int t = 0; t < 2; t++) {
-            go = go && q0 + t < n && key_eq16(key[y[t]], k);
-            if (go) c += cnt[y[t]];
+      for (int q = 0; q < SR_PER; q++) {
+        const uint32_t p = tid + q * SR_THREADS;
+        if (p < nu) {
+          const uint32_t x = idx2[p];
+          const uint4 k = key[x];
+          if (MOX_CHK(w, p < n && d.rec_off + p < w.uniq_cap, CHK_SMALL_OUT)) {  // distinct keys <= records
+            w.uk[d.rec_off + p] = k;
+            w.uc[d.rec_off + p] = acc[x];
           }
-          if (!go) break;
+          lb += key_len16(k);
         }
-        if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {  // distinct keys <= records
-          w.uk[d.rec_off + o] = k;
-          w.uc[d.rec_off + o] = c;
-        }
-        lb += key_len16(k);
-        o++;
       }
       if (lb) atomicAdd(&sbytes, lb);
       if (tid == 0) w.u_uniq[u] = nu;  // summed per partition by k_unit_uniq_scan
+      lds_barrier();  // every read of idx (= the table) is done before the table is reset
+      bins[tid] = 0;
+      bins[tid + SR_THREADS] = 0;
+#pragma unroll
+      for (int q = 0; q < SR_TSLOTS / 2 / SR_THREADS; q++) tab[tid + q * SR_THREADS] = 0xFFFFFFFFu;
     } else {
       // A unit this kernel skips (whole partition or > SMALL_CAP records) has
       // no barrier above: without this one, wave 0 could overwrite
       // dring[it & 1] before a lagging wave has read it as d at the top of
       // this iteration.  That wave would then take unit u + 2G for u, disagree
       // with the others on cur_small, pair its barriers with theirs and write
-      // its scan results to wrong (possibly out-of-range) uk / uc positions:
-      // the intermittent illegal-address faults of round 1.
+      // its results to wrong (possibly out-of-range) uk / uc positions: the
+      // intermittent illegal-address faults of round 1.
       lds_barrier();
     }
     if (tid == 0) dring[it & 1] = dnn;
@@ -2263,6 +2286,192 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
     for (int k = 0; k < 4; k++) atomicAdd(&w.ctl->dbg_cnt[k], (unsigned long long)cyc[k]);
 #endif
 #undef SR_MARK
+}
+
+// ------------------------------------------------------------------ single-wave sort reduce
+// k_reduce_sort1: every split unit of <= SMALL_CAP count-1 records (the bulk of
+// high-cardinality input: C4 at 16 GiB has 4.2 M units of ~370 records) is
+// reduced by ONE wave, with no workgroup barrier at all:
+//  1. its records are loaded (8 per lane, coalesced) into the wave's LDS key
+//     array, and each becomes a 32-bit sort key: 23 bits of (the key hash's
+//     bits below the unit bits, hash32b), then the record index (9 bits;
+//     padding = ~0 sorts last);
+//  2. a bitonic sort of the 512 keys in registers (8 per lane; in-lane
+//     compare-exchanges, cross-lane ones by DPP or ds_bpermute);
+//  3. runs of equal hash bits are the keys' repeats: run heads (verified by
+//     comparing the 16-byte keys of every adjacent pair) are compacted by a
+//     wave prefix sum, run lengths come from the next head's position, and the
+//     distinct keys are written in sort order.
+// A unit where two different keys share the 23 sort-key hash bits (about 0.5 %
+// of C4's units) is not written here: it goes on k_reduce's work list
+// (big_units), which resolves it exactly.  Elsewhere the sort-key order is
+// the table order every reduce kernel uses (key_less).
+constexpr int S1_PER = SMALL_CAP / 64;  // records per lane
+constexpr int S1_WAVES = 4;             // waves per workgroup, one unit each
+static_assert(S1_PER == 8, "k_reduce_sort1: 8 records per lane");
+// value of lane (lane ^ M)
+template <int M>
+__device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
+  if constexpr (M == 1) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  if constexpr (M == 2) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
+  return (uint32_t)__shfl_xor((int)v, M);
+}
+// bitonic compare-exchange with the lane (lane ^ M): the lower lane keeps the
+// minimum when this block sorts ascending
+template <int M>
+__device__ __forceinline__ void s1_cross(uint32_t (&v)[S1_PER], int lane, uint32_t k) {
+  const bool keep_min = ((lane & M) == 0) == (((uint32_t)(lane * S1_PER) & k) == 0);
+#pragma unroll
+  for (int s = 0; s < S1_PER; s++) {
+    const uint32_t pv = xor_lane<M>(v[s]);
+    v[s] = ((pv < v[s]) == keep_min) ? pv : v[s];
+  }
+}
+__device__ __forceinline__ void s1_inlane(uint32_t (&v)[S1_PER], int lane, uint32_t k, int j) {
+#pragma unroll
+  for (int s = 0; s < S1_PER; s++) {
+    const int t = s ^ j;
+    if (t > s) {
+      const bool asc = ((uint32_t)(lane * S1_PER + s) & k) == 0;
+      const uint32_t a = v[s], b = v[t];
+      const bool sw = (a > b) == asc;
+      v[s] = sw ? b : a;
+      v[t] = sw ? a : b;
+    }
+  }
+}
+__device__ __forceinline__ void s1_sort(uint32_t (&v)[S1_PER], int lane) {
+#pragma unroll
+  for (uint32_t k = 2; k <= 512; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 8) {
+        switch (j >> 3) {
+          case 1: s1_cross<1>(v, lane, k); break;
+          case 2: s1_cross<2>(v, lane, k); break;
+          case 4: s1_cross<4>(v, lane, k); break;
+          case 8: s1_cross<8>(v, lane, k); break;
+          case 16: s1_cross<16>(v, lane, k); break;
+          default: s1_cross<32>(v, lane, k); break;
+        }
+      } else {
+        s1_inlane(v, lane, k, (int)j);
+      }
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Work w) {
+  __shared__ uint4 skey[S1_WAVES][SMALL_CAP];
+  __shared__ uint16_t shp[S1_WAVES][SMALL_CAP + 2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint4* key = skey[wv];
+  uint16_t* hp = shp[wv];
+  if (w.ctl->overflow & OVF_RERUN) return;
+  const uint32_t U = (uint32_t)w.ctl->n_units;
+  const uint32_t GW = gridDim.x * S1_WAVES;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  // software pipeline: the next unit's descriptor is loaded one unit ahead and
+  // its records are in flight (registers) while this unit is sorted
+  auto ok_unit = [&](const UnitDesc& dd) {
+    return sort1_unit(dd) && MOX_CHK(w, dd.in_off + dd.in_n <= w.split_k_cap && dd.rec_off + dd.in_n <= w.uniq_cap,
+                                     CHK_SMALL_DESC);
+  };
+  auto load_keys = [&](const UnitDesc& dd, bool ok, uint4 (&kk)[S1_PER]) {
+    const uint4* src = w.split_k + (ok ? dd.in_off : 0);
+    const uint32_t nn = ok ? dd.in_n : 0u;
+#pragma unroll
+    for (int s = 0; s < S1_PER; s++) {
+      const uint32_t i = (uint32_t)(s * 64 + lane);
+      const u32x4 x = *reinterpret_cast<const u32x4*>(src + (i < nn ? i : 0u));
+      kk[s] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+  uint32_t u = blockIdx.x * S1_WAVES + wv;
+  if (u >= U) return;
+  UnitDesc d = w.udesc[u];
+  UnitDesc dn = w.udesc[u + GW < U ? u + GW : U - 1];
+  uint4 k[S1_PER];
+  load_keys(d, ok_unit(d), k);
+  for (; u < U; u += GW) {
+    const UnitDesc dnn = w.udesc[u + 2 * GW < U ? u + 2 * GW : U - 1];
+    uint4 kn[S1_PER];
+    load_keys(dn, u + GW < U && ok_unit(dn), kn);
+    const bool ok = ok_unit(d);
+    const uint32_t n = d.in_n, shift = NB_LOG2 + d.kk;
+    if (ok) {
+      uint32_t v[S1_PER];
+#pragma unroll
+      for (int s = 0; s < S1_PER; s++) {
+        const uint32_t i = (uint32_t)(s * 64 + lane);
+        const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
+        // sort key: the top 23 bits of (h32 bits below the unit, hash32b) --
+        // the leading bits of the table order key_less -- then the record
+        // index (9 bits).  Padding ~0 cannot tie a real key: with padding
+        // present every real index is <= 510.
+        const uint32_t pre = (h << shift) | (hb >> (32 - shift));
+        v[s] = i < n ? ((pre & ~511u) | i) : ~0u;
+        if (i < n) key[i] = k[s];
+      }
+      s1_sort(v, lane);
+      // run heads: hash bits differ from the previous position's
+      uint32_t prev = from_prev_lane(v[S1_PER - 1]);
+      uint32_t hm = 0, bad = 0;
+      wave_lds_fence();  // key[] written by every lane
+#pragma unroll
+      for (int s = 0; s < S1_PER; s++) {
+        const uint32_t p = (uint32_t)(lane * S1_PER + s);
+        const bool valid = p < n;
+        const bool head = valid && (p == 0 || (v[s] >> 9) != (prev >> 9));
+        if (head) hm |= 1u << s;
+        if (valid && !head) bad |= key_eq16(key[v[s] & 511u], key[prev & 511u]) ? 0u : 1u;
+        prev = v[s];
+      }
+      if (__any(bad != 0)) {  // two keys share the sort-key hash bits: k_reduce resolves this unit
+        if (lane == 0) {
+          const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
+          if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
+        }
+      } else {
+        const uint32_t nh = (uint32_t)__popc(hm);
+        const uint32_t incl = wave_incl_scan(nh);
+        const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        uint32_t o = incl - nh;
+#pragma unroll
+        for (int s = 0; s < S1_PER; s++)
+          if ((hm >> s) & 1u) hp[o++] = (uint16_t)(lane * S1_PER + s);
+        if (lane == 0) hp[nu] = (uint16_t)n;
+        wave_lds_fence();
+        o = incl - nh;
+        uint32_t lb = 0;
+#pragma unroll
+        for (int s = 0; s < S1_PER; s++) {
+          if ((hm >> s) & 1u) {
+            const uint32_t p = (uint32_t)(lane * S1_PER + s);
+            const uint4 kk = key[v[s] & 511u];
+            if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {
+              w.uk[d.rec_off + o] = kk;
+              w.uc[d.rec_off + o] = (unsigned long long)(hp[o + 1] - p);
+            }
+            lb += key_len16(kk);
+            o++;
+          }
+        }
+        uint32_t tb = lb;
+        for (int off = 32; off > 0; off >>= 1) tb += __shfl_xor(tb, off);
+        if (lane == 0) {
+          w.u_uniq[u] = nu;
+          w.u_bytes[u] = tb;
+        }
+      }  // no collision
+      wave_lds_fence();  // this unit's LDS reads before the next unit's writes
+    }  // ok
+    d = dn;
+    dn = dnn;
+#pragma unroll
+    for (int s = 0; s < S1_PER; s++) k[s] = kn[s];
+  }
 }
 
 // ------------------------------------------------------------------ table directory
@@ -2365,56 +2574,63 @@ __device__ __forceinline__ void exscan2_256(uint32_t a, uint32_t b, uint32_t (*w
 }
 
 // k_mat (256-thread workgroups): the dense table in one pass -- counts, byte
-// offsets and bytes of every short word (unit by unit, a workgroup scan of the
-// key lengths inside the unit) and of every long word (slice b by workgroup
-// b: scan of the occupied slots), and lpos for the exchange pack.
-extern "C" __global__ __launch_bounds__(256) void k_mat(Work w, Corpus c) {
+// offsets and bytes of every short word, then of every long word, and lpos for
+// the exchange pack.
+//  * short words: one WAVE per unit (no workgroup barrier), 64 words per step
+//    (lane = word): a DPP wave scan of the key lengths gives the byte offsets;
+//    the step's key bytes are assembled in the wave's LDS stage at their
+//    offset from the 16-byte line below the step's first byte, then written
+//    with aligned 16-byte stores; bytes of the partial first and last lines
+//    (shared with the neighbouring steps / units) are stored one by one;
+//  * long words: long-table slice b by workgroup b (scan of the occupied
+//    slots), after every wave of the workgroup is done with its units.
+constexpr int MAT_WAVES = 4;
+extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpus c) {
   __shared__ uint32_t ws[4][2];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[256 * 16 + 32];  // one chunk's key bytes
+  __shared__ __attribute__((aligned(16))) uint8_t stage[MAT_WAVES][64 * 16 + 32];
   if (!table_ok(w)) return;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t U = (uint32_t)w.ctl->n_units;
-  for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
+  uint8_t* st = stage[wv];
+  for (uint32_t u = blockIdx.x * MAT_WAVES + wv; u < U; u += gridDim.x * MAT_WAVES) {
     const UnitDesc ud = w.udesc[u];
     const uint64_t n = w.u_uniq[u], src0 = ud.rec_off;
     const uint64_t dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
     uint64_t boff = w.bytes_off[ud.part] + w.u_bytes_off[u];
-    for (uint64_t i0 = 0; i0 < n; i0 += 256) {
-      const uint64_t i = i0 + tid;
+    for (uint64_t i0 = 0; i0 < n; i0 += 64) {
+      const uint64_t i = i0 + lane;
       uint4 k = make_uint4(0, 0, 0, 0);
       uint32_t len = 0;
-      if (i < n) { k = w.uk[src0 + i]; len = key_len16(k); }
-      uint32_t ex, dummy, tot, t2;
-      exscan2_256(len, 0, ws, ex, dummy, tot, t2);
-      // the chunk's bytes [boff, boff + tot) are staged in LDS at their offset
-      // from the 16-byte line below boff, then written as aligned 16-byte stores
-      // (bytes at the partial first/last line one by one: neighbours share them)
+      unsigned long long cnt = 0;
+      if (i < n) { k = w.uk[src0 + i]; cnt = w.uc[src0 + i]; len = key_len16(k); }
+      const uint32_t incl = wave_incl_scan(len);
+      const uint32_t ex = incl - len, tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       const uint64_t gbase = boff & ~15ull;
       const uint32_t sh = (uint32_t)(boff - gbase);
       if (i < n && MOX_CHK(w, dst0 + i < w.table_cap && boff + ex + len <= w.bytes_cap, CHK_MAT_ROW)) {
-        const uint64_t o = boff + ex;
-        w.t_counts[dst0 + i] = w.uc[src0 + i];
-        w.t_offs[dst0 + i] = o;
+        w.t_counts[dst0 + i] = cnt;
+        w.t_offs[dst0 + i] = boff + ex;
         const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-        for (uint32_t j = 0; j < len; j++) stage[sh + ex + j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
+#pragma unroll
+        for (uint32_t j = 0; j < 16; j++)
+          if (j < len) st[sh + ex + j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
       }
-      __syncthreads();
-      {
-        const uint64_t ge = boff + tot;
-        const uint64_t a0 = (boff + 15) & ~15ull, a1 = ge & ~15ull;  // whole lines [a0, a1)
-        if (a0 < a1) {
-          for (uint64_t q = a0 + 16ull * tid; q < a1; q += 16ull * 256)
-            *reinterpret_cast<uint4*>(w.t_bytes + q) = *reinterpret_cast<const uint4*>(stage + (q - gbase));
-          if (tid < 16 && boff + tid < a0) w.t_bytes[boff + tid] = stage[sh + tid];
-          if (tid >= 16 && tid < 32 && a1 + (tid - 16) < ge) w.t_bytes[a1 + (tid - 16)] = stage[(a1 - gbase) + (tid - 16)];
-        } else if (tid < 32 && boff + tid < ge) {
-          w.t_bytes[boff + tid] = stage[sh + tid];
-        }
+      wave_lds_fence();
+      const uint64_t ge = boff + tot;
+      const uint64_t a0 = (boff + 15) & ~15ull, a1 = ge & ~15ull;  // whole lines [a0, a1)
+      if (a0 < a1) {
+        for (uint64_t q = a0 + 16ull * lane; q < a1; q += 16ull * 64)
+          *reinterpret_cast<uint4*>(w.t_bytes + q) = *reinterpret_cast<const uint4*>(st + (q - gbase));
+        if (lane < 16 && boff + lane < a0) w.t_bytes[boff + lane] = st[sh + lane];
+        if (lane >= 16 && lane < 32 && a1 + (lane - 16) < ge) w.t_bytes[a1 + (lane - 16)] = st[(a1 - gbase) + (lane - 16)];
+      } else if (lane < 32 && boff + lane < ge) {
+        w.t_bytes[boff + lane] = st[sh + lane];
       }
-      __syncthreads();
+      wave_lds_fence();  // the stage is rewritten by the next step
       boff += tot;
     }
   }
+  __syncthreads();
   // long words: slice b = slots [b L, (b + 1) L), in slot order
   const uint64_t ns = w.ctl->n_short, sb = w.ctl->short_bytes, L = w.long_cap / NB;
   for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {

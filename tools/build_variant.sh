@@ -1,0 +1,18 @@
+#!/bin/bash
+# Build an A/B variant of libmox.so with extra -D flags into build/var_NAME/
+# (bench.py / tests load it with MOX_LIB=build/var_NAME/libmox.so).
+# Usage: bash tools/build_variant.sh NAME "-DFLAG ..."
+set -e
+NAME=$1; shift
+FLAGS="$*"
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$ROOT/build/var_$NAME
+mkdir -p $OUT
+H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result"
+C=$ROOT/map-oxidize_amd/csrc
+$H -mllvm -amdgpu-sched-strategy=max-memory-clause $FLAGS -c $C/mox_kernels.hip -o $OUT/k.o &
+$H $FLAGS -c $C/mox_engine.hip -o $OUT/e.o &
+g++ -O3 -std=c++17 -fPIC -c $C/mox_table.cpp -o $OUT/t.o &
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libmox.so $OUT/k.o $OUT/e.o $OUT/t.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+echo "built $OUT/libmox.so"
