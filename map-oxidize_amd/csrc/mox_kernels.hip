@@ -2576,27 +2576,83 @@ __device__ __forceinline__ void exscan2_256(uint32_t a, uint32_t b, uint32_t (*w
 // k_mat (256-thread workgroups): the dense table in one pass -- counts, byte
 // offsets and bytes of every short word, then of every long word, and lpos for
 // the exchange pack.
-//  * short words: one WAVE per unit (no workgroup barrier), 64 words per step
-//    (lane = word): a DPP wave scan of the key lengths gives the byte offsets;
-//    the step's key bytes are assembled in the wave's LDS stage at their
-//    offset from the 16-byte line below the step's first byte, then written
-//    with aligned 16-byte stores; bytes of the partial first and last lines
-//    (shared with the neighbouring steps / units) are stored one by one;
+//  * short words: a whole partition by one workgroup, each unit of a split
+//    partition by one wave (no workgroup barrier).  Either way a step covers
+//    a run of words (lane or thread = word): a scan of the key lengths gives the byte offsets, the
+//    step's key bytes are assembled in LDS at their offset from the 16-byte
+//    line below the step's first byte and written with aligned 16-byte
+//    stores; bytes of the partial first and last lines (shared with the
+//    neighbouring steps / units) are stored one by one;
 //  * long words: long-table slice b by workgroup b (scan of the occupied
 //    slots), after every wave of the workgroup is done with its units.
 constexpr int MAT_WAVES = 4;
+// Writes the staged bytes of [boff, boff + tot) (stage = LDS image of the
+// 16-byte lines from gbase = boff & ~15) by `nt` threads with thread index t.
+__device__ __forceinline__ void mat_flush(const Work& w, const uint8_t* st, uint64_t boff, uint64_t tot, uint32_t t,
+                                          uint32_t nt) {
+  const uint64_t gbase = boff & ~15ull, ge = boff + tot;
+  const uint64_t a0 = (boff + 15) & ~15ull, a1 = ge & ~15ull;  // whole lines [a0, a1)
+  if (a0 < a1) {
+    for (uint64_t q = a0 + 16ull * t; q < a1; q += 16ull * nt)
+      *reinterpret_cast<uint4*>(w.t_bytes + q) = *reinterpret_cast<const uint4*>(st + (q - gbase));
+    if (t < 16 && boff + t < a0) w.t_bytes[boff + t] = st[(boff - gbase) + t];
+    if (t >= 16 && t < 32 && a1 + (t - 16) < ge) w.t_bytes[a1 + (t - 16)] = st[(a1 - gbase) + (t - 16)];
+  } else if (t < 32 && boff + t < ge) {
+    w.t_bytes[boff + t] = st[(boff - gbase) + t];
+  }
+}
+// One word of a step: its count, offset and (staged) bytes.
+__device__ __forceinline__ void mat_word(const Work& w, uint8_t* st, uint64_t dst, uint64_t boff, uint32_t ex, uint4 k,
+                                         uint32_t len, unsigned long long cnt) {
+  if (!MOX_CHK(w, dst < w.table_cap && boff + ex + len <= w.bytes_cap, CHK_MAT_ROW)) return;
+  w.t_counts[dst] = cnt;
+  w.t_offs[dst] = boff + ex;
+  const uint32_t sh = (uint32_t)(boff & 15ull);
+  const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+#pragma unroll
+  for (uint32_t j = 0; j < 16; j++)
+    if (j < len) st[sh + ex + j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
+}
 extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpus c) {
   __shared__ uint32_t ws[4][2];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[MAT_WAVES][64 * 16 + 32];
+  constexpr int WSTAGE = 64 * 16 + 32;  // one wave's step: 64 keys + the partial lines
+  // per-wave stages; the workgroup path uses all of it as one 256-key stage
+  __shared__ __attribute__((aligned(16))) uint8_t stage[MAT_WAVES * WSTAGE];
+  static_assert(MAT_WAVES * WSTAGE >= 64 * MAT_WAVES * 16 + 32, "k_mat workgroup stage");
   if (!table_ok(w)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint32_t U = (uint32_t)w.ctl->n_units;
-  uint8_t* st = stage[wv];
+  // whole partitions (Zipf text: ~1,400 words each): workgroup b takes partition b
+  for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
+    if (w.b_kk[b] != 0) continue;  // split: its units go to the waves below
+    const uint32_t v = w.u_base[b];
+    const uint64_t n = w.u_uniq[v];
+    const UnitDesc ud = w.udesc[v];
+    const uint64_t src0 = ud.rec_off, dst0 = w.uniq_off[b] + w.u_uniq_off[v];
+    uint64_t boff = w.bytes_off[b] + w.u_bytes_off[v];
+    for (uint64_t i0 = 0; i0 < n; i0 += 64 * MAT_WAVES) {
+      const uint64_t i = i0 + tid;
+      uint4 k = make_uint4(0, 0, 0, 0);
+      uint32_t len = 0;
+      unsigned long long cnt = 0;
+      if (i < n) { k = w.uk[src0 + i]; cnt = w.uc[src0 + i]; len = key_len16(k); }
+      uint32_t ex, dummy, tot, t2;
+      exscan2_256(len, 0, ws, ex, dummy, tot, t2);
+      if (i < n) mat_word(w, stage, dst0 + i, boff, ex, k, len, cnt);
+      __syncthreads();
+      mat_flush(w, stage, boff, tot, (uint32_t)tid, 64 * MAT_WAVES);
+      __syncthreads();
+      boff += tot;
+    }
+  }
+  // units of split partitions (high-cardinality input: ~330 words each): one wave each
   for (uint32_t u = blockIdx.x * MAT_WAVES + wv; u < U; u += gridDim.x * MAT_WAVES) {
     const UnitDesc ud = w.udesc[u];
-    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off;
-    const uint64_t dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
+    if (ud.in_n == UNIT_WHOLE) continue;
+    const uint64_t n = w.u_uniq[u];
+    const uint64_t src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
     uint64_t boff = w.bytes_off[ud.part] + w.u_bytes_off[u];
+    uint8_t* st = stage + wv * WSTAGE;
     for (uint64_t i0 = 0; i0 < n; i0 += 64) {
       const uint64_t i = i0 + lane;
       uint4 k = make_uint4(0, 0, 0, 0);
@@ -2604,28 +2660,10 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
       unsigned long long cnt = 0;
       if (i < n) { k = w.uk[src0 + i]; cnt = w.uc[src0 + i]; len = key_len16(k); }
       const uint32_t incl = wave_incl_scan(len);
-      const uint32_t ex = incl - len, tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      const uint64_t gbase = boff & ~15ull;
-      const uint32_t sh = (uint32_t)(boff - gbase);
-      if (i < n && MOX_CHK(w, dst0 + i < w.table_cap && boff + ex + len <= w.bytes_cap, CHK_MAT_ROW)) {
-        w.t_counts[dst0 + i] = cnt;
-        w.t_offs[dst0 + i] = boff + ex;
-        const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
-#pragma unroll
-        for (uint32_t j = 0; j < 16; j++)
-          if (j < len) st[sh + ex + j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
-      }
+      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      if (i < n) mat_word(w, st, dst0 + i, boff, incl - len, k, len, cnt);
       wave_lds_fence();
-      const uint64_t ge = boff + tot;
-      const uint64_t a0 = (boff + 15) & ~15ull, a1 = ge & ~15ull;  // whole lines [a0, a1)
-      if (a0 < a1) {
-        for (uint64_t q = a0 + 16ull * lane; q < a1; q += 16ull * 64)
-          *reinterpret_cast<uint4*>(w.t_bytes + q) = *reinterpret_cast<const uint4*>(st + (q - gbase));
-        if (lane < 16 && boff + lane < a0) w.t_bytes[boff + lane] = st[sh + lane];
-        if (lane >= 16 && lane < 32 && a1 + (lane - 16) < ge) w.t_bytes[a1 + (lane - 16)] = st[(a1 - gbase) + (lane - 16)];
-      } else if (lane < 32 && boff + lane < ge) {
-        w.t_bytes[boff + lane] = st[sh + lane];
-      }
+      mat_flush(w, st, boff, tot, (uint32_t)lane, 64);
       wave_lds_fence();  // the stage is rewritten by the next step
       boff += tot;
     }
