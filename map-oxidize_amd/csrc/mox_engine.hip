@@ -278,7 +278,7 @@ int alloc_fixed(mox_engine* e) {
   if ((rc = dalloc(e, (void**)&w.dict_tag, DICT_SLOTS * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_key, DICT_SLOTS * 16))) return rc;
   if ((rc = dalloc(e, (void**)&w.dict_tot, DICT_SLOTS * 8))) return rc;
-  w.map_grid = (uint32_t)std::min(e->n_cu, MAX_MAP_GRID);
+  w.map_grid = (uint32_t)std::min(e->n_cu * MAP_WG_PER_CU, MAX_MAP_GRID);
   if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.spill_n, (size_t)w.map_grid * 4))) return rc;
   // bucket directory block: one allocation, zeroed per run

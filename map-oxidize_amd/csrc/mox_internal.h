@@ -7,27 +7,46 @@
 namespace mox {
 
 // ---- geometry ----
+#ifdef MOX_MAP2
+// experiment: two map workgroups per CU (1 loader + 9 consumers each, 2,048-slot dictionary)
+constexpr int MAP_THREADS = 640;
+constexpr int MAP_WG_PER_CU = 2;
+constexpr int MAP_MIN_WAVES = 5;            // per SIMD: 2 workgroups x 10 waves / 4 SIMDs
+constexpr int MAP_LOADERS = 1;
+constexpr int RING = 16;
+constexpr int DICT_BUCKETS = 512;
+constexpr int DICT_MAX_WORDS = 1792;
+#else
 constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
-constexpr int MAX_MAP_GRID = 1024;          // map workgroups (one per CU)
+constexpr int MAP_WG_PER_CU = 1;
+constexpr int MAP_MIN_WAVES = 1;
+#ifndef MOX_MAP_LOADERS
+#define MOX_MAP_LOADERS 1
+#endif
+constexpr int MAP_LOADERS = MOX_MAP_LOADERS;  // loader waves (alternate row groups)
+constexpr int RING = 32;                    // power of two
+constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
+constexpr int DICT_MAX_WORDS = 3584;
+#endif
+constexpr int MAX_MAP_GRID = 1024;          // map workgroups
 constexpr int MAP_WAVES = MAP_THREADS / 64;
 constexpr int ROW = 1024;                   // bytes one wave classifies per step (64 lanes x 16 B)
 constexpr int ROWBUF = ROW + 32;            // lowered row + 16 B look-ahead + pad (LDS)
 constexpr int TOKMAX = ROW / 2;             // token starts per row (at most every other byte)
 // k_map row ring (LDS): one loader wave streams rows, the other waves consume
 // them.  Slot = 64 lanes x 16 B = [16 B before | PAY payload bytes | 16 B after].
-constexpr int RING = 32;                    // power of two
 constexpr int SLOT = ROW;
 constexpr int PAY = ROW - 32;               // 992 payload bytes per row
+#ifndef MOX_LD_GROUPS
+#define MOX_LD_GROUPS 3
+#endif
 constexpr int LD_GROUP = 6;                 // loader: rows per register group
-constexpr int LD_GROUPS = 3;                // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
-constexpr int MAP_LOADERS = 2;              // loader waves (alternate row groups)
+constexpr int LD_GROUPS = MOX_LD_GROUPS;    // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
-constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
 constexpr int DICT_SLOTS = 4 * DICT_BUCKETS;
-constexpr int DICT_MAX_WORDS = 3584;
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;
 constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B

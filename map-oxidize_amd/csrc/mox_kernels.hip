@@ -690,7 +690,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
 //  * the other waves = consumers: take rows in order by ticket (dynamic load
 //    balance), process them from LDS (do_row) and release the slot.  Their
 //    cold-record stores are never waited for inside the loop.
-extern "C" __global__ __launch_bounds__(MAP_THREADS, 1) void k_map(Corpus c, Work w, uint64_t nrows) {
+extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(Corpus c, Work w, uint64_t nrows) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   MapCtx m;
   m.c = c;
