@@ -402,6 +402,20 @@ __device__ __forceinline__ uint4 lane0(uint4 v) {
   return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
                     __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
 }
+// inclusive wave scan of x (wave64) on the VALU: Hillis-Steele inside each row
+// of 16 lanes (DPP row_shr 1, 2, 4, 8 with zero fill), then row 0 / row 2 totals
+// into the next row (row_bcast:15) and lane 31 into rows 2, 3 (row_bcast:31);
+// no LDS crossbar round trips (a __shfl_up scan is 6 ds_bpermute latencies)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
+  return x;
+}
+
 // compiler + LDS ordering between lanes of one wave (LDS executes a wave's
 // instructions in order; this keeps the compiler from reordering across it)
 __device__ __forceinline__ void wave_lds_fence() {
@@ -583,8 +597,20 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   bool chk = false;  // rows with NUL bytes or near a non-final buffer end need the odd checks
   uint32_t lim = 64;
   if (!slow) {
-    const uint64_t L = ((uint64_t)a.y << 32) | a.x, H = ((uint64_t)a.w << 32) | a.z;
-    const uint32_t ws16 = movemask8(ws_bytes80(L)) | (movemask8(ws_bytes80(H)) << 8);
+    // per dword (ASCII bytes, no carries between bytes): whitespace = byte < 33
+    // and (byte == 32 or 9 <= byte <= 13); ctl = other bytes < 33 (NUL included)
+    uint32_t ws16 = 0, ctl = 0;
+    {
+      const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int d = 0; d < 4; d++) {
+        const uint32_t x = ad[d];
+        const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
+        const uint32_t wsd = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
+        ctl |= lt33 & ~wsd;
+        ws16 |= (((wsd >> 7) | (wsd >> 14) | (wsd >> 21) | (wsd >> 28)) & 0xFu) << (4 * d);
+      }
+    }
     const uint32_t wsn = from_next_lane(ws16);
     const uint32_t wsp = from_prev_lane(ws16);
     ws32 = ws16 | (wsn << 16);
@@ -594,7 +620,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
       if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
     }
-    const bool anyz = __any((zero_bytes80(L) | zero_bytes80(H)) != 0);
+    const bool anyz = __any((ctl & 0x80808080u) != 0);  // any control byte: NULs are found exactly below
     if (anyz) {
       const uint32_t z16 = zero_mask16(a);
       z32 = z16 | (from_next_lane(z16) << 16);
@@ -609,14 +635,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   const uint32_t cnt = __popc(start);
   ntok += cnt;
   // wave-exclusive prefix of cnt (0..16) and the wave total
-  const uint64_t lt = (1ull << lane) - 1ull;
-  uint32_t pre = 0, total = 0;
-#pragma unroll
-  for (int bit = 0; bit < 5; bit++) {
-    const uint64_t bm = __ballot((cnt >> bit) & 1u);
-    pre += (uint32_t)__popcll(bm & lt) << bit;
-    total += (uint32_t)__popcll(bm) << bit;
-  }
+  const uint32_t incl = wave_incl_scan(cnt);
+  const uint32_t pre = incl - cnt, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return;
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
   // list entry (u16): slot offset (10 bits) | length (5 bits, <= 16) | odd (bit 15)
@@ -2004,20 +2024,6 @@ static_assert(SR_PER * SR_THREADS == (int)SMALL_CAP && SR_BINS == 4 * SR_THREADS
 // LDS-only workgroup barrier: the DS queue drained, no wait on global stores
 // still in flight (a __syncthreads fence would wait for them).
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// inclusive wave scan of x (wave64) on the VALU: Hillis-Steele inside each row
-// of 16 lanes (DPP row_shr 1, 2, 4, 8 with zero fill), then row 0 / row 2 totals
-// into the next row (row_bcast:15) and lane 31 into rows 2, 3 (row_bcast:31);
-// no LDS crossbar round trips (a __shfl_up scan is 6 ds_bpermute latencies)
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
-  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);
-  return x;
-}
 
 struct SmallIn {  // prefetched keys (weighted counts are read at use: rare outside exchange passes)
   uint4 k[SR_PER];
