@@ -416,6 +416,16 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
+// inclusive wave max (same DPP pattern as wave_incl_scan)
+__device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false));
+  x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
+  return x;
+}
 // compiler + LDS ordering between lanes of one wave (LDS executes a wave's
 // instructions in order; this keeps the compiler from reordering across it)
 __device__ __forceinline__ void wave_lds_fence() {
@@ -643,20 +653,28 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   uint32_t k = pre;
   bool any_odd = false;
   if (!chk && !slow) {
-    // common rows: a wave-uniform loop (trip count = most starts in any lane)
-    // with no divergence; a lane that has run out of starts writes the sink
-    // entry list[TOKMAX - 1], which no row reaches (<= PAY / 2 tokens)
+    // common rows: a loop with a wave-uniform trip count (the most starts in
+    // any lane) and no divergence; a lane that has run out of starts writes
+    // the sink entry list[TOKMAX - 1], which no row reaches (<= PAY / 2
+    // tokens).  v_ffbl of 0 is ~0: such a start or length reads as odd.
+    // A token longer than 16 bytes has no whitespace in the 16 bytes after
+    // its start: found once per row from the smeared whitespace mask.
+    uint32_t sm = ws32 >> 1;
+    sm |= sm >> 1;
+    sm |= sm >> 2;
+    sm |= sm >> 4;
+    sm |= sm >> 8;  // bit p: whitespace somewhere in bits p + 1 .. p + 16
+    any_odd = (start & ~sm) != 0;
+    const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(cnt), 63);
     uint32_t st = start;
     uint16_t* const sink = list + (TOKMAX - 1);
-    while (__any(st != 0)) {
-      const bool valid = st != 0;
-      const uint32_t p = valid ? (uint32_t)__builtin_ctz(st) : 0u;
+    const uint32_t lbase = (uint32_t)(lane * 16);
+    for (uint32_t it = 0; it < trips; it++) {
+      const bool valid = it < cnt;
+      const uint32_t p = (uint32_t)__builtin_ctzg(st, -1);
       st &= st - 1;
-      const uint32_t rest = ws32 >> p;
-      const uint32_t len = rest ? (uint32_t)__builtin_ctz(rest) : 32u;
-      const bool odd = len > 16;
-      any_odd |= odd && valid;
-      *(valid ? list + k : sink) = (uint16_t)((uint32_t)(lane * 16) + p + (odd ? 0x8000u : (len << 10)));
+      const uint32_t len = (uint32_t)__builtin_ctzg(ws32 >> (p & 31u), -1);
+      *(valid ? list + k : sink) = (uint16_t)(lbase + p + (len > 16 ? 0x8000u : (len << 10)));
       k += valid ? 1u : 0u;
     }
   } else {
