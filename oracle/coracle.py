@@ -40,8 +40,23 @@ def lib():
         L.moxo_count_tokens.restype = U64
         L.moxo_count_words.argtypes = [VP, U64, ctypes.c_int, VP, VP, U64, VP]
         L.moxo_count_words.restype = None
+        L.moxo_lowercase.argtypes = [ctypes.c_char_p, U64, ctypes.c_char_p]
+        L.moxo_lowercase.restype = U64
+        L.moxo_is_whitespace.argtypes = [ctypes.c_uint32]
+        L.moxo_is_whitespace.restype = ctypes.c_int
         _lib = L
     return _lib
+
+
+def lowercase(word):
+    """The oracle's str::to_lowercase of one token (UTF-8 bytes in and out)."""
+    out = ctypes.create_string_buffer(2 * len(word) + 8)
+    n = lib().moxo_lowercase(word, len(word), out)
+    return out.raw[:n]
+
+
+def is_whitespace(cp):
+    return lib().moxo_is_whitespace(cp) != 0
 
 
 class InvalidUtf8(ValueError):

@@ -24,8 +24,10 @@
  * §8(c)).  This restatement is cross-checked against an independent Python
  * restatement (oracle/pyoracle.py: Python's strict UTF-8 decoder, an explicit
  * White_Space set and str.lower()) and the known-answer table of SURVEY.md §0.1.
- * Case data: Unicode 13.0.0 (map-oxidize_amd/csrc/mox_unicode_tables.h is the
- * shared DATA; this file's code is independent of the GPU code).
+ * Case data: Unicode 14.0.0 from ICU 70.1 (map-oxidize_amd/csrc/mox_unicode_tables.h
+ * is the shared DATA; this file's code is independent of the GPU code).  The
+ * lowercase map, Final_Sigma and White_Space are pinned to ICU's own answers in
+ * tests/test_unicode_pin.py (tests/golden/unicode_icu70.json).
  */
 #include "mox_oracle.h"
 

@@ -73,6 +73,23 @@ def rand_text(rng, n):
     return b"".join(rng.choice(ALPH) for _ in range(n))
 
 
+def test_unicode_icu70_kats(eng, eng_nodict):
+    """The engine's lowercase + Final_Sigma against ICU 70.1 (Unicode 14.0):
+    every probe and hand-picked string of tests/golden/unicode_icu70.json as a
+    token, with and without the dictionary, separated by ASCII and by
+    multi-byte whitespace."""
+    import json
+    from collections import Counter
+    from test_unicode_pin import FIX, icu_words
+    with open(FIX) as f:
+        pairs = icu_words(json.load(f))
+    want = sorted(Counter(w.encode() for _, w in pairs).items())
+    for sep in ("\n", "\u3000", " \u2029"):
+        data = sep.join(s for s, _ in pairs).encode()
+        assert gpu_items(eng, data) == want, repr(sep)
+        assert gpu_items(eng_nodict, data) == want, repr(sep)
+
+
 def test_fuzz_small(eng):
     rng = random.Random(2024)
     for i in range(300):
