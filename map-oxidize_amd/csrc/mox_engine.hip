@@ -551,6 +551,12 @@ int run_corpus(mox_engine* e, const Corpus& c) {
                   mc[8 * i + 5], mc[8 * i + 6]);
         fclose(g);
       }
+      std::vector<unsigned long long> rc(4 * 1024 * 16);
+      (void)hipMemcpy(rc.data(), e->w.stamps + 8 * 4096 + 8 * 1024 * MAP_WAVES, rc.size() * 8, hipMemcpyDeviceToHost);
+      if (FILE* r = fopen("gpurun_out/redcyc.csv", "w")) {
+        for (size_t i = 0; i < rc.size() / 4; i++) fprintf(r, "%zu,%llu,%llu,%llu,%llu\n", i, rc[4 * i], rc[4 * i + 1], rc[4 * i + 2], rc[4 * i + 3]);
+        fclose(r);
+      }
       FILE* f = fopen("gpurun_out/stamps.csv", "w");
       if (f) {
         for (int i = 0; i < NB; i++)
@@ -1189,7 +1195,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     return fail(MOX_EHIP, "hipFuncSetAttribute(dynamic LDS) failed");
   }
   if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
-  if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096 + 8 * 8 * 1024 * MAP_WAVES);
+  if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096 + 8 * 8 * 1024 * MAP_WAVES + 8 * 4 * 1024 * 16);
   e->sync_each = getenv("MOX_SYNC_EACH") != nullptr;
   if (const char* f = getenv("MOX_TEST_FAIL_ALLOC")) e->test_fail_alloc = atoi(f);
   int rc = alloc_fixed(e);

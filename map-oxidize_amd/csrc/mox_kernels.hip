@@ -1447,7 +1447,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {
 constexpr int RED_BK = 608;    // 2 workgroups per CU: table + sort scratch <= 80 KiB
 constexpr int RED_SLOTS = 4 * RED_BK;
 constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort width
-constexpr int RED_UNROLL = 2;
+#ifndef MOX_RED_UNROLL
+#define MOX_RED_UNROLL 2
+#endif
+constexpr int RED_UNROLL = MOX_RED_UNROLL;
 constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
 
 struct RedLds {
@@ -1805,6 +1808,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   // then all workgroups take oversized sub-buckets from the work list
   const uint32_t NBIG = (uint32_t)w.ctl->n_big;
   uint32_t max_kk = 0;
+#ifdef MOX_RED_STATS  // per-wave cycles: [0] between chunks (loop, load waits) [1] hash [2] fast path [3] slow path
+  uint64_t rcyc[4] = {0, 0, 0, 0}, rprev = __builtin_amdgcn_s_memtime();
+#define RED_MARK(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); rcyc[k] += t_ - rprev; rprev = t_; } while (0)
+#else
+#define RED_MARK(k) do { } while (0)
+#endif
   bool own = blockIdx.x < NB && w.b_kk[blockIdx.x] == 0;
   for (;;) {
     uint32_t u;
@@ -1886,18 +1895,22 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           const uint32_t n = __builtin_amdgcn_readlane(myn, kq);
           uint32_t h[RED_UNROLL];
           bool todo[RED_UNROLL];
+          RED_MARK(0);
 #pragma unroll
           for (int u2 = 0; u2 < RED_UNROLL; u2++) {
             h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
             todo[u2] = iq + u2 * 64 + lane < n && in_sub(h[u2], shift0, kk, sub);
           }
+          RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
               if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+            RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
               if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
+            RED_MARK(3);
           } else {
             asm volatile("" ::"v"(h[0]), "v"(h[1]));
           }
@@ -2025,6 +2038,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     if (kk > max_kk) max_kk = kk;
     __syncthreads();
   }
+#ifdef MOX_RED_STATS
+  if (lane == 0 && w.stamps) {
+    unsigned long long* o = w.stamps + 8 * 4096 + 8 * 1024 * MAP_WAVES + ((uint64_t)blockIdx.x * NWV + wv) * 4;
+    for (int k = 0; k < 4; k++) o[k] = rcyc[k];
+  }
+#endif
   if (tid == 0) {
     if (max_kk) atomicMax(&w.ctl->max_sub, 1u << max_kk);
     if (s.dbg) for (int i = 0; i < 3; i++) atomicAdd(&w.ctl->dbg_cnt[i], (unsigned long long)dbgc[i]);

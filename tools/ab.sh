@@ -9,7 +9,7 @@ ARGS=${@:---steps 20 --warmup 5 --no-cpu-baseline}
 O=gpurun_out/ab; mkdir -p $O
 for v in $VARS; do
   MOX_LIB=build/var_$v/libmox.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 \
-    --timeout-method thread -k "kats or fuzz or tile or corpora or huge or misaligned" > $O/par_$v.log 2>&1
+    --timeout-method thread -k "kats or fuzz or tile or corpora or huge or misaligned or split or async" > $O/par_$v.log 2>&1
   rc=$?; echo "parity $v rc=$rc $(tail -1 $O/par_$v.log)"; [ $rc -eq 0 ] || exit $rc
 done
 for r in $(seq $ROUNDS); do

@@ -10,9 +10,10 @@ OUT=$ROOT/build/var_$NAME
 mkdir -p $OUT
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result"
 C=$ROOT/map-oxidize_amd/csrc
-$H -mllvm -amdgpu-sched-strategy=max-memory-clause $FLAGS -c $C/mox_kernels.hip -o $OUT/k.o &
-$H $FLAGS -c $C/mox_engine.hip -o $OUT/e.o &
-g++ -O3 -std=c++17 -fPIC -c $C/mox_table.cpp -o $OUT/t.o &
-wait
+rm -f $OUT/*.o $OUT/libmox.so
+$H -mllvm -amdgpu-sched-strategy=max-memory-clause $FLAGS -c $C/mox_kernels.hip -o $OUT/k.o & P1=$!
+$H $FLAGS -c $C/mox_engine.hip -o $OUT/e.o & P2=$!
+g++ -O3 -std=c++17 -fPIC -c $C/mox_table.cpp -o $OUT/t.o & P3=$!
+wait $P1 && wait $P2 && wait $P3
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $OUT/libmox.so $OUT/k.o $OUT/e.o $OUT/t.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built $OUT/libmox.so"
