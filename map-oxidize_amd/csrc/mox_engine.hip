@@ -38,19 +38,17 @@ __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
 __global__ void k_dict_hist(Work w);
 __global__ void k_dict_pick(Work w, uint32_t max_words);
 __global__ void k_dict_build(Work w, uint32_t max_words);
-__global__ void k_dict_totals(Work w);
 __global__ void k_unicode(Corpus c, Work w, Tables T);
 __global__ void k_hist(Work w);
-__global__ void k_bucket_scan(Work w);
 __global__ void k_scatter(Work w);
 __global__ void k_reduce(Work w);
 __global__ void k_split_count(Work w);
 __global__ void k_unit_scan(Work w);
 __global__ void k_split_scatter(Work w);
 __global__ void k_unit_uniq_scan(Work w);
+__global__ void k_final_scan(Work w);
 __global__ void k_reduce_small(Work w);
 __global__ void k_reduce_sort1(Work w);
-__global__ void k_final_scan(Work w);
 __global__ void k_mat(Work w, Corpus c);
 __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
 __global__ void k_xpack_short(Work w, WRec* out);
@@ -378,15 +376,13 @@ Seq seq_of(mox_engine* e) {
 void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   Work& w = e->w;
   hipStream_t s = e->stream;
-  hipLaunchKernelGGL(k_hist, dim3(w.map_grid), dim3(1024), 0, s, w);
+  hipLaunchKernelGGL(k_hist, dim3(w.map_grid), dim3(1024), 0, s, w);  // last workgroup: partition offsets
   q.step("k_hist");
-  hipLaunchKernelGGL(k_bucket_scan, dim3(1), dim3(NB), 0, s, w);
-  q.step("k_bucket_scan");
   hipLaunchKernelGGL(k_scatter, dim3(w.map_grid), dim3(1024), 0, s, w);
   q.step("k_scatter");
   hipLaunchKernelGGL(k_split_count, dim3(NB), dim3(256), 0, s, w);  // SC_THREADS
   q.step("k_split_count");
-  hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(NB), 0, s, w);
+  hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(256), 0, s, w);  // SC_THREADS
   q.step("k_unit_scan");
   hipLaunchKernelGGL(k_split_scatter, dim3(NB), dim3(1024), 0, s, w);
   q.step("k_split_scatter");
@@ -457,10 +453,8 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_map");
   q.rec(2);
   // 3. lanes
-  hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);
+  hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);  // + dictionary totals
   q.step("k_unicode");
-  hipLaunchKernelGGL(k_dict_totals, dim3(DICT_SLOTS / 256), dim3(256), 0, s, w);
-  q.step("k_dict_totals");
   q.rec(3);
   // 4-5. shuffle directory + bucket reduce, table
   launch_reduce_tail(e, c, q);

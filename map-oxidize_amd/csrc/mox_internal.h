@@ -119,7 +119,7 @@ struct Ctl {
   unsigned int dict_maxprobe;
   unsigned int max_sub;
   unsigned int dict_thresh;
-  unsigned int pad[3];
+  unsigned int done[3];           // last-workgroup tickets: [0] k_hist
   unsigned long long cold_need;   // max records any (workgroup, partition) region asked for
   unsigned long long spill_need;  // max spill records of any map workgroup
   unsigned long long w_total;     // weighted + spilled records

@@ -13,13 +13,16 @@
 //                             LDS dictionary, all other words emitted as exact 16-byte
 //                             keys into 1024 hash partitions
 //                             (= the shuffle write, main.rs:103-109)
-//   k_unicode                 full Unicode lowercase + Final_Sigma for non-ASCII tokens
-//   k_dict_totals, k_hist, k_bucket_scan, k_scatter   shuffle directory
-//   k_split_*, k_unit_scan    high-cardinality split of partitions into sub-bucket units
+//   k_unicode                 full Unicode lowercase + Final_Sigma for non-ASCII tokens,
+//                             and the dictionary totals as weighted records
+//   k_hist (+ bucket scan in its last workgroup), k_scatter   shuffle directory
+//   k_split_count, k_unit_scan, k_split_scatter
+//                             high-cardinality split of partitions into sub-bucket units
 //   k_reduce, k_reduce_small  per-unit LDS hash group-by / sort-based reduce (= reduce_phase merge,
 //                             main.rs:132-134), deterministic (hash, key) order
 //   long table                words > 16 bytes: hashed keys, byte-compare resolution
-//   k_unit_uniq_scan, k_final_scan, k_mat   dense (word, count) table in HBM, one pass
+//   k_unit_uniq_scan, k_final_scan, k_mat
+//                             dense (word, count) table in HBM, one pass
 #include "mox_internal.h"
 
 namespace mox {
@@ -74,8 +77,26 @@ __device__ __forceinline__ uint64_t block_exscan(uint64_t x, uint64_t* wsum, uin
   return pre + incl - x;
 }
 
-// Exclusive scan of v[0..n) (n = *n_ptr) into out[0..n], out[n] = total.
-// Three launches: per-WG totals, one-WG scan of totals, per-WG rescan + offset.
+// Last-workgroup handoff: true in the one workgroup of the grid that takes the
+// last ticket.  The words that workgroup reads from the others are published
+// with agent-scope atomics (RMW or st_agent), which are performed past the
+// XCD-private L2s: no cache write-back, only a wait for them to complete before
+// the ticket (a __threadfence() here would write back L2 in every workgroup).
+// The last workgroup reads them with ld_agent.  `ticket` is a Ctl word zeroed
+// by k_init; every workgroup of the grid must call this (no early return).
+template <class T>
+__device__ __forceinline__ void st_agent(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T>
+__device__ __forceinline__ T ld_agent(const T* p) { return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ __forceinline__ bool last_block(unsigned int* ticket) {
+  __shared__ bool s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's atomics are performed
+  __syncthreads();
+  if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  return s_last;
+}
+
 // Corpus byte with out-of-range bytes reading as ' ' (whitespace).
 __device__ __forceinline__ uint8_t byte_at(const Corpus& c, uint64_t p) {
   if (p < c.lo || p >= c.hi) return 0x20;
@@ -1202,10 +1223,9 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
   if (tid == 0) w.ctl->dict_n = nsel;
 }
 
-// Emit the dictionary totals (summed by k_map's atomics) as weighted records.
-extern "C" __global__ void k_dict_totals(Work w) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= DICT_SLOTS || w.ctl->dict_n == 0 || w.dict_tag[s] == 0) return;
+// Emit dictionary slot s's total (summed by k_map's atomics) as a weighted record.
+__device__ __forceinline__ void dict_total(const Work& w, uint32_t s) {
+  if (w.ctl->dict_n == 0 || w.dict_tag[s] == 0) return;
   const uint64_t tot = w.dict_tot[s];
   if (tot == 0) return;
   const uint4 k = w.dict_key[s];
@@ -1269,7 +1289,12 @@ __device__ __forceinline__ int enc_to(uint32_t cp, uint8_t* o) {
 
 // Rust str::to_lowercase of one token (full mapping + Final_Sigma), written to
 // the arena; then routed as a short key (weighted record) or a long word.
+// Also emits the dictionary totals (thread s: slot s; grid >= DICT_SLOTS threads).
 extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
+  {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < DICT_SLOTS) dict_total(w, s);
+  }
   if (w.ctl->err_utf8 != ~0ull) return;  // invalid input: no result is produced anyway
   uint64_t n = w.ctl->u_n;
   if (n > w.u_cap) n = w.u_cap;
@@ -1330,6 +1355,29 @@ extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
   }
 }
 
+// Partition directory (one thread per partition, NB threads): weighted and
+// record offsets; run by k_hist's last workgroup.
+__device__ void bucket_scan(const Work& w) {
+  __shared__ uint64_t wsum[16];
+  const int b = threadIdx.x;
+  const uint64_t nw = ld_agent(&w.b_w[b]), nr = ld_agent((const unsigned long long*)&w.b_recs[b]);
+  uint64_t sw, sr, cold;
+  const uint64_t ow = block_exscan(nw, wsum, sw);
+  const uint64_t orr = block_exscan(nr + nw, wsum, sr);
+  (void)block_exscan(nr, wsum, cold);
+  w.w_off[b] = ow;
+  w.rec_off[b] = orr;
+  w.b_cur[b] = 0;
+  if (b == 0) {
+    w.w_off[NB] = sw;
+    w.rec_off[NB] = sr;
+    w.ctl->cold_recs = cold;
+    if (sw > w.w_cap) atomicOr(&w.ctl->overflow, OVF_W);
+    if (sr > w.uniq_cap) atomicOr(&w.ctl->overflow, OVF_POOL);
+    w.ctl->w_total = sw;
+  }
+}
+
 // ------------------------------------------------------------------ shuffle directory
 // Records per partition: cold regions (map workgroup x partition) and weighted
 // records (dictionary totals, Unicode-lane words, map spills).
@@ -1357,29 +1405,9 @@ extern "C" __global__ __launch_bounds__(1024) void k_hist(Work w) {
   __syncthreads();
   for (int i = threadIdx.x; i < NB; i += blockDim.x)
     if (hw[i]) atomicAdd(&w.b_w[i], hw[i]);
+  static_assert(NB == 1024, "k_hist's last workgroup scans one partition per thread");
+  if (last_block(&w.ctl->done[0])) bucket_scan(w);
 }
-
-extern "C" __global__ __launch_bounds__(NB) void k_bucket_scan(Work w) {  // one workgroup of NB threads
-  __shared__ uint64_t wsum[16];
-  const int b = threadIdx.x;
-  const uint64_t nw = w.b_w[b], nr = w.b_recs[b];
-  uint64_t sw, sr, cold;
-  const uint64_t ow = block_exscan(nw, wsum, sw);
-  const uint64_t orr = block_exscan(nr + nw, wsum, sr);
-  (void)block_exscan(nr, wsum, cold);
-  w.w_off[b] = ow;
-  w.rec_off[b] = orr;
-  w.b_cur[b] = 0;
-  if (b == 0) {
-    w.w_off[NB] = sw;
-    w.rec_off[NB] = sr;
-    w.ctl->cold_recs = cold;
-    if (sw > w.w_cap) atomicOr(&w.ctl->overflow, OVF_W);
-    if (sr > w.uniq_cap) atomicOr(&w.ctl->overflow, OVF_POOL);
-    w.ctl->w_total = sw;
-  }
-}
-
 // Weighted records (and this map workgroup's spills) to their partition's range
 // of w_sorted.  Each workgroup takes a contiguous chunk, ranks its records per
 // partition in LDS, reserves one range per (workgroup, partition) with a single
@@ -1613,7 +1641,7 @@ __device__ __forceinline__ void for_partition_cold(const Work& w, uint32_t b, F 
 // Partitions with few distinct keys stay whole (their reduce resolves them in
 // one table, or in a few in-kernel sub-passes).
 constexpr int SC_THREADS = 256;  // 8 workgroups per CU: every partition's decision in one round
-extern "C" __global__ __launch_bounds__(SC_THREADS) void k_split_count(Work w) {
+__device__ __forceinline__ void split_count(const Work& w) {
   __shared__ uint32_t bm[LC_BITS / 32];
   __shared__ uint32_t hc[SUB_N], hw[SUB_N];
   __shared__ uint64_t wsum[SC_THREADS / 64];
@@ -1687,26 +1715,42 @@ extern "C" __global__ __launch_bounds__(SC_THREADS) void k_split_count(Work w) {
   for (uint32_t i = tid; i < nsub; i += blockDim.x) { o[i] = hc[i]; o[SUB_N + i] = hw[i]; }
 }
 
-// One workgroup of NB threads: units per partition, split-buffer offsets, the
-// reduce work-queue reset, and the output region of every whole partition.
-extern "C" __global__ __launch_bounds__(NB) void k_unit_scan(Work w) {
+// One workgroup of SC_THREADS threads, SC_PER consecutive partitions each:
+// units per partition, split-buffer offsets, the reduce work-queue reset, and
+// the output region of every whole partition.
+constexpr int SC_PER = NB / SC_THREADS;
+__device__ void unit_scan(const Work& w) {
   __shared__ uint64_t wsum[16];
-  const uint32_t b = threadIdx.x;
-  const uint32_t kk = w.b_kk[b];
-  uint64_t U, tk, tw, ns, nwhole;
-  const uint64_t ub = block_exscan(1ull << kk, wsum, U);
-  const uint64_t ok = block_exscan(kk ? w.b_recs[b] : 0, wsum, tk);
-  const uint64_t ow = block_exscan(kk ? w.b_w[b] : 0, wsum, tw);
-  (void)block_exscan(kk ? 0 : 1, wsum, nwhole);
-  ns = NB - nwhole;
-  w.u_base[b] = (uint32_t)ub;
-  w.b_uniq[b] = 0;  // k_reduce*: set (whole partition) or accumulated (split)
-  w.sp_off[b] = ok;
-  w.spw_off[b] = ow;
-  if (!kk) {
-    w.udesc[ub] = UnitDesc{0, 0, w.rec_off[b], UNIT_WHOLE, 0, b, 0};
+  const int t = threadIdx.x;
+  uint32_t kk[SC_PER];
+  uint64_t nu = 0, nk = 0, nw = 0, nwh = 0;
+#pragma unroll
+  for (int j = 0; j < SC_PER; j++) {
+    const uint32_t b = SC_PER * t + j;
+    kk[j] = w.b_kk[b];
+    nu += 1ull << kk[j];
+    nk += kk[j] ? w.b_recs[b] : 0;
+    nw += kk[j] ? w.b_w[b] : 0;
+    nwh += kk[j] ? 0 : 1;
   }
-  if (b == 0) {
+  uint64_t U, tk, tw, nwhole;
+  uint64_t ub = block_exscan(nu, wsum, U);
+  uint64_t ok = block_exscan(nk, wsum, tk);
+  uint64_t ow = block_exscan(nw, wsum, tw);
+  (void)block_exscan(nwh, wsum, nwhole);
+#pragma unroll
+  for (int j = 0; j < SC_PER; j++) {
+    const uint32_t b = SC_PER * t + j;
+    w.u_base[b] = (uint32_t)ub;
+    w.b_uniq[b] = 0;  // k_reduce*: set (whole partition) or accumulated (split)
+    w.sp_off[b] = ok;
+    w.spw_off[b] = ow;
+    if (!kk[j]) w.udesc[ub] = UnitDesc{0, 0, w.rec_off[b], UNIT_WHOLE, 0, b, 0};
+    ub += 1ull << kk[j];
+    ok += kk[j] ? w.b_recs[b] : 0;
+    ow += kk[j] ? w.b_w[b] : 0;
+  }
+  if (t == 0) {
     w.u_base[NB] = (uint32_t)U;
     w.sp_off[NB] = tk;
     w.spw_off[NB] = tw;
@@ -1715,10 +1759,12 @@ extern "C" __global__ __launch_bounds__(NB) void k_unit_scan(Work w) {
     w.ctl->red_ticket = 0;
     w.ctl->split_k = tk;
     w.ctl->split_w = tw;
-    w.ctl->n_split = (uint32_t)ns;
+    w.ctl->n_split = (uint32_t)(NB - nwhole);
     if (tk > w.split_k_cap || tw > w.split_w_cap) atomicOr(&w.ctl->overflow, OVF_SPLIT);
   }
 }
+extern "C" __global__ __launch_bounds__(SC_THREADS) void k_split_count(Work w) { split_count(w); }
+extern "C" __global__ __launch_bounds__(SC_THREADS) void k_unit_scan(Work w) { unit_scan(w); }  // one workgroup
 
 // k_split_scatter (one workgroup per split partition): unit directory from the
 // histogram, then every record of the partition to its unit's contiguous range
@@ -2523,7 +2569,7 @@ extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Wo
 // partition's totals; plus, for long-table slice b, its occupied slots and their
 // bytes.  No global atomics in the reduce kernels, whose units of one partition
 // run side by side.
-extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) {
+__device__ __forceinline__ void unit_uniq_scan(const Work& w) {
   __shared__ uint64_t wsum[16];
   __shared__ unsigned long long lsn, lsb;
   const uint32_t b = blockIdx.x;
@@ -2570,9 +2616,9 @@ extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) {
 }
 
 // One workgroup of NB threads: partition / slice offsets, table sizes and the
-// table-capacity checks.  Short words come first (partition order = hash
-// order), then long words in slot order.
-extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {
+// table-capacity checks.  Short words come first
+// (partition order = hash order), then long words in slot order.
+__device__ void final_scan(const Work& w) {
   __shared__ uint64_t wsum[16];
   const bool rerun = (w.ctl->overflow & OVF_RERUN) != 0;  // nothing was reduced
   const uint32_t b = threadIdx.x;
@@ -2595,6 +2641,8 @@ extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) {
     if (sb + lb > w.bytes_cap) atomicOr(&w.ctl->overflow, OVF_BYTES);
   }
 }
+extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) { unit_uniq_scan(w); }
+extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) { final_scan(w); }  // one workgroup
 
 // True when this attempt produced a complete table that fits its buffers.
 __device__ __forceinline__ bool table_ok(const Work& w) {
@@ -2607,11 +2655,11 @@ __device__ __forceinline__ void exscan2_256(uint32_t a, uint32_t b, uint32_t (*w
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t ia = wave_incl_scan(a), ib = wave_incl_scan(b);
   if (lane == 63) { ws[wv][0] = ia; ws[wv][1] = ib; }
-  __syncthreads();
+  lds_barrier();  // LDS-only barriers: global loads in flight stay in flight
   uint32_t pa = 0, pb = 0;
   ta = 0; tb = 0;
   for (int k = 0; k < 4; k++) { if (k < wv) { pa += ws[k][0]; pb += ws[k][1]; } ta += ws[k][0]; tb += ws[k][1]; }
-  __syncthreads();
+  lds_barrier();
   ea = pa + ia - a;
   eb = pb + ib - b;
 }
@@ -2667,24 +2715,29 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
   const uint32_t U = (uint32_t)w.ctl->n_units;
   // whole partitions (Zipf text: ~1,400 words each): workgroup b takes partition b
   for (uint32_t b = blockIdx.x; b < NB; b += gridDim.x) {
-    if (w.b_kk[b] != 0) continue;  // split: its units go to the waves below
-    const uint32_t v = w.u_base[b];
-    const uint64_t n = w.u_uniq[v];
-    const UnitDesc ud = w.udesc[v];
-    const uint64_t src0 = ud.rec_off, dst0 = w.uniq_off[b] + w.u_uniq_off[v];
-    uint64_t boff = w.bytes_off[b] + w.u_bytes_off[v];
+    // a whole partition is its own single unit: its key count (k_reduce), input
+    // range and output offsets come straight from the partition directory
+    const uint32_t kkb = w.b_kk[b];
+    const uint64_t n = w.b_uniq[b], src0 = w.rec_off[b], dst0 = w.uniq_off[b];
+    uint64_t boff = w.bytes_off[b];
+    if (kkb != 0) continue;  // split: its units go to the waves below
+    // one step = 256 words; the next step's words load while this one is
+    // staged and written (LDS-only barriers keep those loads in flight)
+    uint4 kn = make_uint4(0, 0, 0, 0);
+    unsigned long long cn = 0;
+    if ((uint64_t)tid < n) { kn = w.uk[src0 + tid]; cn = w.uc[src0 + tid]; }
     for (uint64_t i0 = 0; i0 < n; i0 += 64 * MAT_WAVES) {
       const uint64_t i = i0 + tid;
-      uint4 k = make_uint4(0, 0, 0, 0);
-      uint32_t len = 0;
-      unsigned long long cnt = 0;
-      if (i < n) { k = w.uk[src0 + i]; cnt = w.uc[src0 + i]; len = key_len16(k); }
+      const uint4 k = kn;
+      const unsigned long long cnt = cn;
+      const uint32_t len = i < n ? key_len16(k) : 0u;
+      if (i + 64 * MAT_WAVES < n) { kn = w.uk[src0 + i + 64 * MAT_WAVES]; cn = w.uc[src0 + i + 64 * MAT_WAVES]; }
       uint32_t ex, dummy, tot, t2;
       exscan2_256(len, 0, ws, ex, dummy, tot, t2);
       if (i < n) mat_word(w, stage, dst0 + i, boff, ex, k, len, cnt);
-      __syncthreads();
+      lds_barrier();
       mat_flush(w, stage, boff, tot, (uint32_t)tid, 64 * MAT_WAVES);
-      __syncthreads();
+      lds_barrier();
       boff += tot;
     }
   }
