@@ -1898,6 +1898,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
       if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
       __syncthreads();
+      for (int rep = 0; rep < (MOX_ABL(w.dbg, DBG_RED_TWICE) ? 2 : 1); rep++)
       // cold records: wave wv streams its regions (whole partition: regions
       // g = wv, wv + NWV, ...; split unit: one chunk) 64 x RED_UNROLL records at
       // a time, the next chunk's loads in flight while the current one is
