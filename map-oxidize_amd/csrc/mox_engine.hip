@@ -600,7 +600,8 @@ int run_corpus(mox_engine* e, const Corpus& c) {
       }
     }
     if (getenv("MOX_VERBOSE"))
-      fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu\n", h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3]);
+      fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu; units %llu, k_reduce list %llu, split partitions %u, max sub-passes %u\n",
+              h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3], h.n_units, h.n_big, h.n_split, h.max_sub);
     if ((rc = check_failed(h))) return rc;
     if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
     if (h.halo_err != ~0ull)

@@ -2393,9 +2393,10 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
 //     wave prefix sum, run lengths come from the next head's position, and the
 //     distinct keys are written in sort order.
 // A unit where two different keys share the 23 sort-key hash bits (about 0.5 %
-// of C4's units) is not written here: it goes on k_reduce's work list
-// (big_units), which resolves it exactly.  Elsewhere the sort-key order is
-// the table order every reduce kernel uses (key_less).
+// of C4's units) is sorted again on 64-bit keys (all of both hashes); only a
+// full (h32, hash32b) collision goes on k_reduce's work list (big_units),
+// which resolves it exactly.  The sort-key order is the table order every
+// reduce kernel uses (key_less).
 constexpr int S1_PER = SMALL_CAP / 64;  // records per lane
 constexpr int S1_WAVES = 4;             // waves per workgroup, one unit each
 static_assert(S1_PER == 8, "k_reduce_sort1: 8 records per lane");
@@ -2407,46 +2408,52 @@ __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
   if constexpr (M == 8) return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xF, 0xF, false);  // row_ror:8
   return (uint32_t)__shfl_xor((int)v, M);
 }
+template <int M>
+__device__ __forceinline__ uint64_t xor_lane(uint64_t v) {
+  return ((uint64_t)xor_lane<M>((uint32_t)(v >> 32)) << 32) | xor_lane<M>((uint32_t)v);
+}
 // bitonic compare-exchange with the lane (lane ^ M): the lower lane keeps the
 // minimum when this block sorts ascending
-template <int M>
-__device__ __forceinline__ void s1_cross(uint32_t (&v)[S1_PER], int lane, uint32_t k) {
+template <int M, class T>
+__device__ __forceinline__ void s1_cross(T (&v)[S1_PER], int lane, uint32_t k) {
   const bool keep_min = ((lane & M) == 0) == (((uint32_t)(lane * S1_PER) & k) == 0);
 #pragma unroll
   for (int s = 0; s < S1_PER; s++) {
-    const uint32_t pv = xor_lane<M>(v[s]);
+    const T pv = xor_lane<M>(v[s]);
     v[s] = ((pv < v[s]) == keep_min) ? pv : v[s];
   }
 }
-__device__ __forceinline__ void s1_inlane(uint32_t (&v)[S1_PER], int lane, uint32_t k, int j) {
+template <class T>
+__device__ __forceinline__ void s1_inlane(T (&v)[S1_PER], int lane, uint32_t k, int j) {
 #pragma unroll
   for (int s = 0; s < S1_PER; s++) {
     const int t = s ^ j;
     if (t > s) {
       const bool asc = ((uint32_t)(lane * S1_PER + s) & k) == 0;
-      const uint32_t a = v[s], b = v[t];
+      const T a = v[s], b = v[t];
       const bool sw = (a > b) == asc;
       v[s] = sw ? b : a;
       v[t] = sw ? a : b;
     }
   }
 }
-__device__ __forceinline__ void s1_sort(uint32_t (&v)[S1_PER], int lane) {
+template <class T>
+__device__ __forceinline__ void s1_sort(T (&v)[S1_PER], int lane) {
 #pragma unroll
   for (uint32_t k = 2; k <= 512; k <<= 1) {
 #pragma unroll
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
       if (j >= 8) {
         switch (j >> 3) {
-          case 1: s1_cross<1>(v, lane, k); break;
-          case 2: s1_cross<2>(v, lane, k); break;
-          case 4: s1_cross<4>(v, lane, k); break;
-          case 8: s1_cross<8>(v, lane, k); break;
-          case 16: s1_cross<16>(v, lane, k); break;
-          default: s1_cross<32>(v, lane, k); break;
+          case 1: s1_cross<1, T>(v, lane, k); break;
+          case 2: s1_cross<2, T>(v, lane, k); break;
+          case 4: s1_cross<4, T>(v, lane, k); break;
+          case 8: s1_cross<8, T>(v, lane, k); break;
+          case 16: s1_cross<16, T>(v, lane, k); break;
+          default: s1_cross<32, T>(v, lane, k); break;
         }
       } else {
-        s1_inlane(v, lane, k, (int)j);
+        s1_inlane<T>(v, lane, k, (int)j);
       }
     }
   }
@@ -2506,19 +2513,52 @@ extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Wo
       }
       s1_sort(v, lane);
       // run heads: hash bits differ from the previous position's
-      uint32_t prev = from_prev_lane(v[S1_PER - 1]);
+      uint32_t idx[S1_PER];
       uint32_t hm = 0, bad = 0;
       wave_lds_fence();  // key[] written by every lane
+      {
+        uint32_t prev = from_prev_lane(v[S1_PER - 1]);
 #pragma unroll
-      for (int s = 0; s < S1_PER; s++) {
-        const uint32_t p = (uint32_t)(lane * S1_PER + s);
-        const bool valid = p < n;
-        const bool head = valid && (p == 0 || (v[s] >> 9) != (prev >> 9));
-        if (head) hm |= 1u << s;
-        if (valid && !head) bad |= key_eq16(key[v[s] & 511u], key[prev & 511u]) ? 0u : 1u;
-        prev = v[s];
+        for (int s = 0; s < S1_PER; s++) {
+          const uint32_t p = (uint32_t)(lane * S1_PER + s);
+          const bool valid = p < n;
+          const bool head = valid && (p == 0 || (v[s] >> 9) != (prev >> 9));
+          if (head) hm |= 1u << s;
+          if (valid && !head) bad |= key_eq16(key[v[s] & 511u], key[prev & 511u]) ? 0u : 1u;
+          idx[s] = v[s] & 511u;
+          prev = v[s];
+        }
       }
-      if (__any(bad != 0)) {  // two keys share the sort-key hash bits: k_reduce resolves this unit
+      if (__any(bad != 0)) {
+        // two different keys share the 23 sort-key hash bits (~0.5 % of C4's
+        // units): sort again on 64-bit keys -- the 10 h32 bits below the unit,
+        // all of hash32b, the index -- which is key_less order whenever
+        // (h32, hash32b) differ
+        uint64_t v2[S1_PER];
+#pragma unroll
+        for (int s = 0; s < S1_PER; s++) {
+          const uint32_t i = (uint32_t)(s * 64 + lane);
+          const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
+          const uint64_t pre = ((uint64_t)(shift >= 32 ? 0u : (h << shift) >> shift) << 41) | ((uint64_t)hb << 9);
+          v2[s] = i < n ? (pre | i) : ~0ull;
+        }
+        s1_sort(v2, lane);
+        uint64_t prev = ((uint64_t)from_prev_lane((uint32_t)(v2[S1_PER - 1] >> 32)) << 32) |
+                        from_prev_lane((uint32_t)v2[S1_PER - 1]);
+        hm = 0;
+        bad = 0;
+#pragma unroll
+        for (int s = 0; s < S1_PER; s++) {
+          const uint32_t p = (uint32_t)(lane * S1_PER + s);
+          const bool valid = p < n;
+          const bool head = valid && (p == 0 || (v2[s] >> 9) != (prev >> 9));
+          if (head) hm |= 1u << s;
+          if (valid && !head) bad |= key_eq16(key[(uint32_t)v2[s] & 511u], key[(uint32_t)prev & 511u]) ? 0u : 1u;
+          idx[s] = (uint32_t)v2[s] & 511u;
+          prev = v2[s];
+        }
+      }
+      if (__any(bad != 0)) {  // (h32, hash32b) shared by two keys: k_reduce resolves this unit
         if (lane == 0) {
           const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
           if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
@@ -2539,7 +2579,7 @@ extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Wo
         for (int s = 0; s < S1_PER; s++) {
           if ((hm >> s) & 1u) {
             const uint32_t p = (uint32_t)(lane * S1_PER + s);
-            const uint4 kk = key[v[s] & 511u];
+            const uint4 kk = key[idx[s]];
             if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {
               w.uk[d.rec_off + o] = kk;
               w.uc[d.rec_off + o] = (unsigned long long)(hp[o + 1] - p);
