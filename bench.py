@@ -296,7 +296,7 @@ def main():
             "roofline": {
                 "kernel": "k_map",
                 "bound": "hbm",
-                "limiter": "VALU issue + LDS latency at 3.5 consumer waves/SIMD, not HBM (SQ/PMC counters, DESIGN.md §4)",
+                "limiter": "VALU issue + LDS latency at 3.75 consumer waves/SIMD (1 loader + 15 consumer waves per CU), not HBM (SQ/PMC counters, DESIGN.md §4, §8)",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
