@@ -49,6 +49,7 @@ __global__ void k_unit_uniq_scan(Work w);
 __global__ void k_final_scan(Work w);
 __global__ void k_reduce_small(Work w);
 __global__ void k_reduce_sort1(Work w);
+__global__ void k_reduce_sort2(Work w);
 __global__ void k_mat(Work w, Corpus c);
 __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
 __global__ void k_xpack_short(Work w, WRec* out);
@@ -298,6 +299,8 @@ int alloc_fixed(mox_engine* e) {
   if ((rc = dalloc(e, (void**)&w.spw_off, (NB + 1) * 8))) return rc;
   if ((rc = dalloc(e, (void**)&w.udesc, (size_t)U_MAX * sizeof(UnitDesc)))) return rc;
   if ((rc = dalloc(e, (void**)&w.big_units, (size_t)U_MAX * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.mid_units, (size_t)U_MAX * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.small_units, (size_t)U_MAX * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.u_bytes, (size_t)U_MAX * 8))) return rc;
   if ((rc = dalloc(e, (void**)&w.u_bytes_off, (size_t)U_MAX * 8))) return rc;
   {
@@ -389,6 +392,8 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   // count-1 small units first: its hash-collision fallbacks join k_reduce's work list
   hipLaunchKernelGGL(k_reduce_sort1, dim3(4 * e->n_cu), dim3(256), 0, s, w);  // 4 waves per workgroup, one unit per wave
   q.step("k_reduce_sort1");
+  hipLaunchKernelGGL(k_reduce_sort2, dim3(8 * e->n_cu), dim3(64), 0, s, w);  // one wave per unit of 513..1024 records
+  q.step("k_reduce_sort2");
   hipLaunchKernelGGL(k_reduce, dim3(NB), dim3(RED_THREADS), reduce_lds_bytes(), s, w);  // workgroup b: partition b, then the work list
   q.step("k_reduce");
   hipLaunchKernelGGL(k_reduce_small, dim3(8 * e->n_cu), dim3(128), 0, s, w);  // persistent, 8 per CU (SR_THREADS)
@@ -600,8 +605,8 @@ int run_corpus(mox_engine* e, const Corpus& c) {
       }
     }
     if (getenv("MOX_VERBOSE"))
-      fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu; units %llu, k_reduce list %llu, split partitions %u, max sub-passes %u\n",
-              h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3], h.n_units, h.n_big, h.n_split, h.max_sub);
+      fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu; units %llu, k_reduce_sort2 list %llu, k_reduce list %llu, split partitions %u, max sub-passes %u\n",
+              h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3], h.n_units, h.n_mid, h.n_big, h.n_split, h.max_sub);
     if ((rc = check_failed(h))) return rc;
     if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
     if (h.halo_err != ~0ull)
@@ -1218,7 +1223,7 @@ void mox_engine_destroy(mox_engine* e) {
   void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_text,
-                  w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.u_uniq, w.u_uniq_off,
+                  w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.mid_units, w.small_units, w.u_uniq, w.u_uniq_off,
                   w.u_bytes, w.u_bytes_off, w.b_bytes, w.split_k, w.split_w};
   for (void* p : ptrs) dfree(p);
   for (DevBuf* b : {&e->x_send_short, &e->x_send_blob, &e->x_recv_short, &e->x_recv_blob, &e->g_counts, &e->g_offs,

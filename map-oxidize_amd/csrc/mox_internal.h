@@ -133,6 +133,8 @@ struct Ctl {
   unsigned int pad2;
   unsigned long long n_big;       // entries of big_units (k_reduce work list)
   unsigned long long short_bytes; // table bytes of the short words (long words follow)
+  unsigned long long n_mid;       // entries of mid_units (k_reduce_sort2 work list)
+  unsigned long long n_small;     // entries of small_units (k_reduce_small work list)
 };
 
 #ifdef MOX_CHECK
@@ -276,6 +278,8 @@ struct Work {  // device buffers of one engine
   uint64_t* spw_off;              // NB + 1: first split_w record of partition b
   UnitDesc* udesc;                // U_MAX: input ranges + output region of unit u
   uint32_t* big_units;            // U_MAX: units for k_reduce (whole partitions + oversized sub-buckets)
+  uint32_t* mid_units;            // U_MAX: count-1 units of SMALL_CAP + 1 .. 2 SMALL_CAP records (k_reduce_sort2)
+  uint32_t* small_units;          // U_MAX: units with weighted records, <= SMALL_CAP records (k_reduce_small)
   uint64_t* u_uniq;               // U_MAX: distinct keys of unit u
   uint64_t* u_bytes;              // U_MAX: key bytes of unit u's distinct keys
   uint64_t* u_bytes_off;          // U_MAX: byte offset of unit u inside its partition

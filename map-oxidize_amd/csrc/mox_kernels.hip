@@ -1756,6 +1756,8 @@ __device__ void unit_scan(const Work& w) {
     w.spw_off[NB] = tw;
     w.ctl->n_units = U;
     w.ctl->n_big = 0;  // k_split_scatter lists oversized sub-buckets (whole partitions: k_reduce workgroup b)
+    w.ctl->n_mid = 0;  // ... and the count-1 ones of up to 2 SMALL_CAP records (k_reduce_sort2)
+    w.ctl->n_small = 0;  // ... and the small ones with weighted records (k_reduce_small)
     w.ctl->red_ticket = 0;
     w.ctl->split_k = tk;
     w.ctl->split_w = tw;
@@ -1798,9 +1800,15 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
     if (sb < nsub) {
       const uint32_t u = u0 + sb;
       if (MOX_CHK(w, u < U_MAX, CHK_UNIT)) w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + ec + ew, c[j], d[j], b, kk};
-      if (c[j] + d[j] > SMALL_CAP) {
+      if (d[j] == 0 && c[j] > SMALL_CAP && c[j] <= 2 * SMALL_CAP) {  // count-1, up to twice sort1's size: k_reduce_sort2
+        const unsigned long long q = atomicAdd(&w.ctl->n_mid, 1ull);
+        if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.mid_units[q] = u;
+      } else if (c[j] + d[j] > SMALL_CAP) {
         const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
         if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
+      } else if (d[j] != 0) {  // weighted records, <= SMALL_CAP in all: k_reduce_small
+        const unsigned long long q = atomicAdd(&w.ctl->n_small, 1ull);
+        if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.small_units[q] = u;
       }
       cc[sb] = (uint32_t)ec;
       cw[sb] = (uint32_t)ew;
@@ -2173,12 +2181,14 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (w.ctl->overflow & OVF_RERUN) return;
   const uint32_t U = (uint32_t)w.ctl->n_units;
+  const uint32_t NS = (uint32_t)w.ctl->n_small;  // work list (k_split_scatter): the small units with weighted records
+  auto uid = [&](uint32_t t) { return w.small_units[t < NS ? t : NS - 1]; };
   const uint32_t G = gridDim.x;
   uint16_t* bin16 = reinterpret_cast<uint16_t*>(bins);
   __shared__ UnitDesc dring[2];  // descriptors of this and the next unit (written one unit ahead)
-  uint32_t u = blockIdx.x;
-  if (u >= U) return;
-  if (tid == 0) { dring[0] = load_desc(w, u, U); dring[1] = load_desc(w, u + G, U); sbytes = 0; }
+  uint32_t t = blockIdx.x;
+  if (t >= NS) return;
+  if (tid == 0) { dring[0] = load_desc(w, uid(t), U); dring[1] = load_desc(w, uid(t + G), U); sbytes = 0; }
   bins[tid] = 0;
   bins[tid + SR_THREADS] = 0;
 #pragma unroll
@@ -2195,7 +2205,8 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
 #else
 #define SR_MARK(k) do { } while (0)
 #endif
-  for (uint32_t it = 0; u < U; u += G, it++) {
+  for (uint32_t it = 0; t < NS; t += G, it++) {
+    const uint32_t u = uid(t);
     const UnitDesc d = dring[it & 1], dn = dring[(it + 1) & 1];
     bool cur_small = small_unit(d);
     // check builds: the unit's input and output ranges lie inside their buffers
@@ -2219,9 +2230,9 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
     }
     // the next unit's records and the descriptor after it: in flight during this unit
     SmallIn inn;
-    load_small(w, dn, u + G < U && small_unit(dn), inn);
+    load_small(w, dn, t + G < NS && small_unit(dn), inn);
     UnitDesc dnn;
-    if (tid == 0) dnn = load_desc(w, u + 2 * G, U);
+    if (tid == 0) dnn = load_desc(w, uid(t + 2 * G), U);
     if (cur_small) {
       lds_barrier();
       SR_MARK(0);
@@ -2400,6 +2411,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
 constexpr int S1_PER = SMALL_CAP / 64;  // records per lane
 constexpr int S1_WAVES = 4;             // waves per workgroup, one unit each
 static_assert(S1_PER == 8, "k_reduce_sort1: 8 records per lane");
+constexpr int S2_PER = 2 * S1_PER;      // k_reduce_sort2: units of SMALL_CAP + 1 .. 2 SMALL_CAP records
 // value of lane (lane ^ M)
 template <int M>
 __device__ __forceinline__ uint32_t xor_lane(uint32_t v) {
@@ -2412,24 +2424,25 @@ template <int M>
 __device__ __forceinline__ uint64_t xor_lane(uint64_t v) {
   return ((uint64_t)xor_lane<M>((uint32_t)(v >> 32)) << 32) | xor_lane<M>((uint32_t)v);
 }
-// bitonic compare-exchange with the lane (lane ^ M): the lower lane keeps the
-// minimum when this block sorts ascending
-template <int M, class T>
-__device__ __forceinline__ void s1_cross(T (&v)[S1_PER], int lane, uint32_t k) {
-  const bool keep_min = ((lane & M) == 0) == (((uint32_t)(lane * S1_PER) & k) == 0);
+// Bitonic sort of 64 x PER values in registers, position p = lane * PER + s.
+// Compare-exchange with the lane (lane ^ M): the lower lane keeps the minimum
+// when this block sorts ascending.
+template <int M, int PER, class T>
+__device__ __forceinline__ void s1_cross(T (&v)[PER], int lane, uint32_t k) {
+  const bool keep_min = ((lane & M) == 0) == (((uint32_t)(lane * PER) & k) == 0);
 #pragma unroll
-  for (int s = 0; s < S1_PER; s++) {
+  for (int s = 0; s < PER; s++) {
     const T pv = xor_lane<M>(v[s]);
     v[s] = ((pv < v[s]) == keep_min) ? pv : v[s];
   }
 }
-template <class T>
-__device__ __forceinline__ void s1_inlane(T (&v)[S1_PER], int lane, uint32_t k, int j) {
+template <int PER, class T>
+__device__ __forceinline__ void s1_inlane(T (&v)[PER], int lane, uint32_t k, int j) {
 #pragma unroll
-  for (int s = 0; s < S1_PER; s++) {
+  for (int s = 0; s < PER; s++) {
     const int t = s ^ j;
     if (t > s) {
-      const bool asc = ((uint32_t)(lane * S1_PER + s) & k) == 0;
+      const bool asc = ((uint32_t)(lane * PER + s) & k) == 0;
       const T a = v[s], b = v[t];
       const bool sw = (a > b) == asc;
       v[s] = sw ? b : a;
@@ -2437,26 +2450,135 @@ __device__ __forceinline__ void s1_inlane(T (&v)[S1_PER], int lane, uint32_t k, 
     }
   }
 }
-template <class T>
-__device__ __forceinline__ void s1_sort(T (&v)[S1_PER], int lane) {
+template <int PER, class T>
+__device__ __forceinline__ void s1_sort(T (&v)[PER], int lane) {
 #pragma unroll
-  for (uint32_t k = 2; k <= 512; k <<= 1) {
+  for (uint32_t k = 2; k <= 64u * PER; k <<= 1) {
 #pragma unroll
     for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      if (j >= 8) {
-        switch (j >> 3) {
-          case 1: s1_cross<1, T>(v, lane, k); break;
-          case 2: s1_cross<2, T>(v, lane, k); break;
-          case 4: s1_cross<4, T>(v, lane, k); break;
-          case 8: s1_cross<8, T>(v, lane, k); break;
-          case 16: s1_cross<16, T>(v, lane, k); break;
-          default: s1_cross<32, T>(v, lane, k); break;
+      if (j >= (uint32_t)PER) {
+        switch (j / PER) {
+          case 1: s1_cross<1, PER, T>(v, lane, k); break;
+          case 2: s1_cross<2, PER, T>(v, lane, k); break;
+          case 4: s1_cross<4, PER, T>(v, lane, k); break;
+          case 8: s1_cross<8, PER, T>(v, lane, k); break;
+          case 16: s1_cross<16, PER, T>(v, lane, k); break;
+          default: s1_cross<32, PER, T>(v, lane, k); break;
         }
       } else {
-        s1_inlane<T>(v, lane, k, (int)j);
+        s1_inlane<PER, T>(v, lane, k, (int)j);
       }
     }
   }
+}
+
+// One count-1 unit (n <= 64 PER records, keys k[s] = record s * 64 + lane)
+// reduced by one wave: key[] / hp[] are the wave's LDS arrays (64 PER keys,
+// 64 PER + 2 run heads).  IB index bits; the 32-bit sort key keeps 32 - IB
+// bits of (h32 below the unit bits, hash32b).
+template <int PER>
+__device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, const UnitDesc& d, const uint4 (&k)[PER],
+                                                 uint4* key, uint16_t* hp, int lane) {
+  constexpr uint32_t N = 64u * PER, IB = PER == 8 ? 9u : 10u, IM = N - 1;
+  static_assert((1u << IB) == N, "index bits");
+  const uint32_t n = d.in_n, shift = NB_LOG2 + d.kk;
+  uint32_t v[PER];
+#pragma unroll
+  for (int s = 0; s < PER; s++) {
+    const uint32_t i = (uint32_t)(s * 64 + lane);
+    const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
+    // sort key: the top 32 - IB bits of (h32 bits below the unit, hash32b) --
+    // the leading bits of the table order key_less -- then the record index.
+    // Padding ~0 cannot tie a real key: with padding present every real index
+    // is <= N - 2.
+    const uint32_t pre = (h << shift) | (hb >> (32 - shift));
+    v[s] = i < n ? ((pre & ~IM) | i) : ~0u;
+    if (i < n) key[i] = k[s];
+  }
+  s1_sort<PER, uint32_t>(v, lane);
+  // run heads: hash bits differ from the previous position's
+  uint32_t idx[PER];
+  uint32_t hm = 0, bad = 0;
+  wave_lds_fence();  // key[] written by every lane
+  {
+    uint32_t prev = from_prev_lane(v[PER - 1]);
+#pragma unroll
+    for (int s = 0; s < PER; s++) {
+      const uint32_t p = (uint32_t)(lane * PER + s);
+      const bool valid = p < n;
+      const bool head = valid && (p == 0 || (v[s] >> IB) != (prev >> IB));
+      if (head) hm |= 1u << s;
+      if (valid && !head) bad |= key_eq16(key[v[s] & IM], key[prev & IM]) ? 0u : 1u;
+      idx[s] = v[s] & IM;
+      prev = v[s];
+    }
+  }
+  if (__any(bad != 0)) {
+    // two different keys share the sort-key hash bits (~0.5 % of C4's units):
+    // sort again on 64-bit keys -- the h32 bits below the unit, all of
+    // hash32b, the index -- which is key_less order whenever (h32, hash32b)
+    // differ
+    uint64_t v2[PER];
+#pragma unroll
+    for (int s = 0; s < PER; s++) {
+      const uint32_t i = (uint32_t)(s * 64 + lane);
+      const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
+      const uint64_t pre = ((uint64_t)(shift >= 32 ? 0u : (h << shift) >> shift) << (32 + IB)) | ((uint64_t)hb << IB);
+      v2[s] = i < n ? (pre | i) : ~0ull;
+    }
+    s1_sort<PER, uint64_t>(v2, lane);
+    uint64_t prev = ((uint64_t)from_prev_lane((uint32_t)(v2[PER - 1] >> 32)) << 32) | from_prev_lane((uint32_t)v2[PER - 1]);
+    hm = 0;
+    bad = 0;
+#pragma unroll
+    for (int s = 0; s < PER; s++) {
+      const uint32_t p = (uint32_t)(lane * PER + s);
+      const bool valid = p < n;
+      const bool head = valid && (p == 0 || (v2[s] >> IB) != (prev >> IB));
+      if (head) hm |= 1u << s;
+      if (valid && !head) bad |= key_eq16(key[(uint32_t)v2[s] & IM], key[(uint32_t)prev & IM]) ? 0u : 1u;
+      idx[s] = (uint32_t)v2[s] & IM;
+      prev = v2[s];
+    }
+  }
+  if (__any(bad != 0)) {  // (h32, hash32b) shared by two keys: k_reduce resolves this unit
+    if (lane == 0) {
+      const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
+      if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
+    }
+  } else {
+    const uint32_t nh = (uint32_t)__popc(hm);
+    const uint32_t incl = wave_incl_scan(nh);
+    const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    uint32_t o = incl - nh;
+#pragma unroll
+    for (int s = 0; s < PER; s++)
+      if ((hm >> s) & 1u) hp[o++] = (uint16_t)(lane * PER + s);
+    if (lane == 0) hp[nu] = (uint16_t)n;
+    wave_lds_fence();
+    o = incl - nh;
+    uint32_t lb = 0;
+#pragma unroll
+    for (int s = 0; s < PER; s++) {
+      if ((hm >> s) & 1u) {
+        const uint32_t p = (uint32_t)(lane * PER + s);
+        const uint4 kk = key[idx[s]];
+        if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {
+          w.uk[d.rec_off + o] = kk;
+          w.uc[d.rec_off + o] = (unsigned long long)(hp[o + 1] - p);
+        }
+        lb += key_len16(kk);
+        o++;
+      }
+    }
+    uint32_t tb = lb;
+    for (int off = 32; off > 0; off >>= 1) tb += __shfl_xor(tb, off);
+    if (lane == 0) {
+      w.u_uniq[u] = nu;
+      w.u_bytes[u] = tb;
+    }
+  }  // no collision
+  wave_lds_fence();  // this unit's LDS reads before the next unit's writes
 }
 
 extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Work w) {
@@ -2495,112 +2617,40 @@ extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Wo
     const UnitDesc dnn = w.udesc[u + 2 * GW < U ? u + 2 * GW : U - 1];
     uint4 kn[S1_PER];
     load_keys(dn, u + GW < U && ok_unit(dn), kn);
-    const bool ok = ok_unit(d);
-    const uint32_t n = d.in_n, shift = NB_LOG2 + d.kk;
-    if (ok) {
-      uint32_t v[S1_PER];
-#pragma unroll
-      for (int s = 0; s < S1_PER; s++) {
-        const uint32_t i = (uint32_t)(s * 64 + lane);
-        const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
-        // sort key: the top 23 bits of (h32 bits below the unit, hash32b) --
-        // the leading bits of the table order key_less -- then the record
-        // index (9 bits).  Padding ~0 cannot tie a real key: with padding
-        // present every real index is <= 510.
-        const uint32_t pre = (h << shift) | (hb >> (32 - shift));
-        v[s] = i < n ? ((pre & ~511u) | i) : ~0u;
-        if (i < n) key[i] = k[s];
-      }
-      s1_sort(v, lane);
-      // run heads: hash bits differ from the previous position's
-      uint32_t idx[S1_PER];
-      uint32_t hm = 0, bad = 0;
-      wave_lds_fence();  // key[] written by every lane
-      {
-        uint32_t prev = from_prev_lane(v[S1_PER - 1]);
-#pragma unroll
-        for (int s = 0; s < S1_PER; s++) {
-          const uint32_t p = (uint32_t)(lane * S1_PER + s);
-          const bool valid = p < n;
-          const bool head = valid && (p == 0 || (v[s] >> 9) != (prev >> 9));
-          if (head) hm |= 1u << s;
-          if (valid && !head) bad |= key_eq16(key[v[s] & 511u], key[prev & 511u]) ? 0u : 1u;
-          idx[s] = v[s] & 511u;
-          prev = v[s];
-        }
-      }
-      if (__any(bad != 0)) {
-        // two different keys share the 23 sort-key hash bits (~0.5 % of C4's
-        // units): sort again on 64-bit keys -- the 10 h32 bits below the unit,
-        // all of hash32b, the index -- which is key_less order whenever
-        // (h32, hash32b) differ
-        uint64_t v2[S1_PER];
-#pragma unroll
-        for (int s = 0; s < S1_PER; s++) {
-          const uint32_t i = (uint32_t)(s * 64 + lane);
-          const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
-          const uint64_t pre = ((uint64_t)(shift >= 32 ? 0u : (h << shift) >> shift) << 41) | ((uint64_t)hb << 9);
-          v2[s] = i < n ? (pre | i) : ~0ull;
-        }
-        s1_sort(v2, lane);
-        uint64_t prev = ((uint64_t)from_prev_lane((uint32_t)(v2[S1_PER - 1] >> 32)) << 32) |
-                        from_prev_lane((uint32_t)v2[S1_PER - 1]);
-        hm = 0;
-        bad = 0;
-#pragma unroll
-        for (int s = 0; s < S1_PER; s++) {
-          const uint32_t p = (uint32_t)(lane * S1_PER + s);
-          const bool valid = p < n;
-          const bool head = valid && (p == 0 || (v2[s] >> 9) != (prev >> 9));
-          if (head) hm |= 1u << s;
-          if (valid && !head) bad |= key_eq16(key[(uint32_t)v2[s] & 511u], key[(uint32_t)prev & 511u]) ? 0u : 1u;
-          idx[s] = (uint32_t)v2[s] & 511u;
-          prev = v2[s];
-        }
-      }
-      if (__any(bad != 0)) {  // (h32, hash32b) shared by two keys: k_reduce resolves this unit
-        if (lane == 0) {
-          const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
-          if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
-        }
-      } else {
-        const uint32_t nh = (uint32_t)__popc(hm);
-        const uint32_t incl = wave_incl_scan(nh);
-        const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        uint32_t o = incl - nh;
-#pragma unroll
-        for (int s = 0; s < S1_PER; s++)
-          if ((hm >> s) & 1u) hp[o++] = (uint16_t)(lane * S1_PER + s);
-        if (lane == 0) hp[nu] = (uint16_t)n;
-        wave_lds_fence();
-        o = incl - nh;
-        uint32_t lb = 0;
-#pragma unroll
-        for (int s = 0; s < S1_PER; s++) {
-          if ((hm >> s) & 1u) {
-            const uint32_t p = (uint32_t)(lane * S1_PER + s);
-            const uint4 kk = key[idx[s]];
-            if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {
-              w.uk[d.rec_off + o] = kk;
-              w.uc[d.rec_off + o] = (unsigned long long)(hp[o + 1] - p);
-            }
-            lb += key_len16(kk);
-            o++;
-          }
-        }
-        uint32_t tb = lb;
-        for (int off = 32; off > 0; off >>= 1) tb += __shfl_xor(tb, off);
-        if (lane == 0) {
-          w.u_uniq[u] = nu;
-          w.u_bytes[u] = tb;
-        }
-      }  // no collision
-      wave_lds_fence();  // this unit's LDS reads before the next unit's writes
-    }  // ok
+    if (ok_unit(d)) sort_reduce_unit<S1_PER>(w, u, d, k, key, hp, lane);
     d = dn;
     dn = dnn;
 #pragma unroll
     for (int s = 0; s < S1_PER; s++) k[s] = kn[s];
+  }
+}
+
+// k_reduce_sort2: the count-1 units of SMALL_CAP + 1 .. 2 SMALL_CAP records
+// (listed by k_split_scatter in mid_units; C4 16 GiB: ~2.4 % of its units,
+// where a few 4-letter words repeated ~70 times each land in one sub-bucket),
+// one wave each with 16 records per lane -- the same reduction as
+// k_reduce_sort1 instead of a 1024-thread k_reduce workgroup per unit.
+extern "C" __global__ __launch_bounds__(64) void k_reduce_sort2(Work w) {
+  __shared__ uint4 key[2 * SMALL_CAP];
+  __shared__ uint16_t hp[2 * SMALL_CAP + 2];
+  const int lane = threadIdx.x;
+  if (w.ctl->overflow & OVF_RERUN) return;
+  const uint32_t nm = (uint32_t)w.ctl->n_mid;
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  for (uint32_t t = blockIdx.x; t < nm; t += gridDim.x) {
+    const uint32_t u = w.mid_units[t];
+    const UnitDesc d = w.udesc[u];
+    if (!MOX_CHK(w, d.in_n <= 2 * SMALL_CAP && d.in_off + d.in_n <= w.split_k_cap && d.rec_off + d.in_n <= w.uniq_cap,
+                 CHK_SMALL_DESC))
+      continue;
+    uint4 k[S2_PER];
+#pragma unroll
+    for (int s = 0; s < S2_PER; s++) {
+      const uint32_t i = (uint32_t)(s * 64 + lane);
+      const u32x4 x = *reinterpret_cast<const u32x4*>(w.split_k + d.in_off + (i < d.in_n ? i : 0u));
+      k[s] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+    sort_reduce_unit<S2_PER>(w, u, d, k, key, hp, lane);
   }
 }
 
