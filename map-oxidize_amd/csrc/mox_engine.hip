@@ -195,7 +195,7 @@ Caps initial_caps(uint64_t n, int map_grid) {
 void free_sized(mox_engine* e) {
   FREE_FIELD(cold); FREE_FIELD(spill);
   FREE_FIELD(w); FREE_FIELD(w_sorted); FREE_FIELD(u); FREE_FIELD(arena); FREE_FIELD(ltab); FREE_FIELD(lpos);
-  FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
+  FREE_FIELD(uk); FREE_FIELD(uc); FREE_FIELD(ui); FREE_FIELD(t_counts); FREE_FIELD(t_offs); FREE_FIELD(t_bytes);
   FREE_FIELD(split_k); FREE_FIELD(split_w);
   Work& w = e->w;
   w.cold_cap = w.spill_cap = 0;
@@ -228,7 +228,7 @@ int realloc_sized(mox_engine* e, const Caps& c) {
       {(void**)&n.w, n.w_cap * sizeof(WRec)}, {(void**)&n.w_sorted, n.w_cap * sizeof(WRec)},
       {(void**)&n.u, n.u_cap * sizeof(URec)}, {(void**)&n.arena, n.arena_cap},
       {(void**)&n.ltab, n.long_cap * sizeof(LSlot)}, {(void**)&n.lpos, (n.long_cap + 1) * 8},
-      {(void**)&n.uk, n.uniq_cap * 16}, {(void**)&n.uc, n.uniq_cap * 8},
+      {(void**)&n.uk, n.uniq_cap * 16}, {(void**)&n.uc, n.uniq_cap * 8}, {(void**)&n.ui, n.uniq_cap * 4},
       {(void**)&n.t_counts, n.table_cap * 8}, {(void**)&n.t_offs, (n.table_cap + 1) * 8},
       {(void**)&n.t_bytes, n.bytes_cap}, {(void**)&n.split_k, n.split_k_cap * 16},
       {(void**)&n.split_w, n.split_w_cap * sizeof(WRec)}};
@@ -1222,7 +1222,7 @@ void mox_engine_destroy(mox_engine* e) {
   Work& w = e->w;
   void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
-                  w.uk, w.uc, w.t_counts, w.t_offs, w.t_bytes, e->d_text,
+                  w.uk, w.uc, w.ui, w.t_counts, w.t_offs, w.t_bytes, e->d_text,
                   w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.mid_units, w.small_units, w.u_uniq, w.u_uniq_off,
                   w.u_bytes, w.u_bytes_off, w.b_bytes, w.split_k, w.split_w};
   for (void* p : ptrs) dfree(p);

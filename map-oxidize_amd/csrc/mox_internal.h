@@ -219,6 +219,9 @@ struct Tables {  // Unicode case data in device memory
 // weighted records) or one sub-bucket of a split partition (contiguous ranges of
 // split_k / split_w).  Output: uk / uc from rec_off.
 constexpr uint32_t UNIT_WHOLE = 0xFFFFFFFFu;
+// u_uniq[u] flag: unit u's distinct keys are in ui[] (record index into the
+// unit's split_k range + count) instead of uk[] / uc[]
+constexpr uint64_t U_IDX = 1ull << 62;
 struct UnitDesc {
   uint64_t in_off, win_off, rec_off;
   uint32_t in_n, win_n, part, kk;
@@ -297,6 +300,7 @@ struct Work {  // device buffers of one engine
   // reduce output (capacity = records)
   uint4* uk;                      // keys
   uint64_t* uc;                   // counts
+  uint32_t* ui;                   // count-1 units (k_reduce_sort1/2, u_uniq[u] & U_IDX): (record index << 16) | count
   uint64_t uniq_cap;
   // long uniques compaction
   uint64_t* lpos;                 // long_cap (scan of occupancy)

@@ -2558,23 +2558,22 @@ __device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, cons
     wave_lds_fence();
     o = incl - nh;
     uint32_t lb = 0;
+    // distinct keys as (record index, count) in 4 bytes each: k_mat takes the
+    // key bytes from the unit's split_k range (no 24-byte uk / uc round trip)
 #pragma unroll
     for (int s = 0; s < PER; s++) {
       if ((hm >> s) & 1u) {
         const uint32_t p = (uint32_t)(lane * PER + s);
-        const uint4 kk = key[idx[s]];
-        if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT)) {
-          w.uk[d.rec_off + o] = kk;
-          w.uc[d.rec_off + o] = (unsigned long long)(hp[o + 1] - p);
-        }
-        lb += key_len16(kk);
+        if (MOX_CHK(w, o < n && d.rec_off + o < w.uniq_cap, CHK_SMALL_OUT))
+          w.ui[d.rec_off + o] = (idx[s] << 16) | (uint32_t)(hp[o + 1] - p);
+        lb += key_len16(key[idx[s]]);
         o++;
       }
     }
     uint32_t tb = lb;
     for (int off = 32; off > 0; off >>= 1) tb += __shfl_xor(tb, off);
     if (lane == 0) {
-      w.u_uniq[u] = nu;
+      w.u_uniq[u] = nu | U_IDX;
       w.u_bytes[u] = tb;
     }
   }  // no collision
@@ -2675,7 +2674,7 @@ __device__ __forceinline__ void unit_uniq_scan(const Work& w) {
 #pragma unroll
     for (int j = 0; j < SUB_PER_T; j++) {
       const uint32_t sb = SUB_PER_T * tid + j;
-      v[j] = sb < nsub ? w.u_uniq[u0 + sb] : 0;
+      v[j] = sb < nsub ? w.u_uniq[u0 + sb] & ~U_IDX : 0;
       y[j] = sb < nsub ? w.u_bytes[u0 + sb] : 0;
       sv += v[j];
       sy += y[j];
@@ -2836,7 +2835,8 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
   for (uint32_t u = blockIdx.x * MAT_WAVES + wv; u < U; u += gridDim.x * MAT_WAVES) {
     const UnitDesc ud = w.udesc[u];
     if (ud.in_n == UNIT_WHOLE) continue;
-    const uint64_t n = w.u_uniq[u];
+    const uint64_t nf = w.u_uniq[u], n = nf & ~U_IDX;
+    const bool byidx = (nf & U_IDX) != 0;  // count-1 unit: (record index, count) pairs
     const uint64_t src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
     uint64_t boff = w.bytes_off[ud.part] + w.u_bytes_off[u];
     uint8_t* st = stage + wv * WSTAGE;
@@ -2845,7 +2845,17 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
       uint4 k = make_uint4(0, 0, 0, 0);
       uint32_t len = 0;
       unsigned long long cnt = 0;
-      if (i < n) { k = w.uk[src0 + i]; cnt = w.uc[src0 + i]; len = key_len16(k); }
+      if (i < n) {
+        if (byidx) {
+          const uint32_t v = w.ui[src0 + i];
+          k = w.split_k[ud.in_off + (v >> 16)];
+          cnt = v & 0xFFFFu;
+        } else {
+          k = w.uk[src0 + i];
+          cnt = w.uc[src0 + i];
+        }
+        len = key_len16(k);
+      }
       const uint32_t incl = wave_incl_scan(len);
       const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
       if (i < n) mat_word(w, st, dst0 + i, boff, incl - len, k, len, cnt);
@@ -2910,10 +2920,19 @@ extern "C" __global__ void k_xpack_short(Work w, WRec* out) {
   const uint32_t U = (uint32_t)w.ctl->n_units;
   for (uint32_t u = blockIdx.x; u < U; u += gridDim.x) {
     const UnitDesc ud = w.udesc[u];
-    const uint64_t n = w.u_uniq[u], src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
+    const uint64_t nf = w.u_uniq[u], n = nf & ~U_IDX, src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
     for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const uint4 k = w.uk[src0 + i];
-      out[dst0 + i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, w.uc[src0 + i]};
+      uint4 k;
+      unsigned long long cnt;
+      if (nf & U_IDX) {
+        const uint32_t v = w.ui[src0 + i];
+        k = w.split_k[ud.in_off + (v >> 16)];
+        cnt = v & 0xFFFFu;
+      } else {
+        k = w.uk[src0 + i];
+        cnt = w.uc[src0 + i];
+      }
+      out[dst0 + i] = WRec{((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, cnt};
     }
   }
 }
