@@ -212,7 +212,7 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   (void)hipDeviceSynchronize();
   free_sized(e);
   Work n = e->w;
-  n.cold_cap = (uint32_t)std::min<uint64_t>(c.cold_cap, 0xFFFFFFF0u);
+  n.cold_cap = (uint32_t)std::min<uint64_t>((c.cold_cap + 1) & ~1ull, 0xFFFFFFF0u);  // even: k_map's paired records stay sector-aligned
   n.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
   n.w_cap = c.w_cap;
   n.u_cap = c.u_cap;

@@ -240,6 +240,10 @@ __device__ __forceinline__ uint32_t dict_home(uint32_t h) { return h & (DICT_SLO
 __device__ __forceinline__ uint32_t dict_g1(uint32_t h) { return (h & (DICT_SLOTS - 1)) >> 2; }
 __device__ __forceinline__ uint32_t dict_g2(uint32_t h) { return (h >> 12) & (DICT_BUCKETS - 1); }
 
+// LDS pair slot states (k_map without a dictionary, k_split_scatter): a
+// record waits in its slot until the next record for the same region arrives,
+// and the pair goes out as one aligned 32-byte sector.
+constexpr uint32_t PS_EMPTY = 0u, PS_BUSY = 1u, PS_FULL = 2u;
 struct MapLds {
   uint4* dtag4;     // DICT_BUCKETS x 4 tags (0 = empty)
   uint4* dkey;      // DICT_SLOTS 16-byte keys
@@ -247,6 +251,9 @@ struct MapLds {
   uint32_t* bcnt;   // NB: cold records this workgroup wrote per partition
   uint32_t* misc;   // [0] spills [1] row ticket
   uint4* masktab;   // [17]: byte masks keeping the first len bytes of a 16-byte key
+  // no dictionary (dict_n == 0): pair slots per partition, inside dkey's space
+  uint4* pend;      // NB parked records
+  uint32_t* pst;    // NB slot states (PS_*)
 };
 
 typedef const __attribute__((address_space(4))) Work* KWork;  // constant (kernarg) address space: scalar loads
@@ -315,10 +322,61 @@ __device__ __forceinline__ void cold_spill(const MapCtx& m, uint4 key) {
   }
   atomicOr(&rare(m).ctl->overflow, OVF_POOL);
 }
+// No dictionary: records go out in pairs (one aligned 32-byte sector each; a
+// lone 16-byte store costs the memory a read-modify-write).  Three-state LDS
+// slot per partition; a lane that finds it BUSY retries, and the BUSY holder
+// finishes within the same loop iteration, so no lane waits on another's
+// progress.  Regions start at even records (cold_cap is even).
+// One attempt of the pair protocol on slot `slot` for record k: true when the
+// record was parked or paired.  *q gets the parked partner when paired.
+__device__ __forceinline__ int pair_try(uint32_t* pst, uint4* pend, uint32_t slot, uint4 k, uint4* q) {
+  uint32_t st = PS_EMPTY;
+  if (__hip_atomic_compare_exchange_strong(&pst[slot], &st, PS_BUSY, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP)) {
+    pend[slot] = k;
+    __hip_atomic_store(&pst[slot], PS_FULL, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return 1;  // parked
+  }
+  if (st == PS_FULL && __hip_atomic_compare_exchange_strong(&pst[slot], &st, PS_BUSY, __ATOMIC_ACQUIRE,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+    *q = pend[slot];
+    __hip_atomic_store(&pst[slot], PS_EMPTY, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return 2;  // paired with *q
+  }
+  return 0;  // BUSY: retry
+}
+// The retry loop is a wave-level loop (exit when no lane is left) whose body
+// ends in a wave barrier: a lane's slot stores stay inside the iteration in
+// which it won the slot.  (A per-lane `while (!done)` loop lets the compiler
+// sink them past the loop exit, where the winning lane waits for the spinning
+// lanes of its own wave: a SIMT deadlock.)
+__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t b, uint4 key) {
+  bool done = false;
+  do {
+    if (!done) {
+      uint4 q;
+      const int r = pair_try(m.s.pst, m.s.pend, b, key, &q);
+      if (r == 2) {
+        const uint32_t pos = atomicAdd(&m.s.bcnt[b], 2u);
+        if (pos + 1 < m.w.cold_cap) {
+          uint4* o = m.w.cold + ((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos;
+          o[0] = q;
+          o[1] = key;
+        } else {
+          cold_spill(m, q);
+          cold_spill(m, key);
+        }
+      }
+      done = r != 0;
+    }
+    __builtin_amdgcn_wave_barrier();
+  } while (__any(!done));
+}
 __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+  if (m.dict_n == 0) { cold_pair(m, b, key); return; }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < m.w.cold_cap) {
     m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
@@ -604,6 +662,30 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
   }
 }
 
+// Token pass without a dictionary (high-cardinality input): every list entry
+// straight to the cold path.
+template <int TU>
+__device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
+                                       uint32_t total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t e[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    const uint32_t j = j0 + u * 64 + lane;
+    const uint32_t r = list[j < TOKMAX ? j : TOKMAX - 1];
+    e[u] = j < total ? r : 0x8000u;  // inactive = odd
+  }
+  uint32_t K[TU][4];
+#pragma unroll
+  for (int u = 0; u < TU; u++) key_at(m.s, rowbuf, e[u], K[u]);
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    if (e[u] & 0x8000u) continue;
+    const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
+    cold_word(m, hash32(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1);
+  }
+}
+
 // per-phase cycle accounting of a map consumer wave (-DMOX_STAMP builds only)
 struct Cyc {
   uint64_t wait, byte, pa, pb, miss, rows;
@@ -720,6 +802,14 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
   uint64_t t1 = 0;
   if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
+  if (m.dict_n == 0) {  // no dictionary: no probes (uniform branch)
+    for (uint32_t j0 = 0; j0 < total;) {
+      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, total); j0 += 128; }
+      else { pass_c<1>(m, rowbuf, list, j0, total); j0 += 64; }
+    }
+    wave_lds_fence();
+    return;
+  }
   uint32_t nmiss = 0;
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
@@ -765,6 +855,9 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
   m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
   m.s.masktab = (uint4*)sp; sp += 17 * 16;
+  m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
+  m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB);       // = PS_EMPTY
+  static_assert(NB * 16 + NB * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
@@ -884,6 +977,15 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #endif
   }
   __syncthreads();
+  if (m.dict_n == 0) {  // records still parked in pair slots: written as singles
+    for (int i = tid; i < NB; i += MAP_THREADS) {
+      if (m.s.pst[i] != PS_FULL) continue;
+      const uint32_t pos = atomicAdd(&m.s.bcnt[i], 1u);
+      if (pos < w.cold_cap) w.cold[((uint64_t)blockIdx.x * NB + i) * w.cold_cap + pos] = m.s.pend[i];
+      else cold_spill(m, m.s.pend[i]);
+    }
+    __syncthreads();
+  }
   if (m.dict_n) {
     for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
       const uint32_t cnt = m.s.dcnt[i];
@@ -1099,8 +1201,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_hist(Work w) {
   if (threadIdx.x < 256 && h[threadIdx.x]) atomicAdd(&w.dict_hist[threadIdx.x], h[threadIdx.x]);
 }
 
+constexpr uint32_t DICT_MIN_COVER_INV = 20;  // a dictionary must cover >= 1/20 of the sampled tokens
 extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t max_words) {
   __shared__ uint32_t T, ST, h[256];
+  __shared__ unsigned long long cov[2];
   if (threadIdx.x < 256) h[threadIdx.x] = w.dict_hist[threadIdx.x];
   __syncthreads();
   // T = smallest count class cc >= 2 whose suffix sum S(cc) = sum_{c >= cc} h[c]
@@ -1119,6 +1223,22 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
     if (threadIdx.x < 256 && cc == (int)T) ST = (uint32_t)(ex + x);  // S(T): words picked whole
     if (threadIdx.x == 0) {
       if (T > 255) T = 256;  // nothing fits: pick nothing
+      cov[0] = 0;
+      cov[1] = 0;
+    }
+    __syncthreads();
+    // coverage: sampled tokens of the classes picked whole / all sampled
+    // tokens.  Under DICT_MIN_COVER the dictionary would save next to nothing
+    // (high-cardinality input): none is built, and k_map then sends every
+    // token straight to the cold path (no probes) with paired sector writes.
+    if (threadIdx.x < 256 && cc >= 1 && x) {
+      const unsigned long long tok = x * (unsigned long long)cc;
+      atomicAdd(&cov[0], tok);
+      if ((uint32_t)cc >= T) atomicAdd(&cov[1], tok);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      if (cov[1] < cov[0] / DICT_MIN_COVER_INV) T = 256;
       if (blockIdx.x == 0) w.ctl->dict_thresh = T;
     }
     __syncthreads();
@@ -1715,6 +1835,11 @@ __device__ __forceinline__ void split_count(const Work& w) {
   for (uint32_t i = tid; i < nsub; i += blockDim.x) { o[i] = hc[i]; o[SUB_N + i] = hw[i]; }
 }
 
+// split_k records reserved for a split partition of n cold records in 2^kk
+// sub-buckets: every sub-bucket starts at an even record (32-byte aligned) so
+// that k_split_scatter's record pairs fill whole 32-byte sectors; even total.
+__device__ __forceinline__ uint64_t split_span(uint64_t n, uint32_t kk) { return (n + (1ull << kk) + 1) & ~1ull; }
+
 // One workgroup of SC_THREADS threads, SC_PER consecutive partitions each:
 // units per partition, split-buffer offsets, the reduce work-queue reset, and
 // the output region of every whole partition.
@@ -1729,7 +1854,7 @@ __device__ void unit_scan(const Work& w) {
     const uint32_t b = SC_PER * t + j;
     kk[j] = w.b_kk[b];
     nu += 1ull << kk[j];
-    nk += kk[j] ? w.b_recs[b] : 0;
+    nk += kk[j] ? split_span(w.b_recs[b], kk[j]) : 0;
     nw += kk[j] ? w.b_w[b] : 0;
     nwh += kk[j] ? 0 : 1;
   }
@@ -1747,7 +1872,7 @@ __device__ void unit_scan(const Work& w) {
     w.spw_off[b] = ow;
     if (!kk[j]) w.udesc[ub] = UnitDesc{0, 0, w.rec_off[b], UNIT_WHOLE, 0, b, 0};
     ub += 1ull << kk[j];
-    ok += kk[j] ? w.b_recs[b] : 0;
+    ok += kk[j] ? split_span(w.b_recs[b], kk[j]) : 0;
     ow += kk[j] ? w.b_w[b] : 0;
   }
   if (t == 0) {
@@ -1771,8 +1896,18 @@ extern "C" __global__ __launch_bounds__(SC_THREADS) void k_unit_scan(Work w) { u
 // k_split_scatter (one workgroup per split partition): unit directory from the
 // histogram, then every record of the partition to its unit's contiguous range
 // (LDS cursors: the workgroup owns the whole partition, no global atomics).
+// Records are written in pairs: a sub-bucket's first record waits in an LDS
+// slot until the next one arrives, and the pair goes out as one aligned
+// 32-byte sector (a lone 16-byte store leaves half a sector, which costs the
+// memory a read-modify-write: PMC WRITE_SIZE was 2x the records).  The slot is
+// a three-state LDS lock (EMPTY / BUSY / FULL): a lane that finds it BUSY
+// retries, and the BUSY holder finishes within the same loop iteration, so no
+// lane ever waits on another wave's progress.  Leftover single records are
+// written after the stream.
 extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   __shared__ uint32_t cc[SUB_N], cw[SUB_N];
+  __shared__ uint32_t pst[SUB_N];
+  __shared__ uint4 pend[SUB_N];
   __shared__ uint64_t wsum[16];
   const uint32_t b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -1781,25 +1916,27 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   const uint32_t nsub = 1u << kk, u0 = w.u_base[b];
   const uint32_t* hist = w.sub_hist + (uint64_t)b * 2 * SUB_N;
   // sub-buckets SUB_PER_T t .. SUB_PER_T t + SUB_PER_T - 1 per thread
-  uint32_t c[SUB_PER_T], d[SUB_PER_T], sc = 0, sd = 0;
+  uint32_t c[SUB_PER_T], d[SUB_PER_T], sc = 0, sd = 0, sr = 0;
 #pragma unroll
   for (int j = 0; j < SUB_PER_T; j++) {
     const uint32_t sb = SUB_PER_T * tid + j;
     c[j] = sb < nsub ? hist[sb] : 0;
     d[j] = sb < nsub ? hist[SUB_N + sb] : 0;
-    sc += c[j];
+    sc += (c[j] + 1) & ~1u;  // split_k: even starts
     sd += d[j];
+    sr += c[j];              // output region: records, no padding
   }
-  uint64_t tc, tw;
+  uint64_t tc, tw, tr;
   uint64_t ec = block_exscan(sc, wsum, tc);
   uint64_t ew = block_exscan(sd, wsum, tw);
+  uint64_t er = block_exscan(sr, wsum, tr);
   const uint64_t kb = w.sp_off[b], wb = w.spw_off[b], rb = w.rec_off[b];
 #pragma unroll
   for (int j = 0; j < SUB_PER_T; j++) {
     const uint32_t sb = SUB_PER_T * tid + j;
     if (sb < nsub) {
       const uint32_t u = u0 + sb;
-      if (MOX_CHK(w, u < U_MAX, CHK_UNIT)) w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + ec + ew, c[j], d[j], b, kk};
+      if (MOX_CHK(w, u < U_MAX, CHK_UNIT)) w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + er + ew, c[j], d[j], b, kk};
       if (d[j] == 0 && c[j] > SMALL_CAP && c[j] <= 2 * SMALL_CAP) {  // count-1, up to twice sort1's size: k_reduce_sort2
         const unsigned long long q = atomicAdd(&w.ctl->n_mid, 1ull);
         if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.mid_units[q] = u;
@@ -1812,15 +1949,34 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
       }
       cc[sb] = (uint32_t)ec;
       cw[sb] = (uint32_t)ew;
+      pst[sb] = PS_EMPTY;
     }
-    ec += c[j];
+    ec += (c[j] + 1) & ~1u;
     ew += d[j];
+    er += c[j];
   }
   __syncthreads();
   uint4* ok = w.split_k + kb;
+  // (the lambda runs under a per-record lane mask; the pair loop is the same
+  // wave-level loop as k_map's cold_pair)
   for_partition_cold(w, b, [&](uint4 k) {
-    const uint32_t p = atomicAdd(&cc[hbits(hash32(k.x, k.y, k.z, k.w), NB_LOG2, kk)], 1u);
-    if (MOX_CHK(w, p < tc && kb + p < w.split_k_cap, CHK_SPLIT_K)) ok[p] = k;
+    const uint32_t sb = hbits(hash32(k.x, k.y, k.z, k.w), NB_LOG2, kk);
+    bool done = false;
+    do {
+      if (!done) {
+        uint4 q;
+        const int r = pair_try(pst, pend, sb, k, &q);
+        if (r == 2) {  // second of a pair: the pair goes out as one sector
+          const uint32_t p = atomicAdd(&cc[sb], 2u);
+          if (MOX_CHK(w, p + 1 < tc && kb + p + 1 < w.split_k_cap, CHK_SPLIT_K)) {
+            ok[p] = q;
+            ok[p + 1] = k;
+          }
+        }
+        done = r != 0;
+      }
+      __builtin_amdgcn_wave_barrier();
+    } while (__any(!done));
   });
   const uint64_t w0 = w.w_off[b], w1 = w.w_off[b + 1];
   WRec* ow = w.split_w + wb;
@@ -1828,6 +1984,16 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
     const WRec r = w.w_sorted[i];
     const uint32_t p = atomicAdd(&cw[hbits(key_hash(r.w0, r.w1), NB_LOG2, kk)], 1u);
     if (MOX_CHK(w, p < tw && wb + p < w.split_w_cap, CHK_SPLIT_W)) ow[p] = r;
+  }
+  __syncthreads();
+  // leftover singles (odd counts)
+#pragma unroll
+  for (int j = 0; j < SUB_PER_T; j++) {
+    const uint32_t sb = SUB_PER_T * tid + j;
+    if (sb < nsub && pst[sb] == PS_FULL) {
+      const uint32_t p = cc[sb];
+      if (MOX_CHK(w, p < tc && kb + p < w.split_k_cap, CHK_SPLIT_K)) ok[p] = pend[sb];
+    }
   }
 }
 
@@ -2782,17 +2948,28 @@ __device__ __forceinline__ void mat_flush(const Work& w, const uint8_t* st, uint
     w.t_bytes[boff + t] = st[(boff - gbase) + t];
   }
 }
-// One word of a step: its count, offset and (staged) bytes.
+// One word of a step: its count, offset and (staged) bytes.  The stage is
+// zeroed first and each key is OR-ed in as 5 byte-shifted dwords (its zero
+// padding ORs nothing into the next word's bytes): 5 LDS atomics instead of
+// one byte store per key byte.
 __device__ __forceinline__ void mat_word(const Work& w, uint8_t* st, uint64_t dst, uint64_t boff, uint32_t ex, uint4 k,
                                          uint32_t len, unsigned long long cnt) {
   if (!MOX_CHK(w, dst < w.table_cap && boff + ex + len <= w.bytes_cap, CHK_MAT_ROW)) return;
   w.t_counts[dst] = cnt;
   w.t_offs[dst] = boff + ex;
-  const uint32_t sh = (uint32_t)(boff & 15ull);
-  const uint32_t kw[4] = {k.x, k.y, k.z, k.w};
+  const uint32_t o = (uint32_t)(boff & 15ull) + ex, r = o & 3u;
+  uint32_t* d = reinterpret_cast<uint32_t*>(st) + (o >> 2);
+  const uint32_t kw[5] = {0u, k.x, k.y, k.z, k.w};
 #pragma unroll
-  for (uint32_t j = 0; j < 16; j++)
-    if (j < len) st[sh + ex + j] = (uint8_t)(kw[j >> 2] >> (8 * (j & 3)));
+  for (int j = 0; j < 4; j++) {
+    const uint32_t x = (uint32_t)((((uint64_t)kw[j + 1] << 32) | kw[j]) >> (32 - 8 * r));
+    if (x) atomicOr(&d[j], x);
+  }
+  if (r && k.w >> (32 - 8 * r)) atomicOr(&d[4], k.w >> (32 - 8 * r));
+}
+// Zeroes stage bytes [0, n) (n a multiple of 16) with `nt` threads.
+__device__ __forceinline__ void stage_zero(uint8_t* st, uint32_t n, uint32_t t, uint32_t nt) {
+  for (uint32_t q = 16 * t; q < n; q += 16 * nt) *reinterpret_cast<uint4*>(st + q) = make_uint4(0, 0, 0, 0);
 }
 extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpus c) {
   __shared__ uint32_t ws[4][2];
@@ -2822,8 +2999,9 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
       const unsigned long long cnt = cn;
       const uint32_t len = i < n ? key_len16(k) : 0u;
       if (i + 64 * MAT_WAVES < n) { kn = w.uk[src0 + i + 64 * MAT_WAVES]; cn = w.uc[src0 + i + 64 * MAT_WAVES]; }
+      stage_zero(stage, MAT_WAVES * WSTAGE, (uint32_t)tid, 64 * MAT_WAVES);
       uint32_t ex, dummy, tot, t2;
-      exscan2_256(len, 0, ws, ex, dummy, tot, t2);
+      exscan2_256(len, 0, ws, ex, dummy, tot, t2);  // its LDS barriers also order the zeroing
       if (i < n) mat_word(w, stage, dst0 + i, boff, ex, k, len, cnt);
       lds_barrier();
       mat_flush(w, stage, boff, tot, (uint32_t)tid, 64 * MAT_WAVES);
@@ -2831,7 +3009,11 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
       boff += tot;
     }
   }
-  // units of split partitions (high-cardinality input: ~330 words each): one wave each
+  // units of split partitions (high-cardinality input: ~330 words each): one
+  // wave each, up to 512 words per batch with all their loads issued at once
+  // (count-1 units: the (index, count) pairs, then the key gathers from the
+  // unit's split_k range)
+  constexpr int MB = 8;  // words per lane per batch
   for (uint32_t u = blockIdx.x * MAT_WAVES + wv; u < U; u += gridDim.x * MAT_WAVES) {
     const UnitDesc ud = w.udesc[u];
     if (ud.in_n == UNIT_WHOLE) continue;
@@ -2840,29 +3022,46 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
     const uint64_t src0 = ud.rec_off, dst0 = w.uniq_off[ud.part] + w.u_uniq_off[u];
     uint64_t boff = w.bytes_off[ud.part] + w.u_bytes_off[u];
     uint8_t* st = stage + wv * WSTAGE;
-    for (uint64_t i0 = 0; i0 < n; i0 += 64) {
-      const uint64_t i = i0 + lane;
-      uint4 k = make_uint4(0, 0, 0, 0);
-      uint32_t len = 0;
-      unsigned long long cnt = 0;
-      if (i < n) {
-        if (byidx) {
-          const uint32_t v = w.ui[src0 + i];
-          k = w.split_k[ud.in_off + (v >> 16)];
-          cnt = v & 0xFFFFu;
-        } else {
-          k = w.uk[src0 + i];
-          cnt = w.uc[src0 + i];
+    for (uint64_t c0 = 0; c0 < n; c0 += 64 * MB) {
+      uint4 kb[MB];
+      unsigned long long cb[MB];
+      if (byidx) {
+        uint32_t v[MB];
+#pragma unroll
+        for (int s = 0; s < MB; s++) {
+          const uint64_t i = c0 + s * 64 + lane;
+          v[s] = i < n ? w.ui[src0 + i] : 0u;
         }
-        len = key_len16(k);
+#pragma unroll
+        for (int s = 0; s < MB; s++) {
+          const uint64_t i = c0 + s * 64 + lane;
+          kb[s] = i < n ? w.split_k[ud.in_off + (v[s] >> 16)] : make_uint4(0, 0, 0, 0);
+          cb[s] = v[s] & 0xFFFFu;
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < MB; s++) {
+          const uint64_t i = c0 + s * 64 + lane;
+          kb[s] = i < n ? w.uk[src0 + i] : make_uint4(0, 0, 0, 0);
+          cb[s] = i < n ? w.uc[src0 + i] : 0ull;
+        }
       }
-      const uint32_t incl = wave_incl_scan(len);
-      const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      if (i < n) mat_word(w, st, dst0 + i, boff, incl - len, k, len, cnt);
-      wave_lds_fence();
-      mat_flush(w, st, boff, tot, (uint32_t)lane, 64);
-      wave_lds_fence();  // the stage is rewritten by the next step
-      boff += tot;
+#pragma unroll
+      for (int s = 0; s < MB; s++) {
+        const uint64_t i0 = c0 + s * 64;
+        if (i0 >= n) break;  // wave-uniform
+        const uint64_t i = i0 + lane;
+        const uint32_t len = i < n ? key_len16(kb[s]) : 0u;
+        stage_zero(st, WSTAGE, (uint32_t)lane, 64);
+        const uint32_t incl = wave_incl_scan(len);
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        wave_lds_fence();
+        if (i < n) mat_word(w, st, dst0 + i, boff, incl - len, kb[s], len, cb[s]);
+        wave_lds_fence();
+        mat_flush(w, st, boff, tot, (uint32_t)lane, 64);
+        wave_lds_fence();  // the stage is rewritten by the next step
+        boff += tot;
+      }
     }
   }
   __syncthreads();

@@ -3,7 +3,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-state}; mkdir -p $O
-timeout -k 10 420 python -u -m pytest tests -m "gpu and not slow" -v --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1
+timeout -k 10 420 python -u -m pytest tests -m "gpu and not slow" -v --timeout 150 --timeout-method thread > $O/gpu_fast.log 2>&1
 rc=$?; echo "fast rc=$rc $(tail -1 $O/gpu_fast.log)"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err
 rc=$?; echo "C2 rc=$rc"; [ $rc -eq 0 ] || exit $rc; cut -c1-200 $O/bench_c2.json
