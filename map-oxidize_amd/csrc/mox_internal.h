@@ -38,7 +38,7 @@ constexpr int TOKMAX = ROW / 2;             // token starts per row (at most eve
 constexpr int SLOT = ROW;
 constexpr int PAY = ROW - 32;               // 992 payload bytes per row
 #ifndef MOX_LD_GROUPS
-#define MOX_LD_GROUPS 3
+#define MOX_LD_GROUPS 4  // 3: k_map +2.5-4 % on C2 (interleaved A/B)
 #endif
 constexpr int LD_GROUP = 6;                 // loader: rows per register group
 constexpr int LD_GROUPS = MOX_LD_GROUPS;    // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)

@@ -1731,25 +1731,68 @@ __device__ __forceinline__ bool in_sub(uint32_t h, uint32_t shift, uint32_t kk, 
 __device__ __forceinline__ uint32_t red_bin(uint32_t h, uint32_t shift) { return shift >= 32 ? 0u : (h << shift) >> (32 - 11); }
 
 // Every cold record of partition b (all map workgroups' regions), one wave per
-// region, 4 x 64 records in flight per wave.
+// region, 4 x 64 records per chunk, the next chunk's loads in flight while the
+// current one is processed (ping-pong buffers, as in k_reduce).  The wave's
+// regions go in groups of 64: lane k holds the size of the group's k-th region.
+template <class F>
+__device__ __forceinline__ void for_cold_group(const Work& w, uint32_t b, F f, uint32_t g0, uint32_t nreg, int lane,
+                                               int nwv) {
+  const int wv = 0;  // regions g0 + k nwv
+  const uint32_t myn = lane < (int)nreg ? w.cold_n[(uint64_t)(g0 + lane * nwv) * NB + b] : 0u;
+  const uint64_t nonempty = __ballot(myn != 0);
+  auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
+    const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
+    return m ? (uint32_t)__builtin_ctzll(m) : nreg;
+  };
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto load = [&](uint32_t kq, uint32_t iq, uint4 (&v)[4]) {  // unconditional: uniform vmcnt
+    const uint32_t kc = kq < nreg ? kq : 0u;
+    const uint32_t n = __builtin_amdgcn_readlane(myn, kc);
+    const uint4* reg = w.cold + ((uint64_t)(g0 + wv + kc * nwv) * NB + b) * w.cold_cap;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const uint32_t i = iq + u * 64 + lane;
+      const u32x4 x = *reinterpret_cast<const u32x4*>(reg + (i < n ? i : 0u));
+      v[u] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+  auto process = [&](const uint4 (&v)[4], uint32_t kq, uint32_t iq) {
+    const uint32_t n = __builtin_amdgcn_readlane(myn, kq);
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+      if (iq + u * 64 + lane < n) f(v[u]);
+  };
+  auto advance = [&](uint32_t& kq, uint32_t& iq) {
+    iq += 256;
+    if (iq >= __builtin_amdgcn_readlane(myn, kq)) { kq = next_region(kq + 1); iq = 0; }
+  };
+  uint32_t k = next_region(0), i0 = 0;
+  uint4 A[4], B[4];
+  if (k < nreg) load(k, 0, A);
+  while (k < nreg) {
+    uint32_t kb = k, ib = i0;
+    advance(kb, ib);
+    load(kb, ib, B);
+    process(A, k, i0);
+    k = kb;
+    i0 = ib;
+    if (k >= nreg) break;
+    uint32_t ka = k, ia = i0;
+    advance(ka, ia);
+    load(ka, ia, A);
+    process(B, k, i0);
+    k = ka;
+    i0 = ia;
+  }
+}
+
 template <class F>
 __device__ __forceinline__ void for_partition_cold(const Work& w, uint32_t b, F f) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  for (uint32_t g = wv; g < w.map_grid; g += nwv) {
-    const uint32_t n = w.cold_n[(uint64_t)g * NB + b];
-    const uint4* reg = w.cold + ((uint64_t)g * NB + b) * w.cold_cap;
-    for (uint32_t i0 = 0; i0 < n; i0 += 256) {
-      uint4 v[4];
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const uint32_t i = i0 + u * 64 + lane;
-        v[u] = i < n ? reg[i] : make_uint4(0, 0, 0, 0);
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++)
-        if (i0 + u * 64 + lane < n) f(v[u]);
-    }
-  }
+  const uint32_t G = w.map_grid;
+  const uint32_t nall = G > (uint32_t)wv ? (G - wv + nwv - 1) / nwv : 0;
+  for (uint32_t r0 = 0; r0 < nall; r0 += 64)
+    for_cold_group(w, b, f, wv + r0 * nwv, nall - r0 < 64 ? nall - r0 : 64u, lane, nwv);
 }
 
 // ------------------------------------------------------------------ high-cardinality split
