@@ -40,7 +40,10 @@ constexpr int PAY = ROW - 32;               // 992 payload bytes per row
 #ifndef MOX_LD_GROUPS
 #define MOX_LD_GROUPS 4  // 3: k_map +2.5-4 % on C2 (interleaved A/B)
 #endif
-constexpr int LD_GROUP = 6;                 // loader: rows per register group
+#ifndef MOX_LD_GROUP
+#define MOX_LD_GROUP 6
+#endif
+constexpr int LD_GROUP = MOX_LD_GROUP;      // loader: rows per register group
 constexpr int LD_GROUPS = MOX_LD_GROUPS;    // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
