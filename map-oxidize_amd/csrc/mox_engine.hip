@@ -38,6 +38,7 @@ __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
 __global__ void k_dict_hist(Work w);
 __global__ void k_dict_pick(Work w, uint32_t max_words);
 __global__ void k_dict_build(Work w, uint32_t max_words);
+__global__ void k_dict_zero(Work w);
 __global__ void k_unicode(Corpus c, Work w, Tables T);
 __global__ void k_hist(Work w);
 __global__ void k_scatter(Work w);
@@ -100,6 +101,12 @@ struct DevBuf {
 struct mox_engine {
   int device = 0;
   hipStream_t stream = nullptr;
+  // async passes: pass k + 1's dictionary is built on dstream while pass k's
+  // reduce tail runs on stream (ev_dfree: pass k's k_unicode has read the
+  // dictionary buffers; ev_dready: the next dictionary is built)
+  hipStream_t dstream = nullptr;
+  hipEvent_t ev_dfree = nullptr, ev_dready = nullptr;
+  bool dfree_recorded = false;
   uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 192;
   int n_cu = 256;
   bool sync_each = false;
@@ -430,25 +437,40 @@ int finish_pass(mox_engine* e, const Seq& q) {
 
 // One attempt of the whole device pipeline.  Returns MOX_OK after the control
 // block has been read back into e->h_ctl (caller inspects overflow / errors).
-void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q) {
+// Dictionary kernels of one pass on stream s.
+void launch_dict(mox_engine* e, const Corpus& c, hipStream_t s, const Seq& q) {
+  Work& w = e->w;
+  hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(256), 0, s, c, w, e->sample_pieces);
+  q.step("k_sample");
+  hipLaunchKernelGGL(k_dict_hist, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w);
+  q.step("k_dict_hist");
+  hipLaunchKernelGGL(k_dict_pick, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w, e->dict_words);
+  q.step("k_dict_pick");
+  hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
+  q.step("k_dict_build");
+}
+
+// side: build the dictionary on e->dstream, overlapping the previous pass's
+// reduce tail (async passes).  The dictionary buffers (sampling table,
+// histogram, tags, keys, size) are read by a pass up to its k_unicode only.
+void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = false) {
   Work& w = e->w;
   hipStream_t s = e->stream;
   q.rec(0);
   const bool dict = !(e->flags & MOX_F_NO_DICT) && c.own_hi > c.own_lo;
-  // control block, partition counters, long table, sampling buffers: one launch
-  hipLaunchKernelGGL(k_init, dim3(256), dim3(256), 0, s, w, 0ull, dict ? 1u : 0u);
-  q.step("k_init");
+  const bool sided = side && dict && !q.timing && !q.sync_each;
   // 1. hot dictionary from a sample
-  if (dict) {
-    hipLaunchKernelGGL(k_sample, dim3(e->sample_pieces), dim3(256), 0, s, c, w, e->sample_pieces);
-    q.step("k_sample");
-    hipLaunchKernelGGL(k_dict_hist, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w);
-    q.step("k_dict_hist");
-    hipLaunchKernelGGL(k_dict_pick, dim3(GC_SLOTS / 1024), dim3(1024), 0, s, w, e->dict_words);
-    q.step("k_dict_pick");
-    hipLaunchKernelGGL(k_dict_build, dim3(1), dim3(1024), 0, s, w, e->dict_words);
-    q.step("k_dict_build");
+  if (sided) {
+    if (e->dfree_recorded) (void)hipStreamWaitEvent(e->dstream, e->ev_dfree, 0);
+    hipLaunchKernelGGL(k_dict_zero, dim3(64), dim3(256), 0, e->dstream, w);
+    launch_dict(e, c, e->dstream, q);
+    (void)hipEventRecord(e->ev_dready, e->dstream);
   }
+  // control block, partition counters, long table, sampling buffers: one launch
+  hipLaunchKernelGGL(k_init, dim3(256), dim3(256), 0, s, w, 0ull, sided ? 4u : (dict ? 1u : 0u));  // INIT_DICT_SIDE / INIT_DICT
+  q.step("k_init");
+  if (sided) (void)hipStreamWaitEvent(s, e->ev_dready, 0);
+  else if (dict) launch_dict(e, c, s, q);
   q.rec(1);
   // 2. map: one streaming pass over the corpus
   const uint64_t row0 = c.own_lo & ~15ull;
@@ -461,6 +483,10 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q) {
   hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);  // + dictionary totals
   q.step("k_unicode");
   q.rec(3);
+  if (e->dstream) {  // the dictionary buffers are free for the next pass's side build
+    (void)hipEventRecord(e->ev_dfree, s);
+    e->dfree_recorded = true;
+  }
   // 4-5. shuffle directory + bucket reduce, table
   launch_reduce_tail(e, c, q);
 }
@@ -524,6 +550,7 @@ int check_failed(const Ctl& h) {
 }
 
 int run_corpus(mox_engine* e, const Corpus& c) {
+  if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));  // no side-stream dictionary build in flight
   e->have_result = false;
   uint64_t n = c.own_hi - c.own_lo;
   Caps want = initial_caps(n, e->n_cu);
@@ -676,6 +703,7 @@ int complete_async(mox_engine* e, int k) {
   }
   // overflowed: drain, then the synchronous path (retry loop)
   HIPCHK(hipStreamSynchronize(e->stream));
+  if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));
   e->stats.async_reruns++;
   int rc = run_corpus(e, a.c);
   if (later.pending) {
@@ -699,6 +727,7 @@ int drain_async(mox_engine* e) {
   const int first = e->anext;  // slot written least recently
   int rc = complete_async(e, first);
   const int rc2 = complete_async(e, first ^ 1);
+  if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));
   return rc ? rc : rc2;
 }
 
@@ -1189,6 +1218,12 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
     return fail(MOX_EHIP, "hipStreamCreate failed");
   }
   for (auto& ev : e->ev) (void)hipEventCreate(&ev);
+  if (hipStreamCreateWithFlags(&e->dstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_dfree, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_dready, hipEventDisableTiming) != hipSuccess) {
+    mox_engine_destroy(e);
+    return fail(MOX_EHIP, "side stream / events: creation failed");
+  }
   if (hipFuncSetAttribute((const void*)k_map, hipFuncAttributeMaxDynamicSharedMemorySize, (int)map_lds_bytes()) != hipSuccess ||
       hipFuncSetAttribute((const void*)k_reduce, hipFuncAttributeMaxDynamicSharedMemorySize, (int)reduce_lds_bytes()) != hipSuccess) {
     mox_engine_destroy(e);
@@ -1242,6 +1277,8 @@ void mox_engine_destroy(mox_engine* e) {
     for (int k = 0; k < 2; k++) if (e->file_pin[t][k]) (void)hipHostFree(e->file_pin[t][k]);
   }
   if (e->stream) (void)hipStreamDestroy(e->stream);
+  if (e->dstream) (void)hipStreamDestroy(e->dstream);
+  for (hipEvent_t ev : {e->ev_dfree, e->ev_dready}) if (ev) (void)hipEventDestroy(ev);
   delete e;
 }
 
@@ -1278,7 +1315,7 @@ int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t
   Seq q = seq_of(e);
   q.map_ev[0] = a.ev_map0;
   q.map_ev[1] = a.ev_map1;
-  enqueue_pass(e, c, q);
+  enqueue_pass(e, c, q, /*side=*/true);
   HIPCHK(hipGetLastError());
   static_assert(sizeof(Ctl) / 8 <= 256, "k_ctl_out: one workgroup");
   hipLaunchKernelGGL(k_ctl_out, dim3(1), dim3(256), 0, e->stream, (const Ctl*)e->w.ctl, a.h_ctl);

@@ -54,6 +54,7 @@ constexpr int GC_SLOTS = 65536;             // global dictionary candidate table
 constexpr int MAX_SAMPLE_PIECES = 1024;
 constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B
 constexpr int SAMPLE_SLOTS = 2048;
+constexpr int DH_N = 258, DH_T = 259;       // dict_hist words after the histogram and pick counters
 constexpr int RED_THREADS = 1024;
 // High-cardinality split: a partition whose sampled records are
 // mostly distinct is scattered into 2^kk sub-buckets (the next kk hash bits), and
@@ -242,7 +243,8 @@ struct Work {  // device buffers of one engine
   Ctl* ctl;
   // dictionary
   WRec* cand;                     // GC_SLOTS candidates (key claimed with claim16, count)
-  uint32_t* dict_hist;            // [256] candidate count histogram, [256] picked words (classes >= T), [257] class T - 1 words
+  uint32_t* dict_hist;            // [256] candidate count histogram, [256] picked words (classes >= T), [257] class T - 1 words,
+                                  // [DH_N] dictionary words, [DH_T] threshold (the pass's, read by k_map / k_unicode)
   WRec* dict_list;                // DICT_MAX_WORDS picked words
   uint32_t* dict_tag;             // DICT_SLOTS key hashes (0 = empty), bucket b = slots 4b..4b+3
   uint4* dict_key;                // DICT_SLOTS lowered 16-byte keys

@@ -863,7 +863,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint8_t* ring = sp; sp += RING * SLOT;
   uint16_t* lists = (uint16_t*)sp;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  m.dict_n = w.ctl->dict_n;
+  m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
   // the token passes probe unconditionally: without a dictionary the arrays are
   // zero (no real key is zero, so nothing hits)
@@ -1037,7 +1037,10 @@ extern "C" __global__ void k_ctl_out(const Ctl* __restrict__ src, Ctl* __restric
 // block (zero, no UTF-8 / halo error, w_n), the partition counters, the long
 // table, and (INIT_DICT) the dictionary sampling buffers or (INIT_MAP) the map
 // region counters of an exchange pass.
-enum : uint32_t { INIT_DICT = 1u, INIT_MAP = 2u };
+// INIT_DICT: the dictionary is built on the pass's stream (sampling buffers
+// zeroed here); INIT_DICT_SIDE: it is built on the side stream (k_dict_zero
+// there), only the map's totals are zeroed; neither: no dictionary.
+enum : uint32_t { INIT_DICT = 1u, INIT_MAP = 2u, INIT_DICT_SIDE = 4u };
 __device__ __forceinline__ void zero_words(void* p, uint64_t bytes, uint64_t t, uint64_t stride) {
   uint4* q = reinterpret_cast<uint4*>(p);
   const uint64_t n16 = bytes / 16;
@@ -1061,10 +1064,11 @@ extern "C" __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags
   zero_words(w.b_w, NB * 4, t, stride);
   zero_words(w.ltab, w.long_cap * sizeof(LSlot), t, stride);
   if (flags & INIT_DICT) {
-    zero_words(w.dict_tot, DICT_SLOTS * 8, t, stride);
     zero_words(w.cand, (uint64_t)GC_SLOTS * sizeof(WRec), t, stride);
     zero_words(w.dict_hist, 260 * 4, t, stride);
   }
+  if (flags & (INIT_DICT | INIT_DICT_SIDE)) zero_words(w.dict_tot, DICT_SLOTS * 8, t, stride);
+  else if (t == 0) { w.dict_hist[DH_N] = 0; w.dict_hist[DH_T] = 0; }  // no dictionary this pass
   if (flags & INIT_MAP) {
     zero_words(w.cold_n, (uint64_t)w.map_grid * NB * 4, t, stride);
     zero_words(w.spill_n, (uint64_t)w.map_grid * 4, t, stride);
@@ -1072,6 +1076,13 @@ extern "C" __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags
 }
 
 // ------------------------------------------------------------------ dictionary
+// Sampling buffers of a dictionary built on the side stream (async passes):
+// zeroed there, after the previous pass's k_unicode read the dictionary.
+extern "C" __global__ void k_dict_zero(Work w) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  zero_words(w.cand, (uint64_t)GC_SLOTS * sizeof(WRec), t, stride);
+  zero_words(w.dict_hist, 260 * 4, t, stride);
+}
 // Two-CAS claim of a 16-byte key in a global or LDS table (w1 is stored with the
 // top bit set so that 0 always means "unclaimed"); used only for heuristics.
 __device__ __forceinline__ bool claim16(unsigned long long* k0, unsigned long long* k1, uint64_t w0, uint64_t w1) {
@@ -1239,7 +1250,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
     __syncthreads();
     if (threadIdx.x == 0) {
       if (cov[1] < cov[0] / DICT_MIN_COVER_INV) T = 256;
-      if (blockIdx.x == 0) w.ctl->dict_thresh = T;
+      if (blockIdx.x == 0) w.dict_hist[DH_T] = T;
     }
     __syncthreads();
   }
@@ -1340,12 +1351,12 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
     __syncthreads();
   }
   for (int i = tid; i < DICT_SLOTS; i += 1024) w.dict_tag[i] = ltag[i];
-  if (tid == 0) w.ctl->dict_n = nsel;
+  if (tid == 0) w.dict_hist[DH_N] = nsel;  // outside the control block: a side-stream build may precede k_init
 }
 
 // Emit dictionary slot s's total (summed by k_map's atomics) as a weighted record.
 __device__ __forceinline__ void dict_total(const Work& w, uint32_t s) {
-  if (w.ctl->dict_n == 0 || w.dict_tag[s] == 0) return;
+  if (w.dict_hist[DH_N] == 0 || w.dict_tag[s] == 0) return;
   const uint64_t tot = w.dict_tot[s];
   if (tot == 0) return;
   const uint4 k = w.dict_key[s];
@@ -1414,6 +1425,10 @@ extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
   {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < DICT_SLOTS) dict_total(w, s);
+    if (s == 0) {  // the pass's dictionary size / threshold into the control block (stats)
+      w.ctl->dict_n = w.dict_hist[DH_N];
+      w.ctl->dict_thresh = w.dict_hist[DH_T];
+    }
   }
   if (w.ctl->err_utf8 != ~0ull) return;  // invalid input: no result is produced anyway
   uint64_t n = w.ctl->u_n;
