@@ -139,6 +139,21 @@ def test_corpora_exact(eng, kind):
     assert got == want
 
 
+def test_dictionary_gate(eng):
+    """k_dict_pick builds no dictionary when the sampled words would cover < 5 %
+    of the tokens (high-cardinality input); k_map then writes every token as a
+    paired cold record.  Zipf text keeps its dictionary.  Both exact."""
+    for kind, want_dict in (("hicard", False), ("zipf", True)):
+        k = corpus.KINDS[kind]
+        data = corpus.fill(k, 0x6A7E + k, 0, 12 << 20)
+        t = eng.count(data.tobytes())
+        got = t.sorted_items()
+        t.close()
+        st = eng.stats()
+        assert (st["dict_words"] > 1000) == want_dict, (kind, st["dict_words"])
+        assert got == coracle.count(data, nthreads=16)[0], kind
+
+
 def test_misaligned_and_ranges(eng):
     """run_range on a misaligned device pointer and a sub-range equals the oracle's range rule."""
     data = corpus.fill(corpus.UNICODE, 5, 0, 3 << 20).tobytes()
