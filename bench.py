@@ -68,7 +68,7 @@ def parse():
     ap.add_argument("--xport", default="rccl", choices=["rccl", "host"],
                     help="exchange transport for N > 1 (host: gloo-staged, for ranks sharing one GPU)")
     ap.add_argument("--device", type=int, default=-1, help="override the GPU (default LOCAL_RANK)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_k_map.json"),
+    ap.add_argument("--traffic-json", default=None,  # profiles/pmc_k_map.json (C2) or pmc_k_map_<workload>.json
                     help="PMC summary of the map kernel (tools/pmc_traffic.py) to report as roofline.traffic")
     return ap.parse_args()
 
@@ -258,6 +258,8 @@ def main():
         map_avg = statistics.mean(map_ms)
         achieved = per_rank / (map_avg * 1e-3) / 1e9
         traffic = None
+        if a.traffic_json is None:
+            a.traffic_json = os.path.join(ROOT, "profiles", "pmc_k_map%s.json" % ("" if a.workload == "C2" else "_" + a.workload))
         if a.traffic_json and os.path.exists(a.traffic_json):
             try:
                 tj = json.load(open(a.traffic_json))

@@ -3,7 +3,8 @@
 FETCH_SIZE / WRITE_SIZE are in KiB.  gfx950 correction (MI355X_MICROARCH.md,
 HBM section): FETCH_SIZE reports exactly half of the bytes of a wide coalesced
 streaming read (16 B/lane), so it is doubled; WRITE_SIZE is taken as is.
-Usage: python tools/pmc_traffic.py PROF_DIR KERNEL OUT_JSON
+Usage: python tools/pmc_traffic.py PROF_DIR KERNEL OUT_JSON [WORKLOAD BYTES_PER_GPU]
+(bench.py reports the figure only for the workload and size it was measured on)
 """
 import csv
 import glob
@@ -39,6 +40,9 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 wide-stream under-count), WRITE_SIZE x1; KiB -> bytes x1024",
         "source": prof_dir,
     }
+    if len(sys.argv) > 5:
+        res["workload"] = sys.argv[4]
+        res["bytes_per_gpu"] = int(sys.argv[5])
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
 
