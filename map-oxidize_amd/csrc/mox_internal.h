@@ -66,8 +66,11 @@ constexpr int SUB_PER_T = SUB_N / 1024;     // sub-buckets per thread in the 102
 constexpr uint32_t SPLIT_MIN = 6144;        // records below which a partition is never split
 constexpr uint32_t SPLIT_TARGET = 320;      // records per sub-bucket aimed at
 constexpr uint32_t SMALL_CAP = 512;         // sub-buckets up to this many records: k_reduce_small
-constexpr uint32_t SPLIT_SAMPLE = 1024;     // records sampled for the distinct-fraction estimate
-constexpr uint32_t SPLIT_PER_REGION = 4;    // ... the first 4 of every map workgroup's region
+#ifndef MOX_SPLIT_PER_REGION
+#define MOX_SPLIT_PER_REGION 4
+#endif
+constexpr uint32_t SPLIT_PER_REGION = MOX_SPLIT_PER_REGION;  // sample: the first records of every map workgroup's region
+constexpr uint32_t SPLIT_SAMPLE = 256 * SPLIT_PER_REGION;      // records sampled for the distinct-fraction estimate
 constexpr int LC_BITS = 4096;               // linear-counting bitmap of the sample (4 bits per sample)
 
 constexpr uint64_t LONG_TAG = 0xFF00000000000000ull;   // w1 marker of a hashed (long) key
