@@ -398,6 +398,55 @@ def test_sort_bytes_flag():
         e.close()
 
 
+def test_async_side_stream_dictionaries():
+    """Async passes build their dictionaries on a side stream during the previous
+    pass's reduce tail.  Back-to-back passes over corpora with different hot
+    words (Zipf, Unicode, heavy skew, high cardinality: no dictionary), with the
+    flags switched between calls (no dictionary, full timing = dictionary on the
+    main stream): every completed pass's tokens and distinct words match the
+    oracle, and the last table is exact."""
+    specs = [(corpus.ZIPF, 31, 6 << 20), (corpus.UNICODE, 32, 3 << 20), (corpus.SKEW, 33, 5 << 20),
+             (corpus.HICARD, 34, 4 << 20), (corpus.ZIPF, 35, 2 << 20)]
+    datas = [corpus.fill(k, sd, 0, n).tobytes() for k, sd, n in specs]
+    want = [coracle.count(x) for x in datas]  # (sorted items, tokens)
+    e = mox.Engine(device=0, flags=mox.MOX_F_TIMING_MAP, reserve_bytes=8 << 20)
+    try:
+        bufs = []
+        for x in datas:
+            d = e.alloc(len(x))
+            e.h2d(d, x)
+            bufs.append(d)
+        flags = [mox.MOX_F_TIMING_MAP, mox.MOX_F_TIMING_MAP, mox.MOX_F_NO_DICT, mox.MOX_F_TIMING, mox.MOX_F_TIMING_MAP]
+        order = [0, 1, 2, 3, 4, 0, 2, 1, 4, 3, 0, 1, 2, 0, 4, 2]
+        def check(st, j, i):
+            items, tok = want[j]
+            assert st["tokens"] == tok and st["uniques"] == len(items), (i, j, st)
+
+        prev, reruns = None, 0
+        for i, j in enumerate(order):
+            e.set_flags(flags[i % len(flags)])
+            e.run_range_async(bufs[j], len(datas[j]), 0, len(datas[j]), True)
+            st = e.stats()
+            if st["async_reruns"] != reruns:
+                # the previous pass overflowed: it and this one were re-run
+                # synchronously, so the stats are this pass's and none is pending
+                reruns = st["async_reruns"]
+                check(st, j, i)
+                prev = None
+                continue
+            if prev is not None:  # this call completed the previous pass
+                check(st, prev, i)
+            prev = j
+        e.run_wait()
+        t = e.fetch()
+        assert t.sorted_items() == want[order[-1]][0]
+        t.close()
+        for d in bufs:
+            e.free(d)
+    finally:
+        e.close()
+
+
 def test_async_overflow_reruns_once():
     """An overflowing async pass is re-run once, and so is the pass queued
     behind it; later passes are not re-run (no stale-rerun cascade)."""
