@@ -2650,14 +2650,28 @@ __device__ __forceinline__ uint64_t xor_lane(uint64_t v) {
 }
 // Bitonic sort of 64 x PER values in registers, position p = lane * PER + s.
 // Compare-exchange with the lane (lane ^ M): the lower lane keeps the minimum
-// when this block sorts ascending.
+// when this block sorts ascending.  k_reduce_sort2's 32-bit keys (16 per
+// lane) use min / max with the DPP fused in and one per-stage lane mask: no
+// compare + mask XOR per element, whose SALU write of VCC and DPP source move
+// cost wait states between VALU instructions (k_reduce_sort2 772 -> 670 us at
+// C4).  k_reduce_sort1 keeps compare + select: the same change made it 2-4 %
+// slower (it is not issue-bound).
 template <int M, int PER, class T>
 __device__ __forceinline__ void s1_cross(T (&v)[PER], int lane, uint32_t k) {
   const bool keep_min = ((lane & M) == 0) == (((uint32_t)(lane * PER) & k) == 0);
+  if constexpr (sizeof(T) == 4 && PER == 16) {
 #pragma unroll
-  for (int s = 0; s < PER; s++) {
-    const T pv = xor_lane<M>(v[s]);
-    v[s] = ((pv < v[s]) == keep_min) ? pv : v[s];
+    for (int s = 0; s < PER; s++) {
+      const uint32_t pv = xor_lane<M>((uint32_t)v[s]);
+      const uint32_t lo = min((uint32_t)v[s], pv), hi = max((uint32_t)v[s], pv);
+      v[s] = keep_min ? lo : hi;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < PER; s++) {
+      const T pv = xor_lane<M>(v[s]);
+      v[s] = ((pv < v[s]) == keep_min) ? pv : v[s];
+    }
   }
 }
 template <int PER, class T>
@@ -2668,14 +2682,25 @@ __device__ __forceinline__ void s1_inlane(T (&v)[PER], int lane, uint32_t k, int
     if (t > s) {
       const bool asc = ((uint32_t)(lane * PER + s) & k) == 0;
       const T a = v[s], b = v[t];
-      const bool sw = (a > b) == asc;
-      v[s] = sw ? b : a;
-      v[t] = sw ? a : b;
+      if constexpr (sizeof(T) == 4 && PER == 16) {
+        const T lo = a < b ? a : b, hi = a < b ? b : a;
+        v[s] = asc ? lo : hi;
+        v[t] = asc ? hi : lo;
+      } else {
+        const bool sw = (a > b) == asc;
+        v[s] = sw ? b : a;
+        v[t] = sw ? a : b;
+      }
     }
   }
 }
 template <int PER, class T>
-__device__ __forceinline__ void s1_sort(T (&v)[PER], int lane) {
+__device__ __forceinline__ void s1_sort(T (&v)[PER], int lane_in) {
+  // the per-stage lane masks are recomputed in every sort (one compare each)
+  // instead of being hoisted out of the unit loop, where ~45 live SGPR pairs
+  // spill into VGPR lanes
+  int lane = lane_in;
+  if constexpr (PER == 16) asm volatile("" : "+v"(lane));
 #pragma unroll
   for (uint32_t k = 2; k <= 64u * PER; k <<= 1) {
 #pragma unroll
