@@ -24,7 +24,10 @@ constexpr int MAP_MIN_WAVES = 1;
 #define MOX_MAP_LOADERS 1
 #endif
 constexpr int MAP_LOADERS = MOX_MAP_LOADERS;  // loader waves (alternate row groups)
-constexpr int RING = 32;                    // power of two
+#ifndef MOX_RING
+#define MOX_RING 32
+#endif
+constexpr int RING = MOX_RING;              // k_map row ring slots (LDS)
 constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
 constexpr int DICT_MAX_WORDS = 3584;
 #endif
