@@ -24,6 +24,12 @@ constexpr int MAP_MIN_WAVES = 1;
 #define MOX_MAP_LOADERS 1
 #endif
 constexpr int MAP_LOADERS = MOX_MAP_LOADERS;  // loader waves (alternate row groups)
+#ifndef MOX_LD_SLEEP
+#define MOX_LD_SLEEP 1  // k_map loader's poll for a free ring slot (s_sleep units of 64 clocks)
+#endif
+#ifndef MOX_CO_SLEEP
+#define MOX_CO_SLEEP 1  // k_map consumer's poll for a loaded row
+#endif
 #ifndef MOX_RING
 #define MOX_RING 32
 #endif

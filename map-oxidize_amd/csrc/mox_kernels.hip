@@ -914,7 +914,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
         if (t >= n) continue;
         if (t >= RING)
           while (__hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t - RING + 1)
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(MOX_LD_SLEEP);
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         reinterpret_cast<uint4*>(ring + (t % RING) * SLOT)[lane] = b[i];
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -950,7 +950,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       if (u >= n) break;
       const uint32_t slot = u % RING;
       while (__hip_atomic_load(&sready[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != u + 1)
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(MOX_CO_SLEEP);
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       uint8_t* sl = ring + slot * SLOT;
       const uint64_t sbase = base0 + (rb + u) * PAY - 16;
