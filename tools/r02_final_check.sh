@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-end rehearsal of what the driver runs: GPU suite (fast), smoke(), default bench.py.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-final}; mkdir -p $O
+timeout -k 10 420 python -u -m pytest tests -m "gpu and not slow" -v --timeout 150 --timeout-method thread > $O/gpu_fast.log 2>&1
+rc=$?; echo "fast rc=$rc $(tail -1 $O/gpu_fast.log)"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 180 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1
+rc=$?; echo "smoke rc=$rc $(tail -1 $O/smoke.log)"; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u bench.py > $O/bench.json 2> $O/bench.err
+rc=$?; echo "bench rc=$rc"; [ $rc -eq 0 ] || exit $rc; cut -c1-300 $O/bench.json
