@@ -30,6 +30,9 @@ constexpr int MAP_LOADERS = MOX_MAP_LOADERS;  // loader waves (alternate row gro
 #ifndef MOX_CO_SLEEP
 #define MOX_CO_SLEEP 1  // k_map consumer's poll for a loaded row
 #endif
+#ifndef MOX_DICT_PAIRS
+#define MOX_DICT_PAIRS 0  // k_map pairs cold records with a dictionary too (own LDS slots: needs RING <= 24)
+#endif
 #ifndef MOX_RING
 #define MOX_RING 32
 #endif

@@ -376,7 +376,7 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-  if (m.dict_n == 0) { cold_pair(m, b, key); return; }
+  if (MOX_DICT_PAIRS || m.dict_n == 0) { cold_pair(m, b, key); return; }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < m.w.cold_cap) {
     m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
@@ -855,13 +855,18 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
   m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
   m.s.masktab = (uint4*)sp; sp += 17 * 16;
-  m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
-  m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB);       // = PS_EMPTY
-  static_assert(NB * 16 + NB * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
-  uint16_t* lists = (uint16_t*)sp;
+  uint16_t* lists = (uint16_t*)sp; sp += MAP_CONSUMERS * 2 * TOKMAX;
+#if MOX_DICT_PAIRS
+  m.s.pend = (uint4*)sp; sp += NB * 16;              // pair slots of their own (dictionary path too)
+  m.s.pst = (uint32_t*)sp;
+#else
+  m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
+  m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB);       // = PS_EMPTY
+  static_assert(NB * 16 + NB * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
@@ -873,7 +878,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);
     m.s.dcnt[i] = 0;
   }
-  for (int i = tid; i < NB; i += MAP_THREADS) m.s.bcnt[i] = 0;
+  for (int i = tid; i < NB; i += MAP_THREADS) {
+    m.s.bcnt[i] = 0;
+    if (MOX_DICT_PAIRS) m.s.pst[i] = PS_EMPTY;
+  }
   if (tid < 4) m.s.misc[tid] = 0;
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
   if (tid < 17) {
@@ -970,7 +978,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #endif
   }
   __syncthreads();
-  if (m.dict_n == 0) {  // records still parked in pair slots: written as singles
+  if (MOX_DICT_PAIRS || m.dict_n == 0) {  // records still parked in pair slots: written as singles
     for (int i = tid; i < NB; i += MAP_THREADS) {
       if (m.s.pst[i] != PS_FULL) continue;
       const uint32_t pos = atomicAdd(&m.s.bcnt[i], 1u);
