@@ -10,6 +10,14 @@ copied to HBM before timing.
   python bench.py [--gpus N --steps K --warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no torchrun environment, ONE process drives all N GPUs
+through an engine group (mox_config.n_gpus, include/mox.h): a step is one
+mox_run_shards call (local passes on all GPUs at once, the all-to-all as one
+RCCL group over the members' communicators, per-owner reduce, gather and the
+bytewise sort of the result on GPU 0).  Under torchrun (RANK / WORLD_SIZE
+set) every rank is one process per GPU (mox_comm_init, mox_exchange,
+mox_gather); rank 0 prints the line.
+
 Default workload (N = 1): config C2 of BASELINE.json, 1 GiB Zipf(1.1)
 English-like corpus.  N > 1: config C3, weak scaling with an 8 GiB byte-range
 shard per GPU of the C3 corpus stream (rank r owns bytes [8r GiB, 8(r+1) GiB);
@@ -126,8 +134,132 @@ def local_tokens(eng, d_buf, n, own_b, own_e, at_end):
     return eng.stats()["tokens"]
 
 
+def roofline_fields(per_rank, map_avg, workload, traffic_json):
+    achieved = per_rank / (map_avg * 1e-3) / 1e9
+    traffic = None
+    if traffic_json is None:
+        traffic_json = os.path.join(ROOT, "profiles", "pmc_k_map%s.json" % ("" if workload == "C2" else "_" + workload))
+    if traffic_json and os.path.exists(traffic_json):
+        try:
+            tj = json.load(open(traffic_json))
+            # PMC traffic is per launch of one workload and size: report it only for that one
+            if tj.get("workload", "C2") == workload and tj.get("bytes_per_gpu", 1 << 30) == per_rank:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    return {
+        "kernel": "k_map",
+        # what binds k_map is issue and LDS latency, not HBM bandwidth: the roofline
+        # is priced against HBM (no dense contraction) but the binding unit is named
+        "bound": "hbm",
+        "binding_resource": "VALU issue + LDS latency (1 loader + 15 consumer waves per CU), not HBM bandwidth",
+        "limiter": "k_map moves ~2.3 TB/s of HBM traffic of 8; SQ counters: ~580 VALU instructions per 992-byte row at "
+                   "~46 % VALU issue (DESIGN.md §4, §8)",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": traffic,
+        "algorithmic_bytes_per_launch": per_rank,
+        "avg_launch_ms": round(map_avg, 4),
+    }
+
+
+def main_group(a):
+    """--gpus N > 1 without torchrun: one process, one engine group over N GPUs."""
+    n = a.gpus
+    if not a.workload:
+        a.workload = "C3"
+    kind, seed, per_rank, desc = WORKLOADS[a.workload]
+    if a.bytes_per_gpu:
+        per_rank = a.bytes_per_gpu
+    total = per_rank * n
+    devices = [a.device] * n if a.device >= 0 else None
+    xport = mox.XPORT_COPY if a.xport == "host" else mox.XPORT_RCCL
+    base_flags = (mox.MOX_F_NO_DICT if a.no_dict else 0) | mox.MOX_F_SORT_BYTES
+    g = mox.Engine(n_gpus=n, transport=xport, devices=devices, flags=base_flags | mox.MOX_F_TIMING_MAP,
+                   sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
+    shards, bufs = [], []
+    for r in range(n):
+        lo, hi, ob, oe, end = mdist.shard_range(total, n, r, per_rank=per_rank, halo=HALO)
+        host = corpus.fill(kind, seed, lo, hi - lo)
+        m = g.member(r)
+        d = m.alloc(hi - lo)
+        m.h2d(d, host)
+        del host
+        bufs.append((m, d))
+        shards.append((d, hi - lo, ob, oe, end))
+    for _ in range(a.warmup):
+        g.run_shards(shards)
+    rows = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        g.run_shards(shards)  # synchronous: returns with the sorted table on GPU 0
+        rows.append(g.stats())
+    elapsed = time.perf_counter() - t0
+    last = rows[-1]
+    t = g.fetch()
+    counts, offs, _ = t.arrays()
+    table_n, table_bytes, table_tokens = t.n, int(offs[-1]) if t.n else 0, t.tokens
+    ok = int(counts.sum()) == t.tokens == last["tokens"]
+    t.close()
+    ms_step = elapsed / a.steps * 1e3
+    gbs = total / (elapsed / a.steps) / 1e9
+    map_avg = statistics.mean(r["ms_map"] for r in rows)
+    b_alg = total + table_bytes + 8 * table_n
+    mean = lambda k: round(statistics.mean(r[k] for r in rows), 4)  # noqa: E731
+    line = {
+        "metric": METRIC,
+        "value": round(gbs, 3),
+        "unit": "GB/s",
+        "n_gpus": n,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: mox_corpus kind=%d seed=%#x (%s, host-generated, copied to HBM before timing)"
+                % (kind, seed, KIND_DESC.get(kind, "?")),
+        "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
+                   "parallelism": "dp%d byte-range shards + %s all-to-all + gather and bytewise sort at GPU 0 "
+                                  "(one process, engine group)" % (n, "RCCL" if xport == mox.XPORT_RCCL else "device-copy")},
+        "words_per_s": round(last["tokens"] / (elapsed / a.steps), 1),
+        "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * n), 2),
+        "algorithmic_bytes_per_step": b_alg,
+        "roofline_end_to_end": {"achieved": round(b_alg / (elapsed / a.steps) / 1e9, 1), "peak": HBM_PEAK_GBS * n,
+                                "unit": "GB/s", "frac": round(b_alg / (elapsed / a.steps) / 1e9 / (HBM_PEAK_GBS * n), 4)},
+        "roofline": roofline_fields(per_rank, map_avg, a.workload, a.traffic_json),
+        "pass_mode": "sync (mox_run_shards per step)",
+        "phases_ms": {"local_passes": mean("ms_local"), "map_mean_over_gpus": mean("ms_map"), "exchange": mean("ms_exchange"),
+                      "gather": mean("ms_gather"), "sort_bytes": mean("ms_sort"), "step_wall": mean("ms_run")},
+        "stats": {k: last[k] for k in ("tokens", "uniques", "cold_records", "weighted_records")},
+        "multi_gpu": {
+            "mode": "engine group (one process)",
+            "transport": "RCCL (ncclCommInitAll, one ncclGroupStart/End per all-to-all)" if xport == mox.XPORT_RCCL
+                         else "device-to-device copies (hipMemcpyPeerAsync)",
+            "devices": devices if devices else list(range(n)),
+            "all_to_all_bytes": int(last["x_bytes_sent"]),
+            "all_to_all_bytes_recv": int(last["x_bytes_recv"]),
+            "exchange_ms": mean("ms_exchange"),
+            "gather_ms": mean("ms_gather"),
+            "gather_bytes": int(last["gather_bytes"]),
+            "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens, "order": "bytewise (sorted on GPU 0)"},
+        },
+        "check_sum_counts_eq_tokens": ok,
+        "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
+    for m, d in bufs:
+        m.free(d)
+    g.close()
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return main_group(a)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -256,18 +388,6 @@ def main():
         ms_step = elapsed / a.steps * 1e3
         gbs = total / (elapsed / a.steps) / 1e9
         map_avg = statistics.mean(map_ms)
-        achieved = per_rank / (map_avg * 1e-3) / 1e9
-        traffic = None
-        if a.traffic_json is None:
-            a.traffic_json = os.path.join(ROOT, "profiles", "pmc_k_map%s.json" % ("" if a.workload == "C2" else "_" + a.workload))
-        if a.traffic_json and os.path.exists(a.traffic_json):
-            try:
-                tj = json.load(open(a.traffic_json))
-                # PMC traffic is per launch of one workload and size: report it only for that one
-                if tj.get("workload", "C2") == a.workload and tj.get("bytes_per_gpu", 1 << 30) == per_rank:
-                    traffic = tj.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
         # algorithmic bytes per step = input read once + the output
         # table written once (word bytes + a u64 count per distinct word)
         b_alg = total + (table_bytes + 8 * table_n if (world == 1 or gather) else 0)
@@ -295,18 +415,7 @@ def main():
             "roofline_end_to_end": {"achieved": round(b_alg / (elapsed / a.steps) / 1e9, 1),
                                     "peak": HBM_PEAK_GBS * world, "unit": "GB/s",
                                     "frac": round(b_alg / (elapsed / a.steps) / 1e9 / (HBM_PEAK_GBS * world), 4)},
-            "roofline": {
-                "kernel": "k_map",
-                "bound": "hbm",
-                "limiter": "VALU issue + LDS latency at 3.75 consumer waves/SIMD (1 loader + 15 consumer waves per CU), not HBM (SQ/PMC counters, DESIGN.md §4, §8)",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "algorithmic_bytes_per_launch": per_rank,
-                "avg_launch_ms": round(map_avg, 4),
-            },
+            "roofline": roofline_fields(per_rank, map_avg, a.workload, a.traffic_json),
             "phases_note": "phases_ms: one untimed diagnostic step with per-phase HIP events",
             "pass_mode": "async (mox_run_range_async: back-to-back passes, each completed and checked)" if use_async else "sync",
             "phases_ms": {k: round(statistics.mean(p[k] for p in phases), 4)

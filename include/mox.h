@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MOX_ABI_VERSION 2
+#define MOX_ABI_VERSION 3
 
 /* status codes */
 #define MOX_OK 0
@@ -53,22 +53,47 @@ extern "C" {
 
 /* mox_config.flags */
 #define MOX_F_NO_DICT 0x1u      /* disable the hot-word dictionary (all tokens take the cold path) */
-#define MOX_F_SORT_BYTES 0x2u   /* mox_fetch_table returns the words sorted bytewise ascending (Rust String Ord,
-                                   = mox_table_sort_bytes on the fetched table) instead of engine order */
+#define MOX_F_SORT_BYTES 0x2u   /* the result table is sorted bytewise ascending (Rust String Ord) on the GPU
+                                   (at mox_fetch_table; an engine group: right after its gather, inside the
+                                   mox_count / mox_run_shards call) instead of engine order */
 #define MOX_F_TIMING 0x4u       /* record per-kernel HIP-event timings into mox_stats */
 #define MOX_F_TIMING_MAP 0x8u   /* HIP events around the map kernel only (ms_map): each event record idles
                                    the stream ~5.6 us, so timed loops bracket just the dominant kernel */
+
+#define MOX_MAX_GPUS 16
+/* mox_config.transport of an engine group */
+#define MOX_XPORT_RCCL 0u  /* RCCL communicators (ncclCommInitAll) over xGMI, one ncclGroupStart/End per all-to-all */
+#define MOX_XPORT_COPY 1u  /* device-to-device copies (hipMemcpyPeerAsync); members may share a GPU (tests) */
 
 typedef struct mox_config {
   int device;             /* HIP device ordinal; -1 = current device */
   uint32_t flags;         /* MOX_F_* */
   uint32_t dict_words;    /* hot dictionary capacity; 0 = default (3584, also the maximum) */
   uint32_t sample_pieces; /* 4 KiB pieces sampled to build the dictionary; 0 = default (192), max 1024 */
-  uint64_t reserve_bytes; /* pre-size device buffers for corpora of this size; 0 = grow on demand */
-  uint32_t reserved[8];
+  uint64_t reserve_bytes; /* pre-size device buffers for corpora of this size (per GPU); 0 = grow on demand */
+  /* engine group: n_gpus > 1 makes ONE engine that
+     drives n_gpus GPUs from the calling thread.  mox_count / mox_count_file
+     split the input into byte ranges at whitespace, run the local passes on
+     all GPUs at once, exchange the partial tables (hash-partitioned
+     all-to-all), reduce per owner and gather the final table on member 0;
+     mox_run_shards does the same over device-resident shards. */
+  uint32_t n_gpus;        /* 0 or 1: a single-GPU engine on `device` */
+  uint32_t transport;     /* MOX_XPORT_* (engine group) */
+  uint32_t n_devices;     /* 0: member i runs on device i; else n_gpus: member i runs on devices[i] */
+  int32_t devices[MOX_MAX_GPUS];
+  uint32_t reserved[5];
 } mox_config;
 
 typedef struct mox_engine mox_engine;
+
+/* One shard of a device-resident corpus for mox_run_shards: the buffer lives
+ * on the member's GPU; tokens whose first byte lies in [own_begin, own_end)
+ * belong to it (see mox_run_range for the context / look-ahead rules). */
+typedef struct mox_shard {
+  const void* d_buf;
+  size_t buf_len, own_begin, own_end;
+  int at_corpus_end;
+} mox_shard;
 
 /* Result table: one entry per distinct lowercased word.  Engine order: words
  * of at most 16 bytes without a NUL byte first, ascending by (32-bit key hash,
@@ -77,9 +102,10 @@ typedef struct mox_engine mox_engine;
  * slot order (which can vary from run to run when two long words race for a
  * slot).  With
  * MOX_F_SORT_BYTES (or after mox_table_sort_bytes): bytewise ascending, Rust
- * String Ord.  The reference's own order is HashMap-random
+ * String Ord, sorted on the GPU).  The reference's own order is HashMap-random
  * (/root/reference/src/main.rs:177-179).  After mox_gather the root's table
- * is the ranks' tables one after another (rank order), each in engine order.
+ * is the ranks' tables one after another (rank order), each in engine order;
+ * an engine group's gathered table likewise, unless MOX_F_SORT_BYTES.
  * Memory is owned by the library until mox_table_free. */
 typedef struct mox_table {
   uint64_t n;              /* distinct words */
@@ -119,6 +145,17 @@ typedef struct mox_stats {
   uint64_t x_bytes_recv;   /* exchange payload bytes this rank received */
   uint64_t gather_bytes;   /* table bytes this rank sent to the gather root (root: received) */
   double ms_gather;        /* wall time of the last mox_gather on this rank */
+  /* exactness-fallback hit counters of the last pass (a local pass plus its
+     exchange's reduce pass), counted only by the forced-collision check build
+     (libmox_hc.so, -DMOX_HASH_COLLIDE); zero in production builds:
+     [0] dictionary tag equal, key different   [1] long-word table: equal hash, different bytes
+     [2] one-wave sort reduce re-sorted on 64-bit keys   [3] ... handed its unit to k_reduce
+     [4] k_reduce table: equal tag, different key   [5] k_reduce_small: equal hash, different key */
+  uint64_t path_hits[8];
+  double ms_sort;          /* device bytewise table sort (MOX_F_SORT_BYTES), wall time */
+  double ms_local;         /* engine group: local passes of all members (wall time) */
+  uint32_t n_gpus;         /* engine group size (1 for a single-GPU engine) */
+  uint32_t async_dropped;  /* overflowed async passes superseded by a later queued pass (never re-run) */
 } mox_stats;
 
 const char* mox_last_error(void);
@@ -163,6 +200,16 @@ int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t
                         int at_corpus_end);
 /* Complete every pending async pass; the last one's table is the result. */
 int mox_run_wait(mox_engine* e);
+/* Engine group: one call for n_gpus device-resident shards (shards[i] on
+ * member i's GPU): local passes on every GPU at once, exchange, final
+ * reduce, gather on member 0 (and the bytewise sort with MOX_F_SORT_BYTES).
+ * A single-GPU engine takes one shard (= mox_run_range). */
+int mox_run_shards(mox_engine* e, const mox_shard* shards);
+/* Members of an engine group (1 for a single-GPU engine); member 0 is e
+ * itself.  A member's engine serves device allocations and copies for its
+ * shard (mox_device_alloc / mox_memcpy_h2d). */
+int mox_group_size(const mox_engine* e);
+mox_engine* mox_group_member(mox_engine* e, int i);
 /* Copy the table of the last run (or of the last exchange) to the host. */
 int mox_fetch_table(mox_engine* e, mox_table** out);
 int mox_get_stats(const mox_engine* e, mox_stats* out);

@@ -7,59 +7,15 @@
 // No host round-trip inside the pipeline; one small control-block read at the
 // end decides success, UTF-8 error, or a buffer-growth rerun.
 #include <fcntl.h>
-#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
-#include <algorithm>
-#include <chrono>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <string>
-#include <thread>
-#include <vector>
+#include <mutex>
 
-#include <rccl/rccl.h>
-
-#include "../../include/mox.h"
-#include "mox_internal.h"
-#include "mox_table.h"
+#include "mox_host.h"
 #include "mox_unicode_tables.h"
 
-using namespace mox;
-
-extern "C" {
-__global__ void k_map(Corpus c, Work w, uint64_t ntiles);
-__global__ void k_init(Work w, unsigned long long w_n, uint32_t flags);
-__global__ void k_ctl_out(const Ctl* src, Ctl* dst);
-__global__ void k_sample(Corpus c, Work w, uint32_t npieces);
-__global__ void k_dict_hist(Work w);
-__global__ void k_dict_pick(Work w, uint32_t max_words);
-__global__ void k_dict_build(Work w, uint32_t max_words);
-__global__ void k_dict_zero(Work w);
-__global__ void k_unicode(Corpus c, Work w, Tables T);
-__global__ void k_hist(Work w);
-__global__ void k_scatter(Work w);
-__global__ void k_reduce(Work w);
-__global__ void k_split_count(Work w);
-__global__ void k_unit_scan(Work w);
-__global__ void k_split_scatter(Work w);
-__global__ void k_unit_uniq_scan(Work w);
-__global__ void k_final_scan(Work w);
-__global__ void k_reduce_small(Work w);
-__global__ void k_reduce_sort1(Work w);
-__global__ void k_reduce_sort2(Work w);
-__global__ void k_mat(Work w, Corpus c);
-__global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
-__global__ void k_xpack_short(Work w, WRec* out);
-__global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob);
-__global__ void k_xingest(Work w, XDir dir, uint64_t n_short);
-__global__ void k_gather_offs(const uint8_t* recv, GDir d, uint64_t* out);
-}
-
-namespace {
+namespace mox_host {
 
 thread_local std::string g_err;
 
@@ -73,90 +29,6 @@ int fail(int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIPCHK(expr)                                                                             \
-  do {                                                                                           \
-    hipError_t e_ = (expr);                                                                      \
-    if (e_ != hipSuccess) return fail(MOX_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
-  } while (0)
-
-#define RCCLCHK(expr)                                                                            \
-  do {                                                                                           \
-    ncclResult_t r_ = (expr);                                                                    \
-    if (r_ != ncclSuccess) return fail(MOX_ERCCL, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
-  } while (0)
-
-uint64_t next_pow2(uint64_t x) {
-  uint64_t p = 1;
-  while (p < x) p <<= 1;
-  return p;
-}
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-};
-
-}  // namespace
-
-struct mox_engine {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  // async passes: pass k + 1's dictionary is built on dstream while pass k's
-  // reduce tail runs on stream (ev_dfree: pass k's k_unicode has read the
-  // dictionary buffers; ev_dready: the next dictionary is built)
-  hipStream_t dstream = nullptr;
-  hipEvent_t ev_dfree = nullptr, ev_dready = nullptr;
-  bool dfree_recorded = false;
-  uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 192;
-  int n_cu = 256;
-  bool sync_each = false;
-  int test_fail_alloc = 0;     // MOX_TEST_FAIL_ALLOC=k: the k-th sized allocation fails once (tests)
-  uint64_t next_cold_cap = 0;  // region capacity learnt from spills of an earlier run
-  Work w{};
-  Tables tables{};
-  Ctl* h_ctl = nullptr;       // pinned
-  Ctl* h_ctl_init = nullptr;  // pinned
-  // engine-owned corpus staging for host inputs
-  uint8_t* d_text = nullptr;
-  size_t d_text_cap = 0;
-  hipStream_t file_stream[8]{};  // mox_count_file readers (FILE_READERS)
-  uint8_t* file_pin[8][2]{};
-  // last run
-  bool have_result = false;
-  // where the result table lives (the pass's t_* buffers, or the gather buffers)
-  struct Res {
-    const uint64_t* counts = nullptr;
-    const uint64_t* offs = nullptr;
-    const uint8_t* bytes = nullptr;
-    uint64_t n = 0, nb = 0, tokens = 0;
-    bool pass = false;  // true: the t_* buffers of the last pass (an exchange can start from it)
-  } res;
-  DevBuf g_counts, g_offs, g_bytes, g_recv;  // mox_gather (root)
-  Corpus last_corpus{};
-  mox_stats stats{};
-  hipEvent_t ev[12]{};
-  // mox_run_range_async: two pass slots (the newest pass is enqueued before the
-  // previous one is completed, so the GPU runs them back to back)
-  struct AsyncSlot {
-    bool pending = false;
-    Corpus c{};
-    Ctl* h_ctl = nullptr;                  // pinned copy of this pass's control block
-    hipEvent_t ev_map0 = nullptr, ev_map1 = nullptr, ev_done = nullptr;
-  } aslot[2];
-  int anext = 0;
-  // multi-GPU
-  ncclComm_t comm = nullptr;
-  int nranks = 1, rank = 0;
-  XCnt* d_xcnt = nullptr;                 // [0, MAX_RANKS) sent, [MAX_RANKS, 2 MAX_RANKS) received
-  XCnt* h_xcnt = nullptr;                 // pinned mirror
-  unsigned long long* d_xcur = nullptr;   // 2 MAX_RANKS pack cursors
-  DevBuf x_send_short, x_send_blob, x_recv_short, x_recv_blob;  // device
-  DevBuf hx_send, hx_recv;                // pinned host staging (host transport)
-  Ctl* h_ctl_x = nullptr;                 // pinned control block of an exchange pass
-  std::vector<DevBuf> owned;  // allocations to free
-};
-
-namespace {
 
 int dalloc(mox_engine* e, void** p, size_t bytes) {
   if (bytes == 0) bytes = 16;
@@ -168,10 +40,6 @@ void dfree(void* p) {
   if (p) (void)hipFree(p);
 }
 
-// (Re)allocate every size-dependent buffer for the given capacities.
-struct Caps {
-  uint64_t cold_cap, spill_cap, w_cap, u_cap, arena_cap, long_cap, table_cap, bytes_cap, split_k_cap, split_w_cap;
-};
 
 Caps caps_of(const Work& w) {
   return Caps{w.cold_cap, w.spill_cap, w.w_cap, w.u_cap, w.arena_cap, w.long_cap, w.table_cap, w.bytes_cap, w.split_k_cap, w.split_w_cap};
@@ -356,27 +224,18 @@ float ev_ms(mox_engine* e, int a, int b) {
   return ms;
 }
 
-// Launch sequencing helpers: HIP-event timestamps (MOX_F_TIMING) and, with
-// MOX_SYNC_EACH=1, a synchronisation + name after every launch (hang / fault
-// triage).
-struct Seq {
-  mox_engine* e;
-  hipStream_t s;
-  bool timing, sync_each, map_only;
-  hipEvent_t map_ev[2] = {nullptr, nullptr};  // async passes: their own map events
-  void rec(int i) const {  // map_only: events 1 and 2 (around k_map) only
-    if ((i == 1 || i == 2) && map_ev[0]) {
-      if (timing || map_only) (void)hipEventRecord(map_ev[i - 1], s);
-      return;
-    }
-    if (timing || (map_only && (i == 1 || i == 2))) (void)hipEventRecord(e->ev[i], s);
+void Seq::rec(int i) const {  // map_only: events 1 and 2 (around k_map) only
+  if ((i == 1 || i == 2) && map_ev[0]) {
+    if (timing || map_only) (void)hipEventRecord(map_ev[i - 1], s);
+    return;
   }
-  void step(const char* name) const {
-    if (!sync_each) return;
-    hipError_t er = hipStreamSynchronize(s);
-    fprintf(stderr, "[mox] %s done: %s\n", name, hipGetErrorString(er));
-  }
-};
+  if (timing || (map_only && (i == 1 || i == 2))) (void)hipEventRecord(e->ev[i], s);
+}
+void Seq::step(const char* name) const {
+  if (!sync_each) return;
+  hipError_t er = hipStreamSynchronize(s);
+  fprintf(stderr, "[mox] %s done: %s\n", name, hipGetErrorString(er));
+}
 
 Seq seq_of(mox_engine* e) {
   const bool full = (e->flags & MOX_F_TIMING) != 0;
@@ -536,6 +395,8 @@ void set_result(mox_engine* e, const Ctl& h) {
   e->res.nb = h.bytes_total;
   e->res.tokens = h.tokens;
   e->res.pass = true;
+  e->res.exchanged = false;
+  e->res.sorted = false;
   e->have_result = true;
 }
 
@@ -551,6 +412,85 @@ int check_failed(const Ctl& h) {
   return MOX_OK;
 }
 
+// Diagnostics builds only (-DMOX_ABLATE / -DMOX_STAMP, tools/): per-workgroup
+// cycle stamps and the dictionary, written under $MOX_DEBUG_DIR (nothing is
+// written without it).  Production builds compile none of this.
+#if defined(MOX_ABLATE) || defined(MOX_STAMP)
+FILE* debug_file(const char* name) {
+  const char* dir = getenv("MOX_DEBUG_DIR");
+  if (!dir) return nullptr;
+  return fopen((std::string(dir) + "/" + name).c_str(), "w");
+}
+void debug_dump(mox_engine* e, const Ctl& h) {
+  if ((e->w.dbg & DBG_STAMP) && e->w.stamps) {
+    std::vector<unsigned long long> st(8 * NB);
+    (void)hipMemcpy(st.data(), e->w.stamps, st.size() * 8, hipMemcpyDeviceToHost);
+    std::vector<unsigned long long> mc(8 * 1024 * MAP_WAVES);
+    (void)hipMemcpy(mc.data(), e->w.stamps + 8 * 4096, mc.size() * 8, hipMemcpyDeviceToHost);
+    FILE* g = debug_file("mapcyc.csv");
+    if (g) {
+      for (uint32_t i = 0; i < e->w.map_grid * MAP_WAVES; i++)
+        fprintf(g, "%u,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, mc[8 * i], mc[8 * i + 1], mc[8 * i + 2], mc[8 * i + 3], mc[8 * i + 4],
+                mc[8 * i + 5], mc[8 * i + 6]);
+      fclose(g);
+    }
+    std::vector<unsigned long long> rc(4 * 1024 * 16);
+    (void)hipMemcpy(rc.data(), e->w.stamps + 8 * 4096 + 8 * 1024 * MAP_WAVES, rc.size() * 8, hipMemcpyDeviceToHost);
+    if (FILE* r = debug_file("redcyc.csv")) {
+      for (size_t i = 0; i < rc.size() / 4; i++) fprintf(r, "%zu,%llu,%llu,%llu,%llu\n", i, rc[4 * i], rc[4 * i + 1], rc[4 * i + 2], rc[4 * i + 3]);
+      fclose(r);
+    }
+    FILE* f = debug_file("stamps.csv");
+    if (f) {
+      for (int i = 0; i < NB; i++)
+        fprintf(f, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, st[8 * i], st[8 * i + 1], st[8 * i + 2], st[8 * i + 3], st[8 * i + 4], st[8 * i + 5], st[8 * i + 6]);
+      fclose(f);
+    }
+  }
+  if (getenv("MOX_DUMP_DICT")) {
+    std::vector<uint4> dk(DICT_SLOTS);
+    std::vector<uint32_t> dt(DICT_SLOTS);
+    std::vector<unsigned long long> tot(DICT_SLOTS);
+    (void)hipMemcpy(dk.data(), e->w.dict_key, DICT_SLOTS * 16, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(dt.data(), e->w.dict_tag, DICT_SLOTS * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(tot.data(), e->w.dict_tot, DICT_SLOTS * 8, hipMemcpyDeviceToHost);
+    std::vector<int> order;
+    unsigned long long sum = 0;
+    for (int i = 0; i < DICT_SLOTS; i++) if (dt[i]) { order.push_back(i); sum += tot[i]; }
+    std::sort(order.begin(), order.end(), [&](int a, int b) { return tot[a] > tot[b]; });
+    fprintf(stderr, "[mox] dict words %zu, hits %llu of %llu tokens\n", order.size(), sum, (unsigned long long)h.tokens);
+    {
+      std::vector<WRec> cand(GC_SLOTS), lst(DICT_MAX_WORDS);
+      std::vector<uint32_t> hist(257);
+      (void)hipMemcpy(cand.data(), e->w.cand, GC_SLOTS * sizeof(WRec), hipMemcpyDeviceToHost);
+      (void)hipMemcpy(lst.data(), e->w.dict_list, DICT_MAX_WORDS * sizeof(WRec), hipMemcpyDeviceToHost);
+      (void)hipMemcpy(hist.data(), e->w.dict_hist, 257 * 4, hipMemcpyDeviceToHost);
+      size_t nc = 0, ns = 0;
+      uint64_t best = 0;
+      for (auto& r : cand) if (r.count) { nc++; if ((r.w1 & ~(1ull << 63)) == 0) { ns++; best = std::max(best, (uint64_t)r.count); } }
+      fprintf(stderr, "[mox] cand: %zu used, %zu with w1==0 (max count %llu); picked %u, thresh %u, hist[255]=%u hist[2]=%u\n", nc, ns,
+              (unsigned long long)best, hist[256], h.dict_thresh, hist[255], hist[2]);
+      int k = 0;
+      for (uint32_t i = 0; i < std::min<uint32_t>(hist[256], DICT_MAX_WORDS) && k < 5; i++)
+        if (lst[i].w1 == 0) { char b[9] = {0}; memcpy(b, &lst[i].w0, 8); fprintf(stderr, "[mox]   list short '%s' count %llu\n", b, (unsigned long long)lst[i].count); k++; }
+    }
+    int nshort = 0;
+    for (size_t j = 0; j < order.size(); j++) {
+      const int i = order[j];
+      char wbuf[17] = {0};
+      memcpy(wbuf, &dk[i], 16);
+      if (strlen(wbuf) <= 4 && nshort < 6) { fprintf(stderr, "[mox]   short slot %d total %llu key '%s' tag %08x\n", i, tot[i], wbuf, dt[i]); nshort++; }
+    }
+    for (size_t j = 0; j < order.size() && j < 8; j++) {
+      const int i = order[j];
+      char wbuf[17] = {0};
+      memcpy(wbuf, &dk[i], 16);
+      fprintf(stderr, "[mox]   slot %d home %d total %llu key '%s'\n", i, (int)(dt[i] & (DICT_SLOTS - 1)), tot[i], wbuf);
+    }
+  }
+}
+#endif
+
 int run_corpus(mox_engine* e, const Corpus& c) {
   if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));  // no side-stream dictionary build in flight
   e->have_result = false;
@@ -563,79 +503,13 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   for (int attempt = 0;; attempt++) {
     if ((rc = pipeline_once(e, c))) return rc;
     const Ctl& h = *e->h_ctl;
-    if (getenv("MOX_VERBOSE"))
-      fprintf(stderr, "[mox] attempt %d: overflow 0x%x cold_need %llu spill_need %llu w_total %llu u_n %llu n_total %llu caps cold %u spill %u w %llu run %.3f ms\n",
+    if (e->verbose)
+      fprintf(stderr, "[mox] attempt %d: overflow 0x%x cold_need %llu spill_need %llu w_total %llu u_n %llu n_total %llu caps cold %u spill %u w %llu run %.3f ms; units %llu, sort2 list %llu, k_reduce list %llu, split partitions %u, max sub-passes %u\n",
               attempt, h.overflow, h.cold_need, h.spill_need, h.w_total, h.u_n, h.n_total, e->w.cold_cap, e->w.spill_cap,
-              (unsigned long long)e->w.w_cap, e->stats.ms_run);
-    if ((e->w.dbg & DBG_STAMP) && e->w.stamps) {
-      std::vector<unsigned long long> st(8 * NB);
-      (void)hipMemcpy(st.data(), e->w.stamps, st.size() * 8, hipMemcpyDeviceToHost);
-      std::vector<unsigned long long> mc(8 * 1024 * MAP_WAVES);
-      (void)hipMemcpy(mc.data(), e->w.stamps + 8 * 4096, mc.size() * 8, hipMemcpyDeviceToHost);
-      FILE* g = fopen("gpurun_out/mapcyc.csv", "w");
-      if (g) {
-        for (uint32_t i = 0; i < e->w.map_grid * MAP_WAVES; i++)
-          fprintf(g, "%u,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, mc[8 * i], mc[8 * i + 1], mc[8 * i + 2], mc[8 * i + 3], mc[8 * i + 4],
-                  mc[8 * i + 5], mc[8 * i + 6]);
-        fclose(g);
-      }
-      std::vector<unsigned long long> rc(4 * 1024 * 16);
-      (void)hipMemcpy(rc.data(), e->w.stamps + 8 * 4096 + 8 * 1024 * MAP_WAVES, rc.size() * 8, hipMemcpyDeviceToHost);
-      if (FILE* r = fopen("gpurun_out/redcyc.csv", "w")) {
-        for (size_t i = 0; i < rc.size() / 4; i++) fprintf(r, "%zu,%llu,%llu,%llu,%llu\n", i, rc[4 * i], rc[4 * i + 1], rc[4 * i + 2], rc[4 * i + 3]);
-        fclose(r);
-      }
-      FILE* f = fopen("gpurun_out/stamps.csv", "w");
-      if (f) {
-        for (int i = 0; i < NB; i++)
-          fprintf(f, "%d,%llu,%llu,%llu,%llu,%llu,%llu,%llu\n", i, st[8 * i], st[8 * i + 1], st[8 * i + 2], st[8 * i + 3], st[8 * i + 4], st[8 * i + 5], st[8 * i + 6]);
-        fclose(f);
-      }
-    }
-    if (getenv("MOX_DUMP_DICT")) {
-      std::vector<uint4> dk(DICT_SLOTS);
-      std::vector<uint32_t> dt(DICT_SLOTS);
-      std::vector<unsigned long long> tot(DICT_SLOTS);
-      (void)hipMemcpy(dk.data(), e->w.dict_key, DICT_SLOTS * 16, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(dt.data(), e->w.dict_tag, DICT_SLOTS * 4, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(tot.data(), e->w.dict_tot, DICT_SLOTS * 8, hipMemcpyDeviceToHost);
-      std::vector<int> order;
-      unsigned long long sum = 0;
-      for (int i = 0; i < DICT_SLOTS; i++) if (dt[i]) { order.push_back(i); sum += tot[i]; }
-      std::sort(order.begin(), order.end(), [&](int a, int b) { return tot[a] > tot[b]; });
-      fprintf(stderr, "[mox] dict words %zu, hits %llu of %llu tokens\n", order.size(), sum, (unsigned long long)h.tokens);
-      {
-        std::vector<WRec> cand(GC_SLOTS), lst(DICT_MAX_WORDS);
-        std::vector<uint32_t> hist(257);
-        (void)hipMemcpy(cand.data(), e->w.cand, GC_SLOTS * sizeof(WRec), hipMemcpyDeviceToHost);
-        (void)hipMemcpy(lst.data(), e->w.dict_list, DICT_MAX_WORDS * sizeof(WRec), hipMemcpyDeviceToHost);
-        (void)hipMemcpy(hist.data(), e->w.dict_hist, 257 * 4, hipMemcpyDeviceToHost);
-        size_t nc = 0, ns = 0;
-        uint64_t best = 0;
-        for (auto& r : cand) if (r.count) { nc++; if ((r.w1 & ~(1ull << 63)) == 0) { ns++; best = std::max(best, (uint64_t)r.count); } }
-        fprintf(stderr, "[mox] cand: %zu used, %zu with w1==0 (max count %llu); picked %u, thresh %u, hist[255]=%u hist[2]=%u\n", nc, ns,
-                (unsigned long long)best, hist[256], h.dict_thresh, hist[255], hist[2]);
-        int k = 0;
-        for (uint32_t i = 0; i < std::min<uint32_t>(hist[256], DICT_MAX_WORDS) && k < 5; i++)
-          if (lst[i].w1 == 0) { char b[9] = {0}; memcpy(b, &lst[i].w0, 8); fprintf(stderr, "[mox]   list short '%s' count %llu\n", b, (unsigned long long)lst[i].count); k++; }
-      }
-      int nshort = 0;
-      for (size_t j = 0; j < order.size(); j++) {
-        const int i = order[j];
-        char wbuf[17] = {0};
-        memcpy(wbuf, &dk[i], 16);
-        if (strlen(wbuf) <= 4 && nshort < 6) { fprintf(stderr, "[mox]   short slot %d total %llu key '%s' tag %08x\n", i, tot[i], wbuf, dt[i]); nshort++; }
-      }
-      for (size_t j = 0; j < order.size() && j < 8; j++) {
-        const int i = order[j];
-        char wbuf[17] = {0};
-        memcpy(wbuf, &dk[i], 16);
-        fprintf(stderr, "[mox]   slot %d home %d total %llu key '%s'\n", i, (int)(dt[i] & (DICT_SLOTS - 1)), tot[i], wbuf);
-      }
-    }
-    if (getenv("MOX_VERBOSE"))
-      fprintf(stderr, "[mox] dbg counters %llu %llu %llu %llu; units %llu, k_reduce_sort2 list %llu, k_reduce list %llu, split partitions %u, max sub-passes %u\n",
-              h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2], h.dbg_cnt[3], h.n_units, h.n_mid, h.n_big, h.n_split, h.max_sub);
+              (unsigned long long)e->w.w_cap, e->stats.ms_run, h.n_units, h.n_mid, h.n_big, h.n_split, h.max_sub);
+#if defined(MOX_ABLATE) || defined(MOX_STAMP)
+    debug_dump(e, h);
+#endif
     if ((rc = check_failed(h))) return rc;
     if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
     if (h.halo_err != ~0ull)
@@ -672,6 +546,8 @@ void commit_result(mox_engine* e, const Corpus& c, const Ctl& h) {
   e->stats.max_subpasses = h.max_sub ? h.max_sub : 1;
   e->stats.reduce_units = h.n_units;
   e->stats.split_partitions = h.n_split;
+  static_assert(sizeof(e->stats.path_hits) == sizeof(h.paths), "path counters");
+  std::memcpy(e->stats.path_hits, h.paths, sizeof h.paths);
   e->last_corpus = c;
   set_result(e, h);
 }
@@ -752,448 +628,12 @@ Corpus make_corpus(const void* d_buf, size_t buf_len, size_t own_begin, size_t o
 }
 
 
-// ============================================================== multi-GPU exchange
-//   After a local pass every rank holds a dense table of its
-// byte range.  Each table row goes to the owner of its hash (short words:
-// partition ranges, already contiguous per owner in the dense order; long
-// words: FNV hash ranges, packed per owner).  The exchange is three
-// all-to-alls (per-peer counts, short records, long blobs) over a transport,
-// then one reduce-only pass over the received partials produces this rank's
-// final table.  Ranks own disjoint word sets.
-
-int grow_dev(DevBuf& b, size_t bytes) {
-  if (b.cap >= bytes && b.p) return MOX_OK;
-  dfree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
-  hipError_t err = hipMalloc(&b.p, want);
-  if (err != hipSuccess) return fail(MOX_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(err));
-  b.cap = want;
-  return MOX_OK;
-}
-int grow_pinned(DevBuf& b, size_t bytes) {
-  if (b.cap >= bytes && b.p) return MOX_OK;
-  if (b.p) (void)hipHostFree(b.p);
-  b.p = nullptr;
-  b.cap = 0;
-  size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
-  hipError_t err = hipHostMalloc(&b.p, want, hipHostMallocDefault);
-  if (err != hipSuccess) return fail(MOX_ENOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(err));
-  b.cap = want;
-  return MOX_OK;
-}
-
-// Moves per-peer byte ranges between ranks.  send/recv are device buffers;
-// off/len are per-peer byte offsets and sizes (len identical on both sides of
-// every pair by construction).
-struct Transport {
-  virtual ~Transport() = default;
-  // per-peer count rows: d_send[d] (device, just written by k_xcount) -> peer
-  // d; on return h_send holds this rank's rows and h_recv[s] peer s's rows.
-  virtual int counts(const XCnt* d_send, XCnt* d_recv, XCnt* h_send, XCnt* h_recv) = 0;
-  virtual int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
-                        const uint64_t* rlen) = 0;
-  // two independent all-to-alls (short records, long-word blobs); a transport
-  // may move both in one round
-  virtual int alltoallv_pair(const uint8_t* send_a, const uint64_t* soff_a, const uint64_t* slen_a, uint8_t* recv_a,
-                             const uint64_t* roff_a, const uint64_t* rlen_a, const uint8_t* send_b, const uint64_t* soff_b,
-                             const uint64_t* slen_b, uint8_t* recv_b, const uint64_t* roff_b, const uint64_t* rlen_b) {
-    int rc = alltoallv(send_a, soff_a, slen_a, recv_a, roff_a, rlen_a);
-    return rc ? rc : alltoallv(send_b, soff_b, slen_b, recv_b, roff_b, rlen_b);
-  }
-};
-
-struct RcclTransport : Transport {
-  mox_engine* e;
-  explicit RcclTransport(mox_engine* e_) : e(e_) {}
-  int counts(const XCnt* d_send, XCnt* d_recv, XCnt* h_send, XCnt* h_recv) override {
-    // device to device right after k_xcount: one host synchronisation for both rows
-    const int P = e->nranks;
-    RCCLCHK(ncclGroupStart());
-    for (int p = 0; p < P; p++) {
-      RCCLCHK(ncclSend(d_send + p, sizeof(XCnt), ncclUint8, p, e->comm, e->stream));
-      RCCLCHK(ncclRecv(d_recv + p, sizeof(XCnt), ncclUint8, p, e->comm, e->stream));
-    }
-    RCCLCHK(ncclGroupEnd());
-    HIPCHK(hipMemcpyAsync(h_send, d_send, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipMemcpyAsync(h_recv, d_recv, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    return MOX_OK;
-  }
-  int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
-                const uint64_t* rlen) override {
-    const int P = e->nranks, me = e->rank;
-    if (slen[me]) HIPCHK(hipMemcpyAsync(recv + roff[me], send + soff[me], slen[me], hipMemcpyDeviceToDevice, e->stream));
-    RCCLCHK(ncclGroupStart());
-    for (int p = 0; p < P; p++) {
-      if (p == me) continue;
-      if (slen[p]) RCCLCHK(ncclSend(send + soff[p], slen[p], ncclUint8, p, e->comm, e->stream));
-      if (rlen[p]) RCCLCHK(ncclRecv(recv + roff[p], rlen[p], ncclUint8, p, e->comm, e->stream));
-    }
-    RCCLCHK(ncclGroupEnd());
-    return MOX_OK;
-  }
-  // both payloads inside ONE ncclGroupStart/End: one RCCL launch and one round
-  // of peer handshakes per exchange instead of two
-  int alltoallv_pair(const uint8_t* send_a, const uint64_t* soff_a, const uint64_t* slen_a, uint8_t* recv_a,
-                     const uint64_t* roff_a, const uint64_t* rlen_a, const uint8_t* send_b, const uint64_t* soff_b,
-                     const uint64_t* slen_b, uint8_t* recv_b, const uint64_t* roff_b, const uint64_t* rlen_b) override {
-    const int P = e->nranks, me = e->rank;
-    if (slen_a[me]) HIPCHK(hipMemcpyAsync(recv_a + roff_a[me], send_a + soff_a[me], slen_a[me], hipMemcpyDeviceToDevice, e->stream));
-    if (slen_b[me]) HIPCHK(hipMemcpyAsync(recv_b + roff_b[me], send_b + soff_b[me], slen_b[me], hipMemcpyDeviceToDevice, e->stream));
-    if (P == 1) return MOX_OK;
-    RCCLCHK(ncclGroupStart());
-    for (int p = 0; p < P; p++) {
-      if (p == me) continue;
-      if (slen_a[p]) RCCLCHK(ncclSend(send_a + soff_a[p], slen_a[p], ncclUint8, p, e->comm, e->stream));
-      if (rlen_a[p]) RCCLCHK(ncclRecv(recv_a + roff_a[p], rlen_a[p], ncclUint8, p, e->comm, e->stream));
-      if (slen_b[p]) RCCLCHK(ncclSend(send_b + soff_b[p], slen_b[p], ncclUint8, p, e->comm, e->stream));
-      if (rlen_b[p]) RCCLCHK(ncclRecv(recv_b + roff_b[p], rlen_b[p], ncclUint8, p, e->comm, e->stream));
-    }
-    RCCLCHK(ncclGroupEnd());
-    return MOX_OK;
-  }
-};
-
-// Host-staged transport: device -> pinned host, caller's all-to-all callback
-// (e.g. torch.distributed over gloo), pinned host -> device.  Used where RCCL
-// cannot run (several ranks sharing one GPU in tests).
-struct HostTransport : Transport {
-  mox_engine* e;
-  int P;
-  mox_alltoallv_fn fn;
-  void* user;
-  HostTransport(mox_engine* e_, int P_, mox_alltoallv_fn f, void* u) : e(e_), P(P_), fn(f), user(u) {}
-  int counts(const XCnt* d_send, XCnt*, XCnt* h_send, XCnt* h_recv) override {
-    HIPCHK(hipMemcpyAsync(h_send, d_send, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    uint64_t len[MAX_RANKS];
-    for (int p = 0; p < P; p++) len[p] = sizeof(XCnt);
-    if (fn(user, h_send, len, h_recv, len) != 0) return fail(MOX_EIO, "host all-to-all callback failed (counts)");
-    return MOX_OK;
-  }
-  int alltoallv(const uint8_t* send, const uint64_t* soff, const uint64_t* slen, uint8_t* recv, const uint64_t* roff,
-                const uint64_t* rlen) override {
-    const uint64_t stot = soff[P - 1] + slen[P - 1], rtot = roff[P - 1] + rlen[P - 1];
-    int rc;
-    // a previous call's H2D from hx_recv may still be in flight on the stream:
-    // drain it before a regrow frees the pinned buffer under it
-    if (e->hx_send.cap < stot + 8 || e->hx_recv.cap < rtot + 8) HIPCHK(hipStreamSynchronize(e->stream));
-    if ((rc = grow_pinned(e->hx_send, stot + 8)) || (rc = grow_pinned(e->hx_recv, rtot + 8))) return rc;
-    if (stot) HIPCHK(hipMemcpyAsync(e->hx_send.p, send, stot, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if (fn(user, e->hx_send.p, slen, e->hx_recv.p, rlen) != 0) return fail(MOX_EIO, "host all-to-all callback failed");
-    if (rtot) HIPCHK(hipMemcpyAsync(recv, e->hx_recv.p, rtot, hipMemcpyHostToDevice, e->stream));
-    return MOX_OK;
-  }
-};
-
-// One attempt of the reduce-only pass over the received partials.
-int exchange_pass_once(mox_engine* e, uint64_t r_short, uint64_t blob_bytes, const XDir& rdir) {
-  Work& w = e->w;
-  hipStream_t s = e->stream;
-  const Seq q = seq_of(e);
-  q.rec(0);
-  // control block (w_n = received records), counters, long table, no map regions
-  hipLaunchKernelGGL(k_init, dim3(256), dim3(256), 0, s, w, (unsigned long long)r_short, 2u);
-  if (r_short) HIPCHK(hipMemcpyAsync(w.w, e->x_recv_short.p, r_short * sizeof(WRec), hipMemcpyDeviceToDevice, s));
-  if (blob_bytes) HIPCHK(hipMemcpyAsync(w.arena, e->x_recv_blob.p, blob_bytes, hipMemcpyDeviceToDevice, s));
-  q.rec(1);
-  q.rec(2);
-  hipLaunchKernelGGL(k_xingest, dim3(1024), dim3(256), 0, s, w, rdir, r_short);
-  q.step("k_xingest");
-  q.rec(3);
-  Corpus none{};
-  none.base = (const uint8_t*)w.ctl;  // long refs are all arena refs in this pass
-  launch_reduce_tail(e, none, q);
-  return finish_pass(e, q);
-}
-
-int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, const XDir& rdir, const mox_stats& local,
-                    std::chrono::steady_clock::time_point t0);
-
-int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
-  if (int rc = drain_async(e)) return rc;
-  if (!e->have_result || !e->res.pass) return fail(MOX_ESTATE, "no local result: mox_run_range first");
-  if (P > MAX_RANKS) return fail(MOX_EINVAL, "at most %d ranks", MAX_RANKS);
-  HIPCHK(hipSetDevice(e->device));
-  Work& w = e->w;
-  hipStream_t s = e->stream;
-  int rc;
-  const auto t0 = std::chrono::steady_clock::now();
-  const mox_stats local = e->stats;  // the exchange pass reuses the phase events
-  if (!e->d_xcnt) {
-    if ((rc = dalloc(e, (void**)&e->d_xcnt, 2 * MAX_RANKS * sizeof(XCnt)))) return rc;
-    if ((rc = dalloc(e, (void**)&e->d_xcur, 2 * MAX_RANKS * 8))) return rc;
-    HIPCHK(hipHostMalloc((void**)&e->h_xcnt, 2 * MAX_RANKS * sizeof(XCnt), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc((void**)&e->h_ctl_x, sizeof(Ctl), hipHostMallocDefault));
-  }
-  XCnt* d_send = e->d_xcnt;
-  XCnt* d_recv = e->d_xcnt + MAX_RANKS;
-  XCnt* h_send = e->h_xcnt;
-  XCnt* h_recv = e->h_xcnt + MAX_RANKS;
-  // 1. per-destination counts
-  HIPCHK(hipMemsetAsync(d_send, 0, P * sizeof(XCnt), s));
-  hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, s, w, (uint32_t)P, d_send);
-  if ((rc = T.counts(d_send, d_recv, h_send, h_recv))) return rc;
-  // 2. send layout + pack
-  uint64_t s_short_off[MAX_RANKS], s_short_len[MAX_RANKS], s_blob_off[MAX_RANKS], s_blob_len[MAX_RANKS];
-  uint64_t r_short_off[MAX_RANKS], r_short_len[MAX_RANKS], r_blob_off[MAX_RANKS], r_blob_len[MAX_RANKS];
-  uint64_t ns = 0, sb = 0, rs = 0, rb = 0, r_long = 0;
-  XDir sdir{}, rdir{};
-  sdir.P = rdir.P = (uint32_t)P;
-  for (int d = 0; d < P; d++) {
-    s_short_off[d] = ns * sizeof(WRec);
-    s_short_len[d] = h_send[d].n_short * sizeof(WRec);
-    ns += h_send[d].n_short;
-    sdir.blob[d] = s_blob_off[d] = sb;
-    sdir.nlong[d] = h_send[d].n_long;
-    s_blob_len[d] = h_send[d].n_long * sizeof(XHdr) + h_send[d].long_bytes;
-    sb += s_blob_len[d];
-    r_short_off[d] = rs * sizeof(WRec);
-    r_short_len[d] = h_recv[d].n_short * sizeof(WRec);
-    rs += h_recv[d].n_short;
-    rdir.blob[d] = r_blob_off[d] = rb;
-    rdir.nlong[d] = h_recv[d].n_long;
-    rdir.hpre[d] = r_long;
-    r_long += h_recv[d].n_long;
-    r_blob_len[d] = h_recv[d].n_long * sizeof(XHdr) + h_recv[d].long_bytes;
-    rb += r_blob_len[d];
-  }
-  sdir.blob[P] = sb;
-  rdir.blob[P] = rb;
-  rdir.hpre[P] = r_long;
-  if ((rc = grow_dev(e->x_send_short, ns * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_send_blob, sb + 64)) ||
-      (rc = grow_dev(e->x_recv_short, rs * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_recv_blob, rb + 64)))
-    return rc;
-  hipLaunchKernelGGL(k_xpack_short, dim3(1024), dim3(256), 0, s, w, (WRec*)e->x_send_short.p);
-  HIPCHK(hipMemsetAsync(e->d_xcur, 0, 2 * MAX_RANKS * 8, s));
-  hipLaunchKernelGGL(k_xpack_long, dim3(256), dim3(256), 0, s, w, sdir, e->d_xcur, (uint8_t*)e->x_send_blob.p);
-  HIPCHK(hipGetLastError());
-  (void)me;
-  // 3. payload all-to-alls
-  if ((rc = T.alltoallv_pair((const uint8_t*)e->x_send_short.p, s_short_off, s_short_len, (uint8_t*)e->x_recv_short.p,
-                             r_short_off, r_short_len, (const uint8_t*)e->x_send_blob.p, s_blob_off, s_blob_len,
-                             (uint8_t*)e->x_recv_blob.p, r_blob_off, r_blob_len)))
-    return rc;
-  // 4. reduce-only pass over the received partials (the local table is no
-  //    longer needed: buffers may be regrown)
-  if ((rc = reduce_received(e, rs, rb, r_long, rdir, local, t0))) return rc;
-  e->stats.x_bytes_sent = ns * sizeof(WRec) + sb + P * sizeof(XCnt);
-  e->stats.x_bytes_recv = rs * sizeof(WRec) + rb + P * sizeof(XCnt);
-  return MOX_OK;
-}
-
-// ============================================================== gather (mox_gather)
-// Every rank sends its final table [counts (8 n) | offs (8 n) | bytes (nb,
-// padded to 8)] to the root; the root concatenates the blocks in rank order
-// (counts and bytes by device copies, offsets rebased by k_gather_offs) into
-// its gather buffers, which then become its result.  Ranks own disjoint words
-// after the exchange, so the concatenation is the whole corpus's table.
-int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
-  if (int rc = drain_async(e)) return rc;
-  if (!e->have_result) return fail(MOX_ESTATE, "no result to gather: run (and exchange) first");
-  if (P > MAX_RANKS || root < 0 || root >= P) return fail(MOX_EINVAL, "bad root %d of %d ranks", root, P);
-  HIPCHK(hipSetDevice(e->device));
-  hipStream_t s = e->stream;
-  int rc;
-  const auto t0 = std::chrono::steady_clock::now();
-  if (!e->d_xcnt) {
-    if ((rc = dalloc(e, (void**)&e->d_xcnt, 2 * MAX_RANKS * sizeof(XCnt)))) return rc;
-    if ((rc = dalloc(e, (void**)&e->d_xcur, 2 * MAX_RANKS * 8))) return rc;
-    HIPCHK(hipHostMalloc((void**)&e->h_xcnt, 2 * MAX_RANKS * sizeof(XCnt), hipHostMallocDefault));
-    HIPCHK(hipHostMalloc((void**)&e->h_ctl_x, sizeof(Ctl), hipHostMallocDefault));
-  }
-  const mox_engine::Res r = e->res;
-  const uint64_t n = r.n, nb = r.nb, nb8 = (nb + 7) & ~7ull, block = 16 * n + nb8;
-  // 1. sizes: every rank's (n, nb, tokens) row to every peer (only the root uses them)
-  XCnt* d_send = e->d_xcnt;
-  XCnt* d_recv = e->d_xcnt + MAX_RANKS;
-  XCnt* h_send = e->h_xcnt;
-  XCnt* h_recv = e->h_xcnt + MAX_RANKS;
-  for (int d = 0; d < P; d++) h_send[d] = XCnt{n, nb, r.tokens, 0};
-  HIPCHK(hipMemcpyAsync(d_send, h_send, P * sizeof(XCnt), hipMemcpyHostToDevice, s));
-  if ((rc = T.counts(d_send, d_recv, h_send, h_recv))) return rc;
-  // 2. this rank's block -> the root
-  if ((rc = grow_dev(e->x_send_blob, block + 64))) return rc;
-  uint8_t* sb = (uint8_t*)e->x_send_blob.p;
-  if (n) {
-    HIPCHK(hipMemcpyAsync(sb, r.counts, 8 * n, hipMemcpyDeviceToDevice, s));
-    HIPCHK(hipMemcpyAsync(sb + 8 * n, r.offs, 8 * n, hipMemcpyDeviceToDevice, s));
-    if (nb) HIPCHK(hipMemcpyAsync(sb + 16 * n, r.bytes, nb, hipMemcpyDeviceToDevice, s));
-  }
-  uint64_t soff[MAX_RANKS], slen[MAX_RANKS], roff[MAX_RANKS], rlen[MAX_RANKS];
-  uint64_t so = 0, ro = 0, N = 0, NB = 0, tok = 0;
-  GDir gd{};
-  gd.P = (uint32_t)P;
-  for (int d = 0; d < P; d++) {
-    soff[d] = so;
-    slen[d] = d == root ? block : 0;
-    so += slen[d];
-    const uint64_t bn = h_recv[d].n_short, bb = h_recv[d].n_long;  // rank d's n, nb
-    roff[d] = ro;
-    rlen[d] = me == root ? 16 * bn + ((bb + 7) & ~7ull) : 0;
-    gd.roff[d] = ro + 8 * bn;  // rank d's offs block
-    gd.base_n[d] = N;
-    gd.base_b[d] = NB;
-    ro += rlen[d];
-    N += bn;
-    NB += bb;
-    tok += h_recv[d].long_bytes;
-  }
-  gd.base_n[P] = N;
-  gd.base_b_total = NB;
-  if (me == root && (rc = grow_dev(e->g_recv, ro + 64))) return rc;
-  if ((rc = T.alltoallv(sb, soff, slen, (uint8_t*)(me == root ? e->g_recv.p : e->x_send_blob.p), roff, rlen))) return rc;
-  e->stats.gather_bytes = me == root ? ro : block;
-  if (me == root) {
-    // 3. root: concatenate in rank order
-    if ((rc = grow_dev(e->g_counts, 8 * N + 64)) || (rc = grow_dev(e->g_offs, 8 * (N + 1) + 64)) ||
-        (rc = grow_dev(e->g_bytes, NB + 64)))
-      return rc;
-    const uint8_t* rb = (const uint8_t*)e->g_recv.p;
-    for (int d = 0; d < P; d++) {
-      const uint64_t bn = h_recv[d].n_short, bb = h_recv[d].n_long;
-      if (bn) HIPCHK(hipMemcpyAsync((uint64_t*)e->g_counts.p + gd.base_n[d], rb + roff[d], 8 * bn, hipMemcpyDeviceToDevice, s));
-      if (bb) HIPCHK(hipMemcpyAsync((uint8_t*)e->g_bytes.p + gd.base_b[d], rb + roff[d] + 16 * bn, bb, hipMemcpyDeviceToDevice, s));
-    }
-    hipLaunchKernelGGL(k_gather_offs, dim3(256), dim3(256), 0, s, rb, gd, (uint64_t*)e->g_offs.p);
-    HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(s));
-    e->res.counts = (const uint64_t*)e->g_counts.p;
-    e->res.offs = (const uint64_t*)e->g_offs.p;
-    e->res.bytes = (const uint8_t*)e->g_bytes.p;
-    e->res.n = N;
-    e->res.nb = NB;
-    e->res.tokens = tok;
-    e->res.pass = false;
-  } else {
-    HIPCHK(hipStreamSynchronize(s));  // the send buffer is reused by the next exchange
-  }
-  e->stats.ms_gather = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  return MOX_OK;
-}
-
-// Reduce-only pass over partial (word, count) records already in
-// x_recv_short (rs WRecs) and x_recv_blob (long-word blobs described by rdir):
-// the exchange's final reduce and mox_reduce_pairs (spill files) share it.
-int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, const XDir& rdir, const mox_stats& local,
-                    std::chrono::steady_clock::time_point t0) {
-  Work& w = e->w;
-  int rc;
-  Caps need = w.cold ? caps_of(w) : initial_caps(1 << 20, e->n_cu);
-  need.w_cap = std::max<uint64_t>(need.w_cap, rs + rs / 8 + 1024);
-  need.table_cap = std::max<uint64_t>(need.table_cap, rs + r_long + 1024);
-  need.bytes_cap = std::max<uint64_t>(need.bytes_cap, rs * 16 + rb + 65536);
-  need.long_cap = std::max<uint64_t>(need.long_cap, next_pow2(2 * r_long + 1024));
-  need.arena_cap = std::max<uint64_t>(need.arena_cap, rb + 65536);
-  e->have_result = false;
-  if ((rc = ensure_caps(e, need))) return rc;  // stream-ordered; a regrow synchronises the device itself
-  for (int attempt = 0;; attempt++) {
-    if ((rc = exchange_pass_once(e, rs, rb, rdir))) return rc;
-    const Ctl& h = *e->h_ctl;
-    if ((rc = check_failed(h))) return rc;
-    if (!h.overflow) break;
-    if (h.overflow & OVF_REDUCE) return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
-    if (attempt >= 4) return fail(MOX_ENOMEM, "exchange buffer growth did not converge (overflow mask 0x%x)", h.overflow);
-    e->stats.retries++;
-    if ((rc = ensure_caps(e, grow_for(e, h)))) return rc;
-  }
-  const Ctl& h = *e->h_ctl;
-  const uint32_t retries = e->stats.retries;
-  e->stats = local;
-  e->stats.retries = retries;
-  e->stats.tokens = h.tokens;
-  e->stats.uniques = h.n_total;
-  e->stats.ms_exchange = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  e->last_corpus = Corpus{};
-  e->last_corpus.base = (const uint8_t*)w.ctl;
-  set_result(e, h);
-  return MOX_OK;
-}
-
-// Host (word, count) pairs -> the exchange's receive layout (one source):
-// words of 1..16 bytes without a NUL byte become 16-byte zero-padded WRec keys,
-// every other word an XHdr + its bytes (padded to 8) in the long blob.  Words
-// are taken as given (no lowercasing: reduce_phase sums parts[0] verbatim,
-// main.rs:160-162,131-134).
-int reduce_pairs_impl(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n) {
-  if (int rc = drain_async(e)) return rc;
-  HIPCHK(hipSetDevice(e->device));
-  const auto t0 = std::chrono::steady_clock::now();
-  std::vector<WRec> shorts;
-  std::vector<XHdr> hdrs;
-  std::vector<uint8_t> lbytes;
-  shorts.reserve(n);
-  for (uint64_t i = 0; i < n; i++) {
-    const uint64_t a = offs[i], len = offs[i + 1] - offs[i];
-    if (offs[i + 1] < a) return fail(MOX_EINVAL, "offs not ascending at %llu", (unsigned long long)i);
-    if (len == 0) return fail(MOX_EINVAL, "empty word at %llu (split_whitespace never yields one)", (unsigned long long)i);
-    const bool nul = memchr(bytes + a, 0, len) != nullptr;
-    if (len <= 16 && !nul) {
-      uint8_t k[16] = {0};
-      memcpy(k, bytes + a, len);
-      WRec r;
-      memcpy(&r.w0, k, 8);
-      memcpy(&r.w1, k + 8, 8);
-      r.count = counts[i];
-      shorts.push_back(r);
-    } else {
-      uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a 64 (any hash works: all long words of this pass use it)
-      for (uint64_t j = 0; j < len; j++) h = (h ^ bytes[a + j]) * 0x100000001b3ull;
-      hdrs.push_back(XHdr{h, len, counts[i], (uint64_t)lbytes.size()});
-      lbytes.insert(lbytes.end(), bytes + a, bytes + a + len);
-      lbytes.resize((lbytes.size() + 7) & ~size_t(7), 0);
-    }
-  }
-  const uint64_t rs = shorts.size(), r_long = hdrs.size();
-  const uint64_t rb = r_long * sizeof(XHdr) + lbytes.size();
-  int rc;
-  if ((rc = grow_dev(e->x_recv_short, rs * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_recv_blob, rb + 64))) return rc;
-  if (rs) HIPCHK(hipMemcpyAsync(e->x_recv_short.p, shorts.data(), rs * sizeof(WRec), hipMemcpyHostToDevice, e->stream));
-  if (r_long) {
-    HIPCHK(hipMemcpyAsync(e->x_recv_blob.p, hdrs.data(), r_long * sizeof(XHdr), hipMemcpyHostToDevice, e->stream));
-    if (!lbytes.empty())
-      HIPCHK(hipMemcpyAsync((uint8_t*)e->x_recv_blob.p + r_long * sizeof(XHdr), lbytes.data(), lbytes.size(),
-                            hipMemcpyHostToDevice, e->stream));
-  }
-  // pageable sources: complete the copies before the vectors go away
-  HIPCHK(hipStreamSynchronize(e->stream));
-  XDir rdir{};
-  rdir.P = 1;
-  rdir.blob[0] = 0;
-  rdir.blob[1] = rb;
-  rdir.nlong[0] = r_long;
-  rdir.hpre[0] = 0;
-  rdir.hpre[1] = r_long;
-  mox_stats local{};
-  local.weighted_records = rs + r_long;
-  return reduce_received(e, rs, rb, r_long, rdir, local, t0);
-}
-
-}  // namespace
-
-// ============================================================== C ABI
-extern "C" {
-
-const char* mox_last_error(void) { return g_err.c_str(); }
-int mox_abi_version(void) { return MOX_ABI_VERSION; }
-
-int mox_set_flags(mox_engine* e, uint32_t flags) {
-  if (!e) return fail(MOX_EINVAL, "NULL engine");
-  e->flags = flags;
-  return MOX_OK;
-}
-
-int mox_engine_create(const mox_config* cfg, mox_engine** out) {
-  if (!out) return fail(MOX_EINVAL, "out is NULL");
+// One engine on HIP device dev (-1: the current device).
+int engine_create_one(const mox_config* cfg, int dev, mox_engine** out) {
   *out = nullptr;
   mox_engine* e = new (std::nothrow) mox_engine();
   if (!e) return fail(MOX_ENOMEM, "host allocation failed");
-  int dev = -1;
   if (cfg) {
-    dev = cfg->device;
     e->flags = cfg->flags;
     if (cfg->dict_words) e->dict_words = std::min<uint32_t>(cfg->dict_words, DICT_MAX_WORDS);
     if (cfg->sample_pieces) e->sample_pieces = std::min<uint32_t>(cfg->sample_pieces, MAX_SAMPLE_PIECES);
@@ -1234,6 +674,7 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
   if (const char* d = getenv("MOX_DBG")) e->w.dbg = (uint32_t)strtoul(d, nullptr, 0);
   if (e->w.dbg & DBG_STAMP) (void)hipMalloc((void**)&e->w.stamps, 8 * 8 * 4096 + 8 * 8 * 1024 * MAP_WAVES + 8 * 4 * 1024 * 16);
   e->sync_each = getenv("MOX_SYNC_EACH") != nullptr;
+  e->verbose = getenv("MOX_VERBOSE") != nullptr;
   if (const char* f = getenv("MOX_TEST_FAIL_ALLOC")) e->test_fail_alloc = atoi(f);
   int rc = alloc_fixed(e);
   if (rc == MOX_OK && cfg && cfg->reserve_bytes) rc = ensure_caps(e, initial_caps(cfg->reserve_bytes, e->n_cu));
@@ -1247,8 +688,132 @@ int mox_engine_create(const mox_config* cfg, mox_engine** out) {
   return MOX_OK;
 }
 
+// Host buffer -> the engine's corpus staging buffer d_text.  Pageable copies
+// to one device are serialised: an engine group whose members share a GPU
+// (copy transport, tests) copied corrupted bytes when two threads ran
+// pageable hipMemcpyAsync to the same device at once (an invalid-UTF-8 error
+// in one member's shard of valid text); members on different GPUs still copy
+// in parallel.
+std::mutex g_stage_mu[64];
+int stage_host_range(mox_engine* e, const uint8_t* text, size_t len) {
+  std::lock_guard<std::mutex> lock(g_stage_mu[e->device & 63]);
+  if (len > e->d_text_cap) {
+    dfree(e->d_text);
+    e->d_text = nullptr;
+    e->d_text_cap = 0;
+    int rc = dalloc(e, (void**)&e->d_text, len + 64);
+    if (rc) return rc;
+    e->d_text_cap = len;
+  }
+  const bool timing = (e->flags & MOX_F_TIMING) != 0;
+  if (timing) HIPCHK(hipEventRecord(e->ev[8], e->stream));
+  if (len) HIPCHK(hipMemcpyAsync(e->d_text, text, len, hipMemcpyHostToDevice, e->stream));
+  if (timing) HIPCHK(hipEventRecord(e->ev[9], e->stream));
+  HIPCHK(hipStreamSynchronize(e->stream));
+  if (timing) e->stats.ms_h2d = ev_ms(e, 8, 9);
+  return MOX_OK;
+}
+
+
+// File -> HBM (SURVEY §8(f) rank 2): FILE_READERS threads each pread their
+// chunks (c = t, t + FILE_READERS, ...) into two pinned buffers of their own and
+// copy them with hipMemcpyAsync on a stream of their own, so the page-cache /
+// disk reads of one chunk overlap the PCIe copies of the others.  Pinned
+// buffers and streams are engine-owned and reused across calls.
+constexpr int FILE_READERS = 8;
+constexpr size_t FILE_CHUNK = 32u << 20;
+// Bytes [off, off + len) of the file -> d_text[0, len).
+int stage_file_range(mox_engine* e, int fd, uint64_t off0, size_t len) {
+  if (len > e->d_text_cap) {
+    dfree(e->d_text);
+    e->d_text = nullptr;
+    e->d_text_cap = 0;
+    int rc = dalloc(e, (void**)&e->d_text, len + 64);
+    if (rc) return rc;
+    e->d_text_cap = len;
+  }
+  for (int t = 0; t < FILE_READERS; t++) {
+    if (!e->file_stream[t]) HIPCHK(hipStreamCreateWithFlags(&e->file_stream[t], hipStreamNonBlocking));
+    for (int k = 0; k < 2; k++)
+      if (!e->file_pin[t][k]) HIPCHK(hipHostMalloc((void**)&e->file_pin[t][k], FILE_CHUNK, hipHostMallocDefault));
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  const size_t nchunks = (len + FILE_CHUNK - 1) / FILE_CHUNK;
+  std::vector<int> err(FILE_READERS, 0);
+  std::vector<std::string> msg(FILE_READERS);
+  auto reader = [&](int t) {
+    (void)hipSetDevice(e->device);
+    int k = 0;
+    size_t pending = 0;  // copies in flight on this reader's stream
+    for (size_t c = t; c < nchunks; c += FILE_READERS, k ^= 1) {
+      if (pending == 2) {  // the buffer about to be refilled was copied two chunks ago
+        if (hipStreamSynchronize(e->file_stream[t]) != hipSuccess) { err[t] = MOX_EHIP; msg[t] = "file copy failed"; return; }
+        pending = 0;
+      }
+      const size_t off = c * FILE_CHUNK, n = std::min(FILE_CHUNK, len - off);
+      size_t got = 0;
+      while (got < n) {
+        const ssize_t r = pread(fd, e->file_pin[t][k] + got, n - got, (off_t)(off0 + off + got));
+        if (r < 0 && errno == EINTR) continue;
+        if (r <= 0) { err[t] = MOX_EIO; msg[t] = std::string("read failed: ") + (r < 0 ? strerror(errno) : "short file"); return; }
+        got += (size_t)r;
+      }
+      if (hipMemcpyAsync(e->d_text + off, e->file_pin[t][k], n, hipMemcpyHostToDevice, e->file_stream[t]) != hipSuccess) {
+        err[t] = MOX_EHIP; msg[t] = "hipMemcpyAsync failed"; return;
+      }
+      pending++;
+    }
+    if (hipStreamSynchronize(e->file_stream[t]) != hipSuccess) { err[t] = MOX_EHIP; msg[t] = "file copy failed"; }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < FILE_READERS; t++) th.emplace_back(reader, t);
+  for (auto& x : th) x.join();
+  for (int t = 0; t < FILE_READERS; t++)
+    if (err[t]) return fail(err[t], "%s", msg[t].c_str());
+  e->stats.ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return MOX_OK;
+}
+
+}  // namespace mox_host
+
+// ============================================================== C ABI
+extern "C" {
+
+const char* mox_last_error(void) { return g_err.c_str(); }
+int mox_abi_version(void) { return MOX_ABI_VERSION; }
+
+int mox_set_flags(mox_engine* e, uint32_t flags) {
+  if (!e) return fail(MOX_EINVAL, "NULL engine");
+  e->flags = flags;
+  return MOX_OK;
+}
+
+int mox_engine_create(const mox_config* cfg, mox_engine** out) {
+  if (!out) return fail(MOX_EINVAL, "out is NULL");
+  *out = nullptr;
+  const uint32_t n = cfg ? cfg->n_gpus : 0;
+  if (n > MOX_MAX_GPUS) return fail(MOX_EINVAL, "n_gpus %u > %d", n, MOX_MAX_GPUS);
+  if (cfg && cfg->n_devices && cfg->n_devices != n) return fail(MOX_EINVAL, "n_devices %u != n_gpus %u", cfg->n_devices, n);
+  const int dev0 = cfg && cfg->n_devices ? cfg->devices[0] : (cfg ? cfg->device : -1);
+  mox_engine* e = nullptr;
+  if (int rc = engine_create_one(cfg, n > 1 && dev0 < 0 ? 0 : dev0, &e)) return rc;
+  if (n > 1) {  // engine group: this engine is member 0 (mox_multi.hip)
+    if (int rc = group_create(e, cfg)) {
+      const std::string msg = g_err;
+      mox_engine_destroy(e);
+      g_err = msg;
+      return rc;
+    }
+  }
+  *out = e;
+  return MOX_OK;
+}
+
 void mox_engine_destroy(mox_engine* e) {
   if (!e) return;
+  if (e->grp) group_destroy(e);  // the other members and the communicators
+  xplan_free(e);
+  bsort_free(e);
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
   for (auto& a : e->aslot) {
@@ -1287,6 +852,7 @@ void mox_engine_destroy(mox_engine* e) {
 int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
                         int at_corpus_end) {
   if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (e->grp) return fail(MOX_EINVAL, "engine group: one shard per GPU (mox_run_shards)");
   if (!d_buf && buf_len) return fail(MOX_EINVAL, "buffer is NULL");
   if (own_begin > own_end || own_end > buf_len) return fail(MOX_EINVAL, "bad own range [%zu, %zu) of %zu", own_begin, own_end, buf_len);
   if (own_begin > 0 && own_begin < 4) return fail(MOX_EINVAL, "own_begin must be 0 (corpus start) or >= 4 (left context)");
@@ -1337,6 +903,7 @@ int mox_run_wait(mox_engine* e) {
 
 int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end, int at_corpus_end) {
   if (!e) return fail(MOX_EINVAL, "engine is NULL");
+  if (e->grp) return fail(MOX_EINVAL, "engine group: one shard per GPU (mox_run_shards)");
   if (int rc = drain_async(e)) return rc;
   if (!d_buf && buf_len) return fail(MOX_EINVAL, "buffer is NULL");
   if (own_begin > own_end || own_end > buf_len) return fail(MOX_EINVAL, "bad own range [%zu, %zu) of %zu", own_begin, own_end, buf_len);
@@ -1356,6 +923,16 @@ int mox_fetch_table(mox_engine* e, mox_table** out) {
   if (int rc = drain_async(e)) return rc;
   if (!e->have_result) return fail(MOX_ESTATE, "no result: run first");
   HIPCHK(hipSetDevice(e->device));
+  // MOX_F_SORT_BYTES: bytewise order on the GPU (mox_bsort.hip) before the copy;
+  // a table too big for the sort's device scratch is sorted on the host below
+  bool host_sort = false;
+  if ((e->flags & MOX_F_SORT_BYTES) && !e->res.sorted) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = bsort_table(e);
+    if (rc == MOX_ENOMEM) host_sort = true;
+    else if (rc) return rc;
+    e->stats.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
   const bool timing = (e->flags & MOX_F_TIMING) != 0;
   if (timing) HIPCHK(hipEventRecord(e->ev[6], e->stream));
   const mox_engine::Res& r = e->res;
@@ -1382,7 +959,7 @@ int mox_fetch_table(mox_engine* e, mox_table** out) {
   if (timing) HIPCHK(hipEventRecord(e->ev[7], e->stream));
   HIPCHK(hipStreamSynchronize(e->stream));
   if (timing) e->stats.ms_d2h = ev_ms(e, 6, 7);
-  if (e->flags & MOX_F_SORT_BYTES) {
+  if (host_sort) {
     if (int rc = mox_table_sort_bytes(t)) {
       free(mem);
       return rc;
@@ -1412,106 +989,36 @@ int mox_get_stats(const mox_engine* e, mox_stats* out) {
   return MOX_OK;
 }
 
-static int stage_host(mox_engine* e, const uint8_t* text, size_t len) {
-  if (len > e->d_text_cap) {
-    dfree(e->d_text);
-    e->d_text = nullptr;
-    e->d_text_cap = 0;
-    int rc = dalloc(e, (void**)&e->d_text, len + 64);
-    if (rc) return rc;
-    e->d_text_cap = len;
-  }
-  const bool timing = (e->flags & MOX_F_TIMING) != 0;
-  if (timing) HIPCHK(hipEventRecord(e->ev[8], e->stream));
-  if (len) HIPCHK(hipMemcpyAsync(e->d_text, text, len, hipMemcpyHostToDevice, e->stream));
-  if (timing) HIPCHK(hipEventRecord(e->ev[9], e->stream));
-  HIPCHK(hipStreamSynchronize(e->stream));
-  if (timing) e->stats.ms_h2d = ev_ms(e, 8, 9);
-  return MOX_OK;
-}
-
 int mox_count(mox_engine* e, const uint8_t* text, size_t len, mox_table** out) {
   if (!e || !out || (!text && len)) return fail(MOX_EINVAL, "NULL argument");
   *out = nullptr;
   HIPCHK(hipSetDevice(e->device));
   if (int rc = drain_async(e)) return rc;
-  int rc = stage_host(e, text, len);
+  if (e->grp) {  // engine group: byte ranges at whitespace, one per GPU (mox_multi.hip)
+    if (int rc = group_count_host(e, text, len)) return rc;
+    return mox_fetch_table(e, out);
+  }
+  int rc = stage_host_range(e, text, len);
   if (rc) return rc;
   if ((rc = mox_run_range(e, len ? (const void*)e->d_text : nullptr, len, 0, len, 1))) return rc;
   return mox_fetch_table(e, out);
 }
-
-// File -> HBM (SURVEY §8(f) rank 2): FILE_READERS threads each pread their
-// chunks (c = t, t + FILE_READERS, ...) into two pinned buffers of their own and
-// copy them with hipMemcpyAsync on a stream of their own, so the page-cache /
-// disk reads of one chunk overlap the PCIe copies of the others.  Pinned
-// buffers and streams are engine-owned and reused across calls.
-namespace {
-constexpr int FILE_READERS = 8;
-constexpr size_t FILE_CHUNK = 32u << 20;
-int stage_file(mox_engine* e, int fd, size_t len) {
-  if (len > e->d_text_cap) {
-    dfree(e->d_text);
-    e->d_text = nullptr;
-    e->d_text_cap = 0;
-    int rc = dalloc(e, (void**)&e->d_text, len + 64);
-    if (rc) return rc;
-    e->d_text_cap = len;
-  }
-  for (int t = 0; t < FILE_READERS; t++) {
-    if (!e->file_stream[t]) HIPCHK(hipStreamCreateWithFlags(&e->file_stream[t], hipStreamNonBlocking));
-    for (int k = 0; k < 2; k++)
-      if (!e->file_pin[t][k]) HIPCHK(hipHostMalloc((void**)&e->file_pin[t][k], FILE_CHUNK, hipHostMallocDefault));
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  const size_t nchunks = (len + FILE_CHUNK - 1) / FILE_CHUNK;
-  std::vector<int> err(FILE_READERS, 0);
-  std::vector<std::string> msg(FILE_READERS);
-  auto reader = [&](int t) {
-    (void)hipSetDevice(e->device);
-    int k = 0;
-    size_t pending = 0;  // copies in flight on this reader's stream
-    for (size_t c = t; c < nchunks; c += FILE_READERS, k ^= 1) {
-      if (pending == 2) {  // the buffer about to be refilled was copied two chunks ago
-        if (hipStreamSynchronize(e->file_stream[t]) != hipSuccess) { err[t] = MOX_EHIP; msg[t] = "file copy failed"; return; }
-        pending = 0;
-      }
-      const size_t off = c * FILE_CHUNK, n = std::min(FILE_CHUNK, len - off);
-      size_t got = 0;
-      while (got < n) {
-        const ssize_t r = pread(fd, e->file_pin[t][k] + got, n - got, (off_t)(off + got));
-        if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) { err[t] = MOX_EIO; msg[t] = std::string("read failed: ") + (r < 0 ? strerror(errno) : "short file"); return; }
-        got += (size_t)r;
-      }
-      if (hipMemcpyAsync(e->d_text + off, e->file_pin[t][k], n, hipMemcpyHostToDevice, e->file_stream[t]) != hipSuccess) {
-        err[t] = MOX_EHIP; msg[t] = "hipMemcpyAsync failed"; return;
-      }
-      pending++;
-    }
-    if (hipStreamSynchronize(e->file_stream[t]) != hipSuccess) { err[t] = MOX_EHIP; msg[t] = "file copy failed"; }
-  };
-  std::vector<std::thread> th;
-  for (int t = 0; t < FILE_READERS; t++) th.emplace_back(reader, t);
-  for (auto& x : th) x.join();
-  for (int t = 0; t < FILE_READERS; t++)
-    if (err[t]) return fail(err[t], "%s", msg[t].c_str());
-  e->stats.ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-  return MOX_OK;
-}
-}  // namespace
 
 int mox_count_file(mox_engine* e, const char* path, mox_table** out) {
   if (!e || !path || !out) return fail(MOX_EINVAL, "NULL argument");
   *out = nullptr;
   HIPCHK(hipSetDevice(e->device));
   if (int rc = drain_async(e)) return rc;
+  if (e->grp) {  // engine group: every GPU reads its own byte range of the file
+    if (int rc = group_count_file(e, path)) return rc;
+    return mox_fetch_table(e, out);
+  }
   int fd = open(path, O_RDONLY);
   if (fd < 0) return fail(MOX_EIO, "cannot open %s: %s", path, strerror(errno));
   struct stat st;
   if (fstat(fd, &st) != 0) { close(fd); return fail(MOX_EIO, "cannot stat %s: %s", path, strerror(errno)); }
   const size_t len = (size_t)st.st_size;
-  int rc = stage_file(e, fd, len);
+  int rc = stage_file_range(e, fd, 0, len);
   close(fd);
   if (rc) return rc;
   const double h2d = e->stats.ms_h2d;
@@ -1590,62 +1097,6 @@ int mox_print_top_words(const mox_table* t, size_t n) {
            (unsigned long long)t->counts[j]);
   }
   return MOX_OK;
-}
-
-// ---- multi-GPU ----
-int mox_comm_unique_id(uint8_t id[MOX_UNIQUE_ID_BYTES]) {
-  if (!id) return fail(MOX_EINVAL, "NULL argument");
-  static_assert(sizeof(ncclUniqueId) <= MOX_UNIQUE_ID_BYTES, "unique id size");
-  ncclUniqueId u;
-  RCCLCHK(ncclGetUniqueId(&u));
-  memset(id, 0, MOX_UNIQUE_ID_BYTES);
-  memcpy(id, &u, sizeof u);
-  return MOX_OK;
-}
-
-int mox_comm_init(mox_engine* e, int nranks, int rank, const uint8_t id[MOX_UNIQUE_ID_BYTES]) {
-  if (!e || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad communicator arguments");
-  HIPCHK(hipSetDevice(e->device));
-  if (e->comm) { ncclCommDestroy(e->comm); e->comm = nullptr; }
-  ncclUniqueId u;
-  memcpy(&u, id, sizeof u);
-  RCCLCHK(ncclCommInitRank(&e->comm, nranks, u, rank));
-  e->nranks = nranks;
-  e->rank = rank;
-  return MOX_OK;
-}
-
-int mox_exchange(mox_engine* e) {
-  if (!e) return fail(MOX_EINVAL, "engine is NULL");
-  if (!e->comm) return fail(MOX_ESTATE, "mox_comm_init first");
-  RcclTransport t(e);
-  return exchange_impl(e, e->nranks, e->rank, t);
-}
-
-int mox_exchange_host(mox_engine* e, int nranks, int rank, mox_alltoallv_fn fn, void* user) {
-  if (!e || !fn) return fail(MOX_EINVAL, "NULL argument");
-  if (nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad rank %d of %d", rank, nranks);
-  HostTransport t(e, nranks, fn, user);
-  return exchange_impl(e, nranks, rank, t);
-}
-
-int mox_gather(mox_engine* e, int root) {
-  if (!e) return fail(MOX_EINVAL, "engine is NULL");
-  if (!e->comm) return fail(MOX_ESTATE, "mox_comm_init first");
-  RcclTransport t(e);
-  return gather_impl(e, e->nranks, e->rank, root, t);
-}
-
-int mox_gather_host(mox_engine* e, int nranks, int rank, int root, mox_alltoallv_fn fn, void* user) {
-  if (!e || !fn) return fail(MOX_EINVAL, "NULL argument");
-  if (nranks < 1 || nranks > MAX_RANKS || rank < 0 || rank >= nranks) return fail(MOX_EINVAL, "bad rank %d of %d", rank, nranks);
-  HostTransport t(e, nranks, fn, user);
-  return gather_impl(e, nranks, rank, root, t);
-}
-
-int mox_reduce_pairs(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n) {
-  if (!e || (n && (!bytes || !offs || !counts))) return fail(MOX_EINVAL, "NULL argument");
-  return reduce_pairs_impl(e, bytes, offs, counts, n);
 }
 
 }  // extern "C"

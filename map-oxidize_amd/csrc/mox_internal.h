@@ -154,7 +154,72 @@ struct Ctl {
   unsigned long long short_bytes; // table bytes of the short words (long words follow)
   unsigned long long n_mid;       // entries of mid_units (k_reduce_sort2 work list)
   unsigned long long n_small;     // entries of small_units (k_reduce_small work list)
+  unsigned long long paths[8];    // PATH_* hit counters (MOX_PATHS builds only; zero otherwise)
 };
+
+// ---- forced-collision check build (libmox_hc.so, `make hc`)
+// -DMOX_HASH_COLLIDE truncates every key hash to a few bits, so that distinct
+// words share hashes and each exactness fallback that resolves a collision by
+// comparing key bytes actually runs: the 32-bit key hash (partitions,
+// dictionary, reduce tables) keeps MOX_H32_BITS bits, the order hash hash32b
+// MOX_H32B_BITS bits, the long-word FNV-1a-64 MOX_FNV_BITS bits.  The kept
+// value is multiplied by an odd constant (a bijection), so collisions stay
+// exactly as frequent while every bit position still varies (partition bits,
+// dictionary slots, sub-bucket bits).  Production builds use the full hashes.
+#ifdef MOX_HASH_COLLIDE
+#ifndef MOX_H32_BITS
+#define MOX_H32_BITS 22
+#endif
+#ifndef MOX_H32B_BITS
+#define MOX_H32B_BITS 2
+#endif
+#ifndef MOX_FNV_BITS
+#define MOX_FNV_BITS 8
+#endif
+#ifndef MOX_PATHS
+#define MOX_PATHS 1
+#endif
+#else
+#define MOX_H32_BITS 32   // unused: collide32 / fnv_finish are the identity
+#define MOX_H32B_BITS 32
+#endif
+__host__ __device__ __forceinline__ uint32_t collide32(uint32_t h, int bits) {
+#ifdef MOX_HASH_COLLIDE
+  if (bits >= 32) return h;
+  return (h & ((1u << bits) - 1u)) * 0x9E3779B1u;
+#else
+  (void)bits;
+  return h;
+#endif
+}
+// Finish of the long-word FNV-1a-64 (host and device): identity in production.
+__host__ __device__ __forceinline__ uint64_t fnv_finish(uint64_t h) {
+#ifdef MOX_HASH_COLLIDE
+  if (MOX_FNV_BITS >= 64) return h;
+  return (h & ((1ull << (MOX_FNV_BITS & 63)) - 1ull)) * 0x9E3779B97F4A7C15ull;
+#else
+  return h;
+#endif
+}
+// Exactness-fallback hit counters (Ctl::paths, reported as mox_stats.path_hits):
+// compiled in with -DMOX_PATHS (the collision build), so tests can assert that
+// the path they target ran.
+enum : uint32_t {
+  PATH_DICT_TAG = 0,      // k_map pass B: dictionary tag equal, key different -> full dictionary search
+  PATH_LONG_EQHASH = 1,   // long-word table: equal FNV hash, different bytes -> probe on
+  PATH_SORT_RESORT = 2,   // k_reduce_sort1/2: two keys share the 23-bit sort key -> 64-bit re-sort
+  PATH_SORT_TO_RED = 3,   // k_reduce_sort1/2: two keys share (h32, hash32b) -> unit goes to k_reduce
+  PATH_RED_TAG = 4,       // k_reduce: table tag equal, key different
+  PATH_SMALL_TAG = 5,     // k_reduce_small: hash equal, key different
+  PATH_N = 8
+};
+#if defined(MOX_PATHS) && MOX_PATHS
+#define MOX_PATH(ctlp, i) atomicAdd(&(ctlp)->paths[(i)], 1ull)
+#define MOX_PATH_ADD(ctlp, i, n) atomicAdd(&(ctlp)->paths[(i)], (unsigned long long)(n))
+#else
+#define MOX_PATH(ctlp, i) ((void)0)
+#define MOX_PATH_ADD(ctlp, i, n) ((void)0)
+#endif
 
 #ifdef MOX_CHECK
 __device__ __forceinline__ bool chk_record(Ctl* ctl, bool ok, uint32_t site) {

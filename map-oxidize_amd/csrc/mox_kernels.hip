@@ -170,41 +170,73 @@ __device__ bool long_equal(const uint8_t* base, const uint8_t* arena, uint64_t r
 }
 // Exact insert into the long-word table; every access is an atomic (memory-side,
 // coherent across XCDs).  Keys: (hash, len) + byte compare on hash equality.
+// A wave-level loop (as cold_pair's): every lane takes one probe step per
+// iteration and the body ends in a wave barrier, so a lane that claims a slot
+// publishes it inside that iteration.  In a lane-level loop the compiler may
+// sink the claimant's publication (code reached only on the exit path) past the
+// loop exit, where it waits for lanes of its own wave that spin on that very
+// publication: the forced-collision build (-DMOX_HASH_COLLIDE) lost the counts
+// of repeated long words that way.
 template <class W>  // Work, or the kernarg-segment Work of k_map's rare paths
 __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_t ref, uint64_t len, uint64_t cnt) {
   h |= 1;
-  uint64_t mask = w.long_cap - 1, slot = h & mask;
-  uint32_t spins = 0;
-  for (uint64_t probes = 0; probes <= mask; ) {
-    if (++spins > (1u << 24)) { atomicOr(&w.ctl->overflow, OVF_PROBE); return; }
-    LSlot* s = &w.ltab[slot];
-    unsigned long long cur = atomicCAS(&s->h, 0ull, (unsigned long long)h);
-    if (cur == 0) {
-      // publish len before ref: memory-side atomics to different words complete
-      // in any order, so the fence (s_waitcnt vmcnt(0)) orders them
-      atomicExch(&s->len, (unsigned long long)len);
-      __threadfence();
-      atomicExch(&s->ref, (unsigned long long)(ref + 1));
-      atomicAdd(&s->count, (unsigned long long)cnt);
-      atomicAdd(&w.ctl->long_uniq, 1ull);
-      return;
-    }
-    if (cur == h) {
-      unsigned long long r = atomicAdd(&s->ref, 0ull);
-      if (r == 0) continue;  // claimant still publishing: retry this slot
-      // acquire: the claimant's arena bytes (written before its release fence,
-      // possibly from another XCD's L2) must be seen before they are compared
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);
-      unsigned long long l = atomicAdd(&s->len, 0ull);
-      if (l == len && long_equal(base, w.arena, r - 1, ref, len)) {
-        atomicAdd(&s->count, (unsigned long long)cnt);
-        return;
+  const uint64_t mask = w.long_cap - 1;
+  uint64_t slot = h & mask, probes = 0;
+  uint32_t spins = 0, eqh = 0;
+  bool done = false;
+  do {
+    if (!done) {
+      if (++spins > (1u << 24)) {
+        atomicOr(&w.ctl->overflow, OVF_PROBE);
+        done = true;
+      } else {
+        LSlot* s = &w.ltab[slot];
+        const unsigned long long cur = atomicCAS(&s->h, 0ull, (unsigned long long)h);
+        bool next = false;
+        if (cur == 0) {
+          // publish len before ref: memory-side atomics to different words complete
+          // in any order, so the fence (s_waitcnt vmcnt(0)) orders them
+          atomicExch(&s->len, (unsigned long long)len);
+          __threadfence();
+          atomicExch(&s->ref, (unsigned long long)(ref + 1));
+          atomicAdd(&s->count, (unsigned long long)cnt);
+          atomicAdd(&w.ctl->long_uniq, 1ull);
+          done = true;
+        } else if (cur == h) {
+          const unsigned long long r = atomicAdd(&s->ref, 0ull);
+          if (r != 0) {  // (0: the claimant is still publishing -- this slot again next iteration)
+            // acquire: the claimant's arena bytes (written before its release fence,
+            // possibly from another XCD's L2) must be seen before they are compared
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            const unsigned long long l = atomicAdd(&s->len, 0ull);
+            if (l == len && long_equal(base, w.arena, r - 1, ref, len)) {
+              atomicAdd(&s->count, (unsigned long long)cnt);
+              done = true;
+            } else {
+              eqh++;  // same hash, another word: probe on
+              next = true;
+            }
+          }
+        } else {
+          next = true;
+        }
+        if (next) {
+          slot = (slot + 1) & mask;
+          if (++probes > mask) {
+            atomicOr(&w.ctl->overflow, OVF_LONG);
+            done = true;
+          }
+        }
       }
     }
-    slot = (slot + 1) & mask;
-    probes++;
-  }
-  atomicOr(&w.ctl->overflow, OVF_LONG);
+    __builtin_amdgcn_wave_barrier();
+  } while (__any(!done));
+  // the path counter is added once, after the loop: an atomic on it inside the
+  // loop next to the slot-count add (both "+1" in k_unicode) was merged by the
+  // compiler (ROCm 7.2) into one atomic whose address lost the slot-count case
+  // -- repeated long words' counts went to the counter
+  if (eqh) MOX_PATH_ADD(w.ctl, PATH_LONG_EQHASH, eqh);
+  (void)eqh;
 }
 
 // ------------------------------------------------------------------ map kernel
@@ -219,7 +251,9 @@ __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2
   a ^= a >> 15;
   a *= 0x85EBCA6Bu;
   a ^= a >> 13;
-  return a;
+  // never 0: 0 marks a free slot in the dictionary and k_reduce tag arrays (a
+  // key hashing to 0 would spin on a "free" slot); 1 simply shares its hash
+  return max(collide32(a, MOX_H32_BITS), 1u);  // collide32: identity except in the collision build
 }
 __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   return hash32((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
@@ -425,6 +459,7 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
   }
   uint64_t h = FNV0;
   for (uint64_t i = 0; i < len; i++) h = fnv_step(h, ascii_lower(c.base[p + i]));
+  h = fnv_finish(h);
   atomicAdd(&rare(m).ctl->long_n, 1ull);
   long_insert(rare(m), c.base, h, p, len, 1);
 }
@@ -655,6 +690,7 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
       continue;
     }
     if (slot[u] >= 0) {  // tag matched another word: full search (rare)
+      MOX_PATH(rare(m).ctl, PATH_DICT_TAG);
       const int s2 = dict_find(m.s, h[u], w0, w1);
       if (s2 >= 0) { atomicAdd(&m.s.dcnt[s2], 1u); continue; }
     }
@@ -1485,6 +1521,7 @@ extern "C" __global__ void k_unicode(Corpus c, Work w, Tables T) {
     } else {
       uint64_t h = FNV0;
       for (uint64_t k = 0; k < o; k++) h = fnv_step(h, out[k]);
+      h = fnv_finish(h);
       atomicAdd(&w.ctl->long_n, 1ull);
       long_insert(w, c.base, h, ARENA_BIT | ao, o, 1);
     }
@@ -1626,6 +1663,7 @@ struct RedLds {
   uint16_t* fill;          // RED_SORTB: bin fill cursors
   uint32_t* misc;          // [0] uniques [1] overflow [2] compaction cursor
   uint32_t* dbg;           // DBG_COUNT: [0] slow inserts [1] slow iterations [2] publication retries
+  Ctl* ctl;                // path counters (MOX_PATHS builds)
   bool plain;
 };
 
@@ -1644,41 +1682,59 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   uint32_t b = red_bucket(h);
   if (s.dbg) atomicAdd(&s.dbg[0], 1u);
   const uint32_t* tags = reinterpret_cast<const uint32_t*>(s.tag4);
-  for (uint32_t it = 0; it < 64u * RED_BK;) {
-    const uint4 t = s.tag4[b];
-    const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
-    bool retry = false;
+  uint32_t it = 0;
+  bool done = false;
+  // wave-level loop (see long_insert): a lane that claims a slot stores the key
+  // and publishes its count inside the iteration, never past the loop exit
+  do {
+    if (!done) {
+      const uint4 t = s.tag4[b];
+      const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
+      bool retry = false;
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      if (tv[i] != h) continue;
-      const uint32_t sl = 4 * b + i;
-      if (__hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) { retry = true; break; }
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      if (key_eq16(s.key[sl], k)) { atomicAdd(&s.cnt[sl], (unsigned long long)c); return; }
-    }
-    if (s.dbg) atomicAdd(&s.dbg[1], 1u);
-    if (retry) { if (s.dbg) atomicAdd(&s.dbg[2], 1u); it++; continue; }
-    int e = -1;
-#pragma unroll
-    for (int i = 3; i >= 0; i--) if (tv[i] == 0) e = i;
-    if (e >= 0) {
-      const uint32_t sl = 4 * b + e;
-      if (atomicCAS(const_cast<uint32_t*>(&tags[sl]), 0u, h) == 0u) {
-        s.key[sl] = k;
+      for (int i = 0; i < 4; i++) {
+        if (done || retry || tv[i] != h) continue;
+        const uint32_t sl = 4 * b + i;
+        if (__hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0) { retry = true; continue; }
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-        atomicAdd(&s.cnt[sl], (unsigned long long)c);
-        const uint32_t u = atomicAdd(&s.misc[0], 1u);
-        if (u >= RED_CAP) s.misc[1] = 1;
-        return;
+        if (key_eq16(s.key[sl], k)) {
+          atomicAdd(&s.cnt[sl], (unsigned long long)c);
+          done = true;
+        } else {
+          MOX_PATH(s.ctl, PATH_RED_TAG);  // same tag, another key
+        }
       }
-      it++;
-      continue;  // lost the slot: re-read this bucket
+      if (!done) {
+        if (s.dbg) atomicAdd(&s.dbg[1], 1u);
+        if (retry) {
+          if (s.dbg) atomicAdd(&s.dbg[2], 1u);
+        } else {
+          int e = -1;
+#pragma unroll
+          for (int i = 3; i >= 0; i--) if (tv[i] == 0) e = i;
+          if (e >= 0) {
+            const uint32_t sl = 4 * b + e;
+            if (atomicCAS(const_cast<uint32_t*>(&tags[sl]), 0u, h) == 0u) {
+              s.key[sl] = k;
+              __atomic_signal_fence(__ATOMIC_SEQ_CST);
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+              atomicAdd(&s.cnt[sl], (unsigned long long)c);
+              const uint32_t u = atomicAdd(&s.misc[0], 1u);
+              if (u >= RED_CAP) s.misc[1] = 1;
+              done = true;
+            }  // lost the slot: re-read this bucket
+          } else {
+            b = b + 1 == RED_BK ? 0 : b + 1;
+          }
+        }
+        if (!done && ++it >= 64u * RED_BK) {
+          s.misc[1] = 1;
+          done = true;
+        }
+      }
     }
-    b = b + 1 == RED_BK ? 0 : b + 1;
-    it++;
-  }
-  s.misc[1] = 1;
+    __builtin_amdgcn_wave_barrier();
+  } while (__any(!done));
 }
 
 // Fast path for records whose key is already published in its home bucket or
@@ -1714,7 +1770,7 @@ __device__ __forceinline__ uint32_t hash32b(uint32_t k0, uint32_t k1, uint32_t k
   a ^= a >> 12;
   a *= 0x297A2D39u;
   a ^= a >> 15;
-  return a;
+  return collide32(a, MOX_H32B_BITS);  // identity except in the collision build
 }
 __device__ __forceinline__ bool key_less(uint32_t ha, uint4 ka, uint32_t hb, uint4 kb) {
   if (ha != hb) return ha < hb;
@@ -2075,6 +2131,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   __shared__ uint32_t s_unit;
   s.dbg = MOX_ABL(w.dbg, DBG_COUNT) ? dbgc : nullptr;
   s.plain = MOX_ABL(w.dbg, DBG_RED_PLAINADD) != 0;
+  s.ctl = w.ctl;
   if (threadIdx.x < 4) dbgc[threadIdx.x] = 0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NWV = RED_THREADS / 64;
@@ -2491,6 +2548,7 @@ extern "C" __global__ __launch_bounds__(SR_THREADS, 4) void k_reduce_small(Work 
                 atomicAdd(&acc[cur], acc[i]);
                 placed = true;
               } else {
+                if (hh[cur] == hj) MOX_PATH(w.ctl, PATH_SMALL_TAG);  // same hash, another key
                 sl = (sl + 1) & (SR_TSLOTS - 1);
               }
             }
@@ -2764,6 +2822,7 @@ __device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, cons
     }
   }
   if (__any(bad != 0)) {
+    if (lane == 0) MOX_PATH(w.ctl, PATH_SORT_RESORT);
     // two different keys share the sort-key hash bits (~0.5 % of C4's units):
     // sort again on 64-bit keys -- the h32 bits below the unit, all of
     // hash32b, the index -- which is key_less order whenever (h32, hash32b)
@@ -2793,6 +2852,7 @@ __device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, cons
   }
   if (__any(bad != 0)) {  // (h32, hash32b) shared by two keys: k_reduce resolves this unit
     if (lane == 0) {
+      MOX_PATH(w.ctl, PATH_SORT_TO_RED);
       const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
       if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
     }

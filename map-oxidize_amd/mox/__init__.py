@@ -46,6 +46,11 @@ class Utf8Error(MoxError):
     """Input is not valid UTF-8 (reference: tokio lines() -> InvalidData)."""
 
 
+MAX_GPUS = 16
+XPORT_RCCL = 0  # engine group: RCCL communicators over xGMI
+XPORT_COPY = 1  # engine group: device-to-device copies (members may share a GPU)
+
+
 class Config(ctypes.Structure):
     _fields_ = [
         ("device", ctypes.c_int),
@@ -53,7 +58,21 @@ class Config(ctypes.Structure):
         ("dict_words", ctypes.c_uint32),
         ("sample_pieces", ctypes.c_uint32),
         ("reserve_bytes", ctypes.c_uint64),
-        ("reserved", ctypes.c_uint32 * 8),
+        ("n_gpus", ctypes.c_uint32),
+        ("transport", ctypes.c_uint32),
+        ("n_devices", ctypes.c_uint32),
+        ("devices", ctypes.c_int32 * MAX_GPUS),
+        ("reserved", ctypes.c_uint32 * 5),
+    ]
+
+
+class Shard(ctypes.Structure):
+    _fields_ = [
+        ("d_buf", ctypes.c_void_p),
+        ("buf_len", ctypes.c_size_t),
+        ("own_begin", ctypes.c_size_t),
+        ("own_end", ctypes.c_size_t),
+        ("at_corpus_end", ctypes.c_int),
     ]
 
 
@@ -96,24 +115,38 @@ class Stats(ctypes.Structure):
         ("x_bytes_recv", ctypes.c_uint64),
         ("gather_bytes", ctypes.c_uint64),
         ("ms_gather", ctypes.c_double),
+        ("path_hits", ctypes.c_uint64 * 8),
+        ("ms_sort", ctypes.c_double),
+        ("ms_local", ctypes.c_double),
+        ("n_gpus", ctypes.c_uint32),
+        ("async_dropped", ctypes.c_uint32),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        d["path_hits"] = [int(x) for x in self.path_hits]
+        return d
 
 
 # int (*)(void* user, const void* send, const uint64_t* send_bytes, void* recv, const uint64_t* recv_bytes)
 _A2A_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
 
-_lib = None
+# exactness-fallback counters (mox_stats.path_hits; collision check build only)
+PATH_DICT_TAG, PATH_LONG_EQHASH, PATH_SORT_RESORT, PATH_SORT_TO_RED, PATH_RED_TAG, PATH_SMALL_TAG = range(6)
+HC_LIB_PATH = os.path.join(_HERE, "libmox_hc.so")  # forced-collision check build (Makefile `hc`)
+CHECK_LIB_PATH = os.path.join(_HERE, "libmox_check.so")  # bounds-check build (Makefile `check`)
+
+_libs = {}
 
 
-def lib():
-    """Load libmox.so (fails loudly: there is no fallback path)."""
-    global _lib
-    if _lib is None:
+def lib(path=None):
+    """Load libmox.so, or the library at ``path`` (a check build), once per path.
+    Fails loudly: there is no fallback path."""
+    if path is None:
         path = os.environ.get("MOX_LIB", LIB_PATH)  # diagnostics builds only (tools/)
+    _lib = _libs.get(path)
+    if _lib is None:
         if not os.path.exists(path):
             raise MoxError(MOX_ESTATE, "%s not built (run `make` or __graft_entry__.build())" % path)
         L = ctypes.CDLL(path)
@@ -149,18 +182,21 @@ def lib():
             "mox_write_final_result": ([P(_Table), ctypes.c_char_p], I),
             "mox_print_top_words": ([P(_Table), sz], I),
             "mox_reduce_pairs": ([VP, VP, VP, VP, U64], I),
+            "mox_run_shards": ([VP, P(Shard)], I),
+            "mox_group_size": ([VP], I),
+            "mox_group_member": ([VP, I], VP),
         }
         for name, (args, res) in sig.items():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
-        _lib = L
+        _lib = _libs[path] = L
     return _lib
 
 
-def _check(rc):
+def _check(rc, L=None):
     if rc != MOX_OK:
-        msg = lib().mox_last_error().decode("utf-8", "replace")
+        msg = (L or lib()).mox_last_error().decode("utf-8", "replace")
         if rc == MOX_EUTF8:
             raise Utf8Error(rc, msg)
         raise MoxError(rc, msg)
@@ -169,11 +205,15 @@ def _check(rc):
 class Table:
     """Owning wrapper of a mox_table (words are bytes, counts are ints)."""
 
-    def __init__(self, ptr):
+    def __init__(self, ptr, L=None):
+        self._L = L or lib()
         self._p = ptr
         t = ptr.contents
         self.n = int(t.n)
         self.tokens = int(t.tokens)
+
+    def _c(self, rc):
+        _check(rc, self._L)
 
     def _raw(self):
         import numpy as np
@@ -205,15 +245,15 @@ class Table:
 
     def sort_bytes(self):
         """Reorder this table bytewise ascending in place (mox_table_sort_bytes)."""
-        _check(lib().mox_table_sort_bytes(self._p))
+        self._c(self._L.mox_table_sort_bytes(self._p))
         return self
 
     def write_final_result(self, path):
-        _check(lib().mox_write_final_result(self._p, path.encode()))
+        self._c(self._L.mox_write_final_result(self._p, path.encode()))
 
     def close(self):
         if self._p is not None:
-            lib().mox_table_free(self._p)
+            self._L.mox_table_free(self._p)
             self._p = None
 
     def __del__(self):
@@ -224,54 +264,91 @@ class Table:
 
 
 class Engine:
-    def __init__(self, device=-1, flags=0, dict_words=0, sample_pieces=0, reserve_bytes=0):
+    def __init__(self, device=-1, flags=0, dict_words=0, sample_pieces=0, reserve_bytes=0, lib_path=None,
+                 n_gpus=0, transport=XPORT_RCCL, devices=None, _handle=None):
+        """lib_path: a check build instead of libmox.so (CHECK_LIB_PATH, HC_LIB_PATH).
+        n_gpus > 1: an engine group (include/mox.h) on ``devices`` (default 0..n_gpus-1)
+        over ``transport``."""
+        self._L = lib(lib_path)
+        self._borrowed = _handle is not None
+        if _handle is not None:  # a group member's engine: owned by the group
+            self._h = ctypes.c_void_p(_handle)
+            return
         cfg = Config()
         cfg.device = device
         cfg.flags = flags
         cfg.dict_words = dict_words
         cfg.sample_pieces = sample_pieces
         cfg.reserve_bytes = reserve_bytes
+        cfg.n_gpus = n_gpus
+        cfg.transport = transport
+        if devices is not None:
+            cfg.n_devices = len(devices)
+            for i, d in enumerate(devices):
+                cfg.devices[i] = d
         h = ctypes.c_void_p()
-        _check(lib().mox_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._c(self._L.mox_engine_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
 
+    # -- engine group (mox_config.n_gpus > 1)
+    def group_size(self):
+        return int(self._L.mox_group_size(self._h))
+
+    def member(self, i):
+        """Member i's engine (device allocations / copies for its shard)."""
+        h = self._L.mox_group_member(self._h, i)
+        if not h:
+            raise MoxError(MOX_EINVAL, "no group member %d" % i)
+        return Engine(lib_path=self._L._name, _handle=h)
+
+    def run_shards(self, shards):
+        """One group call over device-resident shards: [(d_ptr, buf_len, own_begin, own_end, at_end)]
+        per member (mox_run_shards)."""
+        arr = (Shard * len(shards))()
+        for i, (d, n, a, b, end) in enumerate(shards):
+            arr[i] = Shard(ctypes.c_void_p(d), n, a, b, 1 if end else 0)
+        self._c(self._L.mox_run_shards(self._h, arr))
+
+    def _c(self, rc):
+        _check(rc, self._L)
+
     def set_flags(self, flags):
-        _check(lib().mox_set_flags(self._h, flags))
+        self._c(self._L.mox_set_flags(self._h, flags))
 
     # -- drop-in for main.rs:16-22
     def count(self, data):
         buf = bytes(data)
         t = ctypes.POINTER(_Table)()
-        _check(lib().mox_count(self._h, buf, len(buf), ctypes.byref(t)))
-        return Table(t)
+        self._c(self._L.mox_count(self._h, buf, len(buf), ctypes.byref(t)))
+        return Table(t, self._L)
 
     def count_file(self, path):
         t = ctypes.POINTER(_Table)()
-        _check(lib().mox_count_file(self._h, os.fsencode(path), ctypes.byref(t)))
-        return Table(t)
+        self._c(self._L.mox_count_file(self._h, os.fsencode(path), ctypes.byref(t)))
+        return Table(t, self._L)
 
     # -- device-resident path
     def run_device(self, d_ptr, n):
-        _check(lib().mox_run_device(self._h, ctypes.c_void_p(d_ptr), n))
+        self._c(self._L.mox_run_device(self._h, ctypes.c_void_p(d_ptr), n))
 
     def run_range(self, d_ptr, buf_len, own_begin, own_end, at_end):
-        _check(lib().mox_run_range(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
+        self._c(self._L.mox_run_range(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
 
     def run_range_async(self, d_ptr, buf_len, own_begin, own_end, at_end):
         """Enqueue a pass; completes the previously enqueued one (include/mox.h)."""
-        _check(lib().mox_run_range_async(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
+        self._c(self._L.mox_run_range_async(self._h, ctypes.c_void_p(d_ptr), buf_len, own_begin, own_end, 1 if at_end else 0))
 
     def run_wait(self):
-        _check(lib().mox_run_wait(self._h))
+        self._c(self._L.mox_run_wait(self._h))
 
     def fetch(self):
         t = ctypes.POINTER(_Table)()
-        _check(lib().mox_fetch_table(self._h, ctypes.byref(t)))
-        return Table(t)
+        self._c(self._L.mox_fetch_table(self._h, ctypes.byref(t)))
+        return Table(t, self._L)
 
     def stats(self):
         s = Stats()
-        _check(lib().mox_get_stats(self._h, ctypes.byref(s)))
+        self._c(self._L.mox_get_stats(self._h, ctypes.byref(s)))
         return s.as_dict()
 
     def ms_map(self):
@@ -279,16 +356,16 @@ class Engine:
         if not hasattr(self, "_st"):
             self._st = Stats()
             self._st_ref = ctypes.byref(self._st)
-        _check(lib().mox_get_stats(self._h, self._st_ref))
+        self._c(self._L.mox_get_stats(self._h, self._st_ref))
         return self._st.ms_map
 
     def alloc(self, nbytes):
         p = ctypes.c_void_p()
-        _check(lib().mox_device_alloc(self._h, nbytes, ctypes.byref(p)))
+        self._c(self._L.mox_device_alloc(self._h, nbytes, ctypes.byref(p)))
         return p.value
 
     def free(self, d_ptr):
-        _check(lib().mox_device_free(self._h, ctypes.c_void_p(d_ptr)))
+        self._c(self._L.mox_device_free(self._h, ctypes.c_void_p(d_ptr)))
 
     def h2d(self, d_ptr, host_buf, nbytes=None):
         if nbytes is None:
@@ -296,32 +373,32 @@ class Engine:
         src = ctypes.c_char_p(host_buf) if isinstance(host_buf, bytes) else host_buf
         if hasattr(host_buf, "ctypes"):
             src = ctypes.c_void_p(host_buf.ctypes.data)
-        _check(lib().mox_memcpy_h2d(self._h, ctypes.c_void_p(d_ptr), src, nbytes))
+        self._c(self._L.mox_memcpy_h2d(self._h, ctypes.c_void_p(d_ptr), src, nbytes))
 
     def synchronize(self):
-        _check(lib().mox_synchronize(self._h))
+        self._c(self._L.mox_synchronize(self._h))
 
     # -- multi-GPU
     def comm_init(self, nranks, rank, uid):
-        _check(lib().mox_comm_init(self._h, nranks, rank, uid))
+        self._c(self._L.mox_comm_init(self._h, nranks, rank, uid))
 
     def exchange(self):
         """RCCL all-to-all exchange + final reduce (after run_range on every rank)."""
-        _check(lib().mox_exchange(self._h))
+        self._c(self._L.mox_exchange(self._h))
 
     def exchange_host(self, nranks, rank, alltoallv):
         """The same exchange over a host transport.  ``alltoallv(send, send_sizes,
         recv_sizes)`` gets the send bytes (memoryview, blocks for ranks 0..n-1)
         and must return the received bytes (blocks from ranks 0..n-1)."""
-        self._host_call(lambda fn: lib().mox_exchange_host(self._h, nranks, rank, fn, None), nranks, alltoallv)
+        self._host_call(lambda fn: self._L.mox_exchange_host(self._h, nranks, rank, fn, None), nranks, alltoallv)
 
     def gather(self, root=0):
         """Gather every rank's final table into root's engine over RCCL (mox_gather)."""
-        _check(lib().mox_gather(self._h, root))
+        self._c(self._L.mox_gather(self._h, root))
 
     def gather_host(self, nranks, rank, alltoallv, root=0):
         """mox_gather over a host transport (same callback as exchange_host)."""
-        self._host_call(lambda fn: lib().mox_gather_host(self._h, nranks, rank, root, fn, None), nranks, alltoallv)
+        self._host_call(lambda fn: self._L.mox_gather_host(self._h, nranks, rank, root, fn, None), nranks, alltoallv)
 
     def _host_call(self, call, nranks, alltoallv):
         err = []
@@ -358,13 +435,14 @@ class Engine:
         if len(cnt) != len(offs) - 1:
             raise ValueError("words and counts differ in length")
         buf = ctypes.create_string_buffer(data, max(1, len(data)))
-        _check(lib().mox_reduce_pairs(self._h, buf, ctypes.c_void_p(offs.ctypes.data),
+        self._c(self._L.mox_reduce_pairs(self._h, buf, ctypes.c_void_p(offs.ctypes.data),
                                       ctypes.c_void_p(cnt.ctypes.data), len(cnt)))
         return self.fetch()
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().mox_engine_destroy(self._h)
+            if not getattr(self, "_borrowed", False):
+                self._L.mox_engine_destroy(self._h)
             self._h = None
 
     def __del__(self):

@@ -32,17 +32,18 @@ def mixed_corpus(n, seed):
     return z[: n // 2] + b" " + u + b"\n" + extra + b" " + z[n // 2:]
 
 
-def run_ranks(data, world, gather_root=None):
+def run_ranks(data, world, gather_root=None, lib_path=None, stats=None):
     """Each rank: engine on device 0, its shard, exchange over ThreadAlltoall;
     with gather_root, then the gather of every table into that rank's engine
-    (out[root] is then the gathered table, the others their own)."""
+    (out[root] is then the gathered table, the others their own).  lib_path:
+    a check build; stats: a list that receives every rank's mox_stats."""
     x = mdist.ThreadAlltoall(world)
     out, errs = [None] * world, []
 
     def rank_main(r):
         try:
             lo, hi, ob, oe, at_end = mdist.shard_range(len(data), world, r)
-            e = mox.Engine(device=0)
+            e = mox.Engine(device=0, lib_path=lib_path)
             try:
                 buf = data[lo:hi]
                 d = e.alloc(max(1, len(buf)))
@@ -56,6 +57,8 @@ def run_ranks(data, world, gather_root=None):
                     t = e.fetch()
                     out[r] = (t.sorted_items(), t.tokens)
                     t.close()
+                    if stats is not None:
+                        stats.append(e.stats())
                 finally:
                     e.free(d)
             finally:

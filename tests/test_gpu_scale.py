@@ -6,9 +6,10 @@ table is too big to build, checked through size-independent properties.
   mix of (FNV-1a(word), count)) equals the oracle's, computed by routing tokens
   to owner threads by hash (oracle/mox_oracle.c, moxo_count_digest).  This size
   crosses the >2 GiB table-bytes fetch and splits partitions to kk >= 10.
-* C4 at 16 GiB (1.4e9 distinct): sum of counts == tokens == the oracle's token
-  count (a tokenize-only pass), every word distinct and NUL-free, and a spot
-  check: the oracle's counts of 4,000 random table words equal the table's.
+* C4 at 16 GiB (1.4e9 distinct): the same digest against the oracle's --
+  distinct words == the oracle's distinct count, and a word split over two
+  rows (or two words merged) changes the mix sums -- plus sum of counts ==
+  tokens, NUL-free words and a spot check of 4,000 random words' counts.
 * C5 at 16 GiB (heavy skew, ~1e6 distinct): the full sorted table against the
   oracle's.
 Each test holds the corpus, its device copy and the fetched table: tens of GB
@@ -63,15 +64,20 @@ def spot_check(data, counts, offs, raw, k, seed):
     assert want == [int(counts[i]) for i in idx]
 
 
-def test_c4_full_16gib_properties():
+def test_c4_full_16gib_digest():
     cfg = corpus.CONFIGS["C4"]
     data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
     counts, offs, raw, tokens, st = gpu_table(data)
     assert int(counts.sum()) == tokens
-    assert tokens == coracle.count_tokens(data, nthreads=16)
     assert counts.size > 1_000_000_000 and (counts > 0).all()
     assert np.frombuffer(raw, np.uint8).min() > 0  # C4 words are [a-z0-9]: no NUL, lowercased
     spot_check(data, counts, offs, raw, 4000, 1)
+    got = coracle.table_digest(counts, offs, raw)
+    del counts, offs, raw
+    want, wtok = coracle.count_digest(data, nthreads=16)
+    assert tokens == wtok
+    assert got[0] == want[0]  # distinct words: every table row is a different word
+    assert got == want
 
 
 def test_c5_full_16gib_exact():
