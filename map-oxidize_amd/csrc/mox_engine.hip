@@ -10,8 +10,6 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-#include <mutex>
-
 #include "mox_host.h"
 #include "mox_unicode_tables.h"
 
@@ -688,15 +686,8 @@ int engine_create_one(const mox_config* cfg, int dev, mox_engine** out) {
   return MOX_OK;
 }
 
-// Host buffer -> the engine's corpus staging buffer d_text.  Pageable copies
-// to one device are serialised: an engine group whose members share a GPU
-// (copy transport, tests) copied corrupted bytes when two threads ran
-// pageable hipMemcpyAsync to the same device at once (an invalid-UTF-8 error
-// in one member's shard of valid text); members on different GPUs still copy
-// in parallel.
-std::mutex g_stage_mu[64];
+// Host buffer -> the engine's corpus staging buffer d_text.
 int stage_host_range(mox_engine* e, const uint8_t* text, size_t len) {
-  std::lock_guard<std::mutex> lock(g_stage_mu[e->device & 63]);
   if (len > e->d_text_cap) {
     dfree(e->d_text);
     e->d_text = nullptr;

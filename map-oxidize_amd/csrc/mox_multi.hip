@@ -684,11 +684,21 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// One group call over per-member corpora c[i] (already on the members' GPUs).
-int group_run(mox_engine* e, const std::vector<Corpus>& c) {
+// One group call over per-member corpora c[i] (already on the members' GPUs);
+// base[i] = where member i's bytes start in the caller's input (error offsets).
+int group_run(mox_engine* e, const std::vector<Corpus>& c, const std::vector<uint64_t>& base = {}) {
   Group& G = *e->grp;
   const auto t0 = std::chrono::steady_clock::now();
   int rc = for_members(G, [&](int i) { return run_corpus(G.m[i], c[i]); });
+  if (rc == MOX_EUTF8 && !base.empty()) {  // the reference's InvalidData: report the input offset
+    for (int i = 0; i < G.n; i++) {
+      const Ctl& h = *G.m[i]->h_ctl;
+      if (h.err_utf8 != ~0ull) {
+        const uint64_t own = c[i].own_lo - c[i].lo;
+        return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", (unsigned long long)(base[i] + h.err_utf8 - own));
+      }
+    }
+  }
   if (rc) return rc;
   const double ms_local = ms_since(t0);
   uint64_t bytes = 0, tokens = 0, cold = 0, words_local = 0;
@@ -775,7 +785,7 @@ int group_count_host(mox_engine* e, const uint8_t* text, size_t len) {
     const size_t n = cut[i + 1] - cut[i];
     c[i] = make_corpus(n ? (const void*)G.m[i]->d_text : (const void*)G.m[i]->w.ctl, n, 0, n, 1);
   }
-  return group_run(e, c);
+  return group_run(e, c, std::vector<uint64_t>(cut.begin(), cut.end() - 1));
 }
 
 // Each member reads its own byte range of the file (its reader threads,
@@ -813,7 +823,7 @@ int group_count_file(mox_engine* e, const char* path) {
     const size_t n = cut[i + 1] - cut[i];
     c[i] = make_corpus(n ? (const void*)G.m[i]->d_text : (const void*)G.m[i]->w.ctl, n, 0, n, 1);
   }
-  if ((rc = group_run(e, c))) return rc;
+  if ((rc = group_run(e, c, std::vector<uint64_t>(cut.begin(), cut.end() - 1)))) return rc;
   e->stats.ms_h2d = ms_ingest;
   return MOX_OK;
 }

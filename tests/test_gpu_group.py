@@ -33,8 +33,10 @@ def group(n, flags=0, **kw):
 
 
 def mixed(n, seed):
+    """test_gpu_exchange's mixed corpus, made valid UTF-8 (its Unicode part is
+    cut at a byte count, which can split a character)."""
     import test_gpu_exchange as X
-    return X.mixed_corpus(n, seed)
+    return X.mixed_corpus(n, seed).decode("utf-8", "ignore").encode()
 
 
 @pytest.mark.parametrize("n", [2, 3])
