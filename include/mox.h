@@ -22,8 +22,9 @@
  *
  * Conventions: every entry point returns an int status (0 = MOX_OK); no
  * exception crosses the ABI; mox_last_error() holds a thread-local message.
- * An engine is bound to one HIP device and is not thread-safe (one host thread
- * per engine).  Every call except mox_run_range_async is synchronous: it
+ * An engine is bound to one HIP device -- or, as an engine group
+ * (mox_config.n_gpus > 1), drives several from the calling thread -- and is
+ * not thread-safe (one host thread per engine).  Every call except mox_run_range_async is synchronous: it
  * returns after its work (and any pending asynchronous pass) is complete.
  * mox_run_range_async returns once its pass is queued; see its comment for
  * the lifetime rule of the device buffer it reads.
@@ -195,7 +196,9 @@ int mox_run_range(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_b
  * Buffer lifetime: an overflowed pass is re-run later from d_buf, so d_buf
  * must stay valid and unmodified until the call that completes the pass has
  * returned (the next mox_run_range_async, mox_run_wait, or any other entry
- * point of this engine). */
+ * point of this engine).  An overflowed pass with a later pass already queued
+ * behind it is not re-run: the later pass supersedes its table
+ * (mox_stats.async_dropped). */
 int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t own_begin, size_t own_end,
                         int at_corpus_end);
 /* Complete every pending async pass; the last one's table is the result. */

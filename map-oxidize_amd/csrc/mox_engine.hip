@@ -493,10 +493,11 @@ int run_corpus(mox_engine* e, const Corpus& c) {
   if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));  // no side-stream dictionary build in flight
   e->have_result = false;
   uint64_t n = c.own_hi - c.own_lo;
-  Caps want = initial_caps(n, e->n_cu);
+  Caps want = caps_max(initial_caps(n, e->n_cu), e->grow_hint);
   want.cold_cap = std::max<uint64_t>(want.cold_cap, e->next_cold_cap);
   int rc = ensure_caps(e, want);
   if (rc) return rc;
+  e->grow_hint = Caps{};
   e->stats.retries = 0;
   for (int attempt = 0;; attempt++) {
     if ((rc = pipeline_once(e, c))) return rc;
@@ -552,9 +553,8 @@ void commit_result(mox_engine* e, const Corpus& c, const Ctl& h) {
 
 // ---- asynchronous passes (mox_run_range_async / mox_run_wait)
 // Completes async slot k: waits for its control block, then either commits its
-// result, or (overflow) re-runs its corpus synchronously with grown buffers.
-// A synchronous re-run overwrites the device state, so a later pending pass is
-// re-run synchronously right after it.
+// result, or (overflow) re-runs its corpus synchronously with grown buffers --
+// unless a later pass is already queued behind it, which supersedes it.
 int complete_async(mox_engine* e, int k) {
   auto& a = e->aslot[k];
   if (!a.pending) return MOX_OK;
@@ -577,25 +577,21 @@ int complete_async(mox_engine* e, int k) {
     if (later.pending) e->have_result = false;  // the later pass is overwriting this table
     return MOX_OK;
   }
+  if (later.pending) {
+    // A later pass is queued behind this one: it ran after this one on the same
+    // stream and overwrites this pass's table, so this one's result can never
+    // be observed.  It is not re-run: the capacities it asked for
+    // are remembered for the next run, and the later pass completes on its own
+    // (re-run there only if it overflowed itself).
+    e->grow_hint = caps_max(e->grow_hint, grow_for(e, h));
+    e->stats.async_dropped++;
+    return MOX_OK;
+  }
   // overflowed: drain, then the synchronous path (retry loop)
   HIPCHK(hipStreamSynchronize(e->stream));
   if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));
   e->stats.async_reruns++;
-  int rc = run_corpus(e, a.c);
-  if (later.pending) {
-    // The re-run overwrote the device state the later pass had written, so
-    // that pass is stale: re-run it now as well.  Left queued as stale, it
-    // would be re-run by the call that completes it, which by then has queued
-    // a newer pass that it would make stale in turn -- every following pass
-    // would run twice.  The first error is the one returned.
-    later.pending = false;
-    e->stats.async_reruns++;
-    const std::string msg = g_err;
-    const int rc2 = run_corpus(e, later.c);
-    if (rc == MOX_OK) rc = rc2;
-    else g_err = msg;
-  }
-  return rc;
+  return run_corpus(e, a.c);
 }
 
 int drain_async(mox_engine* e) {
@@ -711,8 +707,26 @@ int stage_host_range(mox_engine* e, const uint8_t* text, size_t len) {
 // copy them with hipMemcpyAsync on a stream of their own, so the page-cache /
 // disk reads of one chunk overlap the PCIe copies of the others.  Pinned
 // buffers and streams are engine-owned and reused across calls.
-constexpr int FILE_READERS = 8;
-constexpr size_t FILE_CHUNK = 32u << 20;
+constexpr int MAX_FILE_READERS = 16;
+// Reader threads and chunk size of mox_count_file: MOX_FILE_READERS (1..16,
+// default 8) and MOX_FILE_CHUNK_MIB (default 32) tune them (ingest A/B,
+// tools/ingest_bench.py).
+int file_readers() {
+  static const int n = [] {
+    const char* v = getenv("MOX_FILE_READERS");
+    const int k = v ? atoi(v) : 8;
+    return k < 1 ? 1 : (k > MAX_FILE_READERS ? MAX_FILE_READERS : k);
+  }();
+  return n;
+}
+size_t file_chunk() {
+  static const size_t c = [] {
+    const char* v = getenv("MOX_FILE_CHUNK_MIB");
+    const long k = v ? atol(v) : 32;
+    return (size_t)(k < 1 ? 1 : (k > 256 ? 256 : k)) << 20;
+  }();
+  return c;
+}
 // Bytes [off, off + len) of the file -> d_text[0, len).
 int stage_file_range(mox_engine* e, int fd, uint64_t off0, size_t len) {
   if (len > e->d_text_cap) {
@@ -722,6 +736,14 @@ int stage_file_range(mox_engine* e, int fd, uint64_t off0, size_t len) {
     int rc = dalloc(e, (void**)&e->d_text, len + 64);
     if (rc) return rc;
     e->d_text_cap = len;
+  }
+  const int FILE_READERS = file_readers();
+  const size_t FILE_CHUNK = file_chunk();
+  if (e->file_pin_bytes != FILE_CHUNK) {  // (re)size the pinned buffers
+    for (int t = 0; t < MAX_FILE_READERS; t++)
+      for (int k = 0; k < 2; k++)
+        if (e->file_pin[t][k]) { (void)hipHostFree(e->file_pin[t][k]); e->file_pin[t][k] = nullptr; }
+    e->file_pin_bytes = FILE_CHUNK;
   }
   for (int t = 0; t < FILE_READERS; t++) {
     if (!e->file_stream[t]) HIPCHK(hipStreamCreateWithFlags(&e->file_stream[t], hipStreamNonBlocking));
@@ -830,7 +852,7 @@ void mox_engine_destroy(mox_engine* e) {
   if (e->h_ctl) (void)hipHostFree(e->h_ctl);
   if (e->h_ctl_init) (void)hipHostFree(e->h_ctl_init);
   for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
-  for (int t = 0; t < 8; t++) {
+  for (int t = 0; t < 16; t++) {
     if (e->file_stream[t]) (void)hipStreamDestroy(e->file_stream[t]);
     for (int k = 0; k < 2; k++) if (e->file_pin[t][k]) (void)hipHostFree(e->file_pin[t][k]);
   }
@@ -861,7 +883,7 @@ int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t
     HIPCHK(hipEventCreate(&a.ev_map1));
     HIPCHK(hipEventCreateWithFlags(&a.ev_done, hipEventDisableTiming));
   }
-  Caps want = initial_caps(c.own_hi - c.own_lo, e->n_cu);
+  Caps want = caps_max(initial_caps(c.own_hi - c.own_lo, e->n_cu), e->grow_hint);
   want.cold_cap = std::max<uint64_t>(want.cold_cap, e->next_cold_cap);
   if (!(e->w.cold && caps_cover(caps_of(e->w), want))) {
     // a regrow frees the buffers a pending pass wrote its table into: complete
@@ -870,6 +892,7 @@ int mox_run_range_async(mox_engine* e, const void* d_buf, size_t buf_len, size_t
   }
   int rc = ensure_caps(e, want);
   if (rc) return rc;
+  e->grow_hint = Caps{};
   e->have_result = false;
   Seq q = seq_of(e);
   q.map_ev[0] = a.ev_map0;

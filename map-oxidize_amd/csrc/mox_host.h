@@ -117,8 +117,9 @@ struct mox_engine {
   // engine-owned corpus staging for host inputs
   uint8_t* d_text = nullptr;
   size_t d_text_cap = 0;
-  hipStream_t file_stream[8]{};  // mox_count_file readers (FILE_READERS)
-  uint8_t* file_pin[8][2]{};
+  hipStream_t file_stream[16]{};  // mox_count_file readers (up to MAX_FILE_READERS)
+  uint8_t* file_pin[16][2]{};
+  size_t file_pin_bytes = 0;      // size of each pinned reader buffer
   // last run
   bool have_result = false;
   // where the result table lives (the pass's t_* buffers, or the gather buffers)

@@ -394,6 +394,7 @@ int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
     e->res.sorted = false;
   } else {
     HIPCHK(hipStreamSynchronize(s));  // the send buffer is reused by the next exchange
+    e->res.exchanged = false;  // sent to the root: a table takes part in one gather
   }
   e->stats.ms_gather = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return MOX_OK;

@@ -1,7 +1,10 @@
-"""Worker of tests/test_gpu_exchange.py::test_host_exchange_gloo_processes:
-one rank of a gloo process group, engine on device 0, host-staged exchange
-and gather (mox_gather_host); rank 0 writes the gathered table, bytewise
-sorted by the engine (MOX_F_SORT_BYTES), as hex words to argv[1]."""
+"""Worker of tests/test_gpu_exchange.py: one rank of a gloo process group.
+Default: engine on device 0, host-staged exchange and gather
+(mox_gather_host).  With argv[2] == "rccl": engine on device LOCAL_RANK, the
+RCCL exchange and gather (mox_comm_init, mox_exchange, mox_gather) -- one
+process per GPU, needs as many GPUs as ranks.  Rank 0 writes the gathered
+table, bytewise sorted by the engine (MOX_F_SORT_BYTES), as hex words to
+argv[1]."""
 import json
 import os
 import sys
@@ -21,13 +24,21 @@ def main():
     rank, world = dist.get_rank(), dist.get_world_size()
     data = mixed_corpus(4 << 20, 77)
     lo, hi, ob, oe, at_end = mdist.shard_range(len(data), world, rank)
-    e = mox.Engine(device=0, flags=mox.MOX_F_SORT_BYTES)
+    rccl = len(sys.argv) > 2 and sys.argv[2] == "rccl"
+    e = mox.Engine(device=int(os.environ.get("LOCAL_RANK", "0")) if rccl else 0, flags=mox.MOX_F_SORT_BYTES)
     d = e.alloc(hi - lo)
     e.h2d(d, data[lo:hi])
     e.run_range(d, hi - lo, ob, oe, at_end)
-    a2a = mdist.gloo_alltoallv()
-    e.exchange_host(world, rank, a2a)
-    e.gather_host(world, rank, a2a, root=0)
+    if rccl:
+        obj = [mox.comm_unique_id() if rank == 0 else b""]
+        dist.broadcast_object_list(obj, src=0)
+        e.comm_init(world, rank, obj[0])
+        e.exchange()
+        e.gather(0)
+    else:
+        a2a = mdist.gloo_alltoallv()
+        e.exchange_host(world, rank, a2a)
+        e.gather_host(world, rank, a2a, root=0)
     if rank == 0:
         t = e.fetch()
         items = list(t.items())

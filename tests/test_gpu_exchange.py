@@ -126,6 +126,73 @@ def test_host_exchange_gloo_processes(tmp_path):
     assert [(bytes.fromhex(w), c) for w, c in res] == coracle.count(data)[0]
 
 
+def gpu_count():
+    import ctypes
+    n = ctypes.c_int(0)
+    ctypes.CDLL("libamdhip64.so").hipGetDeviceCount(ctypes.byref(n))
+    return n.value
+
+
+def test_rccl_exchange_gather_two_processes(tmp_path):
+    """One process per GPU over RCCL at world size 2: the exchange's ncclSend /
+    ncclRecv between two ranks and the gather where only the root receives
+    (ADVICE r2).  Needs two GPUs; the one-GPU box skips it (RCCL refuses two
+    ranks on one device, "Duplicate GPU detected")."""
+    if gpu_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    out = tmp_path / "merged.json"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29563",
+           os.path.join(ROOT, "tests", "dist_worker.py"), str(out), "rccl"]
+    r = subprocess.run(cmd, capture_output=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    res = json.loads(out.read_text())
+    data = mixed_corpus(4 << 20, 77)
+    assert [(bytes.fromhex(w), c) for w, c in res] == coracle.count(data)[0]
+
+
+def test_gather_requires_an_exchanged_table():
+    """mox_gather / mox_gather_host refuse a table that is not the result of an
+    exchange (ranks' local tables overlap) and a table that was already
+    gathered: MOX_ESTATE on every rank, no transport call."""
+    data = mixed_corpus(2 << 20, 61)
+    world = 2
+    x = mdist.ThreadAlltoall(world)
+    codes, errs = [[] for _ in range(world)], []
+
+    def rank_main(r):
+        try:
+            lo, hi, ob, oe, at_end = mdist.shard_range(len(data), world, r)
+            e = mox.Engine(device=0)
+            d = e.alloc(hi - lo)
+            try:
+                e.h2d(d, data[lo:hi])
+                e.run_range(d, hi - lo, ob, oe, at_end)
+                for step in ("gather_local", "exchange", "gather", "gather_again"):
+                    try:
+                        if step == "exchange":
+                            e.exchange_host(world, r, x.fn(r))
+                        else:
+                            e.gather_host(world, r, x.fn(r), root=0)
+                        codes[r].append((step, 0))
+                    except mox.MoxError as ex:
+                        codes[r].append((step, ex.code))
+            finally:
+                e.free(d)
+                e.close()
+        except BaseException as ex:  # noqa: BLE001
+            errs.append(ex)
+            x.barrier.abort()
+
+    ts = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    [t.start() for t in ts]
+    [t.join(300) for t in ts]
+    if errs:
+        raise errs[0]
+    want = [("gather_local", mox.MOX_ESTATE), ("exchange", 0), ("gather", 0), ("gather_again", mox.MOX_ESTATE)]
+    assert codes[0] == want and codes[1] == want
+
+
 def test_host_exchange_high_cardinality():
     """The reduce-only pass over received partials splits mostly-distinct
     partitions too (weighted records only)."""
