@@ -420,6 +420,8 @@ FILE* debug_file(const char* name) {
   return fopen((std::string(dir) + "/" + name).c_str(), "w");
 }
 void debug_dump(mox_engine* e, const Ctl& h) {
+  if (e->w.dbg & DBG_COUNT)  // k_reduce slow path: inserts, lane iterations not done, publication retries
+    fprintf(stderr, "mox dbg_cnt %llu %llu %llu\n", h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2]);
   if ((e->w.dbg & DBG_STAMP) && e->w.stamps) {
     std::vector<unsigned long long> st(8 * NB);
     (void)hipMemcpy(st.data(), e->w.stamps, st.size() * 8, hipMemcpyDeviceToHost);

@@ -1733,6 +1733,9 @@ constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort
 #ifndef MOX_RED_UNROLL
 #define MOX_RED_UNROLL 2
 #endif
+#ifndef MOX_RED_FLAT
+#define MOX_RED_FLAT 1  // k_reduce streams a unit's records as one flat range, equal shares per wave
+#endif
 constexpr int RED_UNROLL = MOX_RED_UNROLL;
 constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
 
@@ -2211,6 +2214,9 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   s.misc = (uint32_t*)sp; sp += 16;
   __shared__ uint32_t dbgc[4];
   __shared__ uint32_t s_unit;
+  __shared__ uint64_t red_wsum[RED_THREADS / 64];
+  uint32_t* rpre = reinterpret_cast<uint32_t*>(s.idx);  // region prefix (G + 1 words in the idx + bin space)
+  static_assert(RED_CAP * 2 + (RED_SORTB + 8) * 2 >= (MAX_MAP_GRID + 1) * 4, "region prefix space");
   s.dbg = MOX_ABL(w.dbg, DBG_COUNT) ? dbgc : nullptr;
   s.plain = MOX_ABL(w.dbg, DBG_RED_PLAINADD) != 0;
   s.ctl = w.ctl;
@@ -2260,7 +2266,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     // split unit: its contiguous cold range is cut into NWV wave chunks
     const uint64_t kin0 = split ? ud.in_off : 0;
     const uint32_t kin_n = split ? ud.in_n : 0;
-    const uint32_t kchunk = (kin_n + NWV - 1) / NWV;
+    [[maybe_unused]] const uint32_t kchunk = (kin_n + NWV - 1) / NWV;
     const bool stamp = MOX_ABL(w.dbg, DBG_STAMP) && tid == 0 && !split;
     if (stamp) w.stamps[b * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     uint32_t kk = 0;
@@ -2269,8 +2275,100 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     for (uint32_t sub = 0; sub < (1u << kk);) {
       for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
       if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
+#if MOX_RED_FLAT
+      // region prefix of a whole partition (the map workgroups' regions one after
+      // another), in the sort index / bin space, which is free until the sort
+      if (!split) {
+        uint64_t tot;
+        const uint64_t ex = block_exscan(tid < (int)G ? w.cold_n[(uint64_t)tid * NB + b] : 0u, red_wsum, tot);
+        if (tid < (int)G) rpre[tid] = (uint32_t)ex;
+        if (tid == 0) rpre[G] = (uint32_t)tot;
+      }
+#endif
       __syncthreads();
       for (int rep = 0; rep < (MOX_ABL(w.dbg, DBG_RED_TWICE) ? 2 : 1); rep++)
+#if MOX_RED_FLAT
+      // cold records: the unit's records as one flat index space (whole
+      // partition: region g = map workgroup g, at rpre[g]; split unit: one
+      // contiguous range), cut into NWV equal wave shares in 64-record steps so
+      // the waves finish together and every chunk is full but the wave's last.
+      // Each lane walks forward through the regions (its records ascend by 64
+      // per step), the next chunk's loads in flight while the current one is
+      // inserted.
+      {
+        const uint32_t n = split ? kin_n : rpre[G];
+        const uint32_t per = (((n + NWV - 1) / NWV) + 63) & ~63u;
+        const uint32_t a0 = (uint32_t)wv * per < n ? (uint32_t)wv * per : n;
+        const uint32_t a1 = n - a0 < per ? n : a0 + per;
+        const uint4* ubase = split ? w.split_k + kin0 : w.cold + b * w.cold_cap;  // region g at + g NB cold_cap
+        const uint64_t gstride = (uint64_t)NB * w.cold_cap;
+        // lane state: region r holds flat records [rs, re)
+        uint32_t r = 0, rs = 0, re = split ? 0xFFFFFFFFu : 0u;
+        if (!split && a0 < a1) {  // region of a0: last r with rpre[r] <= a0 (wave-uniform search)
+          uint32_t lo = 0, hi = G - 1;
+          while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (rpre[mid] <= a0) lo = mid; else hi = mid - 1;
+          }
+          r = lo;
+          rs = rpre[r];
+          re = rpre[r + 1];
+        }
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        auto load = [&](uint32_t c, uint4 (&v)[RED_UNROLL]) {  // unconditional: uniform vmcnt
+#pragma unroll
+          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+            const uint32_t i = c + u2 * 64 + lane;
+            const bool ok = i < a1;
+            bool adv = ok && i >= re;
+            while (__any(adv)) {  // no cross-lane dependence: a plain per-lane walk
+              if (adv) { r++; rs = re; re = rpre[r + 1]; }
+              adv = ok && i >= re;
+            }
+            const uint4* p = ok ? ubase + (uint64_t)r * gstride + (i - rs) : ubase;
+            const u32x4 x = *reinterpret_cast<const u32x4*>(p);
+            v[u2] = make_uint4(x.x, x.y, x.z, x.w);
+          }
+        };
+        auto process = [&](const uint4 (&cur)[RED_UNROLL], uint32_t c) {
+          if (__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;  // redone anyway
+          uint32_t h[RED_UNROLL];
+          bool todo[RED_UNROLL];
+          RED_MARK(0);
+#pragma unroll
+          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+            h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
+            todo[u2] = c + u2 * 64 + lane < a1 && in_sub(h[u2], shift0, kk, sub);
+          }
+          RED_MARK(1);
+          if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
+#pragma unroll
+            for (int u2 = 0; u2 < RED_UNROLL; u2++)
+              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+            RED_MARK(2);
+#pragma unroll
+            for (int u2 = 0; u2 < RED_UNROLL; u2++)
+              if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
+            RED_MARK(3);
+          } else {
+            asm volatile("" ::"v"(h[0]), "v"(h[1]));
+          }
+        };
+        constexpr uint32_t CH = 64 * RED_UNROLL;
+        uint32_t c = a0;
+        uint4 A[RED_UNROLL], B[RED_UNROLL];
+        if (c < a1) load(c, A);
+        while (c < a1) {
+          load(c + CH, B);
+          process(A, c);
+          c += CH;
+          if (c >= a1) break;
+          load(c + CH, A);
+          process(B, c);
+          c += CH;
+        }
+      }
+#else
       // cold records: wave wv streams its regions (whole partition: regions
       // g = wv, wv + NWV, ...; split unit: one chunk) 64 x RED_UNROLL records at
       // a time, the next chunk's loads in flight while the current one is
@@ -2357,6 +2455,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           i0 = ia;
         }
       }
+#endif
       if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
       for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
         const WRec rr = wsrc[i];
@@ -2394,10 +2493,9 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         }
       __syncthreads();
       {  // exclusive scan of the RED_SORTB bin counts (2 per thread)
-        __shared__ uint64_t wsum[RED_THREADS / 64];
         uint64_t tot;
         const uint32_t c0 = s.bin[2 * tid], c1 = s.bin[2 * tid + 1];
-        const uint64_t ex = block_exscan(c0 + c1, wsum, tot);
+        const uint64_t ex = block_exscan(c0 + c1, red_wsum, tot);
         s.bin[2 * tid] = (uint16_t)ex;
         s.bin[2 * tid + 1] = (uint16_t)(ex + c0);
         if (tid == 0) s.bin[RED_SORTB] = (uint16_t)tot;
