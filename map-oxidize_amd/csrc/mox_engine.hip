@@ -152,6 +152,8 @@ int alloc_fixed(mox_engine* e) {
   if ((rc = dalloc(e, (void**)&w.dict_tot, DICT_SLOTS * 8))) return rc;
   w.map_grid = (uint32_t)std::min(e->n_cu * MAP_WG_PER_CU, MAX_MAP_GRID);
   if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.samp, (size_t)w.map_grid * NB * SPLIT_PER_REGION * 4))) return rc;
+  HIPCHK(hipMemset(w.samp, 0, (size_t)w.map_grid * NB * SPLIT_PER_REGION * 4));
   if ((rc = dalloc(e, (void**)&w.spill_n, (size_t)w.map_grid * 4))) return rc;
   // bucket directory block: one allocation, zeroed per run
   size_t dir_bytes = NB * 8 + NB * 4 + NB * 4 + 2 * (NB + 1) * 8 + NB * 8 + (NB + 1) * 8;
@@ -837,7 +839,7 @@ void mox_engine_destroy(mox_engine* e) {
   }
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
-  void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
+  void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.samp, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.ui, w.t_counts, w.t_offs, w.t_bytes, e->d_text,
                   w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.mid_units, w.small_units, w.u_uniq, w.u_uniq_off,

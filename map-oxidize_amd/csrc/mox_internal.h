@@ -332,6 +332,8 @@ struct Work {  // device buffers of one engine
   // cold records: region (map workgroup g, partition b) = cold[(g*NB + b)*cold_cap ...]
   uint4* cold;                    // map_grid * NB * cold_cap records of 16 B
   uint32_t* cold_n;               // map_grid * NB records written per region
+  uint32_t* samp;                 // NB * map_grid * SPLIT_PER_REGION: key hashes of every region's first records
+                                  // (k_map writes them, 0 = none; k_split_count's sample)
   uint32_t cold_cap;
   uint32_t map_grid;
   uint4* spill;                   // map_grid * spill_cap records (regions that overflowed)

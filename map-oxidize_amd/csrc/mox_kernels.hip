@@ -393,7 +393,14 @@ __device__ __forceinline__ int pair_try(uint32_t* pst, uint4* pend, uint32_t slo
 // which it won the slot.  (A per-lane `while (!done)` loop lets the compiler
 // sink them past the loop exit, where the winning lane waits for the spinning
 // lanes of its own wave: a SIMT deadlock.)
-__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t b, uint4 key) {
+// k_split_count's sample: the key hashes of the first SPLIT_PER_REGION records
+// of every (workgroup, partition) region, written when a record lands at such a
+// position (rare: 4 of ~150 records per region at C2), so that the split
+// decision reads 4 KiB per partition instead of 1,024 scattered records.
+__device__ __forceinline__ void note_sample(const MapCtx& m, uint32_t b, uint32_t pos, uint32_t h) {
+  if (pos < SPLIT_PER_REGION) rare(m).samp[((uint64_t)b * rare(m).map_grid + blockIdx.x) * SPLIT_PER_REGION + pos] = h;
+}
+__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t b, uint32_t h, uint4 key) {
   bool done = false;
   do {
     if (!done) {
@@ -401,6 +408,10 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t b, uint4 key
       const int r = pair_try(m.s.pst, m.s.pend, b, key, &q);
       if (r == 2) {
         const uint32_t pos = atomicAdd(&m.s.bcnt[b], 2u);
+        if (pos < SPLIT_PER_REGION) {
+          note_sample(m, b, pos, hash32(q.x, q.y, q.z, q.w));
+          note_sample(m, b, pos + 1, h);
+        }
         if (pos + 1 < m.w.cold_cap) {
           uint4* o = m.w.cold + ((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos;
           o[0] = q;
@@ -419,8 +430,9 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-  if (MOX_DICT_PAIRS || m.dict_n == 0) { cold_pair(m, b, key); return; }
+  if (MOX_DICT_PAIRS || m.dict_n == 0) { cold_pair(m, b, h, key); return; }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
+  if (pos < SPLIT_PER_REGION) note_sample(m, b, pos, h);
   if (pos < m.w.cold_cap) {
     m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
     return;
@@ -1100,6 +1112,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     for (int i = tid; i < NB; i += MAP_THREADS) {
       if (m.s.pst[i] != PS_FULL) continue;
       const uint32_t pos = atomicAdd(&m.s.bcnt[i], 1u);
+      const uint4 q = m.s.pend[i];
+      note_sample(m, i, pos, hash32(q.x, q.y, q.z, q.w));
       if (pos < w.cold_cap) w.cold[((uint64_t)blockIdx.x * NB + i) * w.cold_cap + pos] = m.s.pend[i];
       else cold_spill(m, m.s.pend[i]);
     }
@@ -1121,6 +1135,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   for (int i = tid; i < NB; i += MAP_THREADS) {
     const uint32_t cnt = m.s.bcnt[i];
     w.cold_n[(uint64_t)blockIdx.x * NB + i] = cnt < w.cold_cap ? cnt : w.cold_cap;
+    for (uint32_t j = cnt; j < SPLIT_PER_REGION; j++) note_sample(m, i, j, 0u);  // no record there (0 = none)
     cmax = cnt > cmax ? cnt : cmax;
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -1188,8 +1203,9 @@ extern "C" __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags
   }
   if (flags & (INIT_DICT | INIT_DICT_SIDE)) zero_words(w.dict_tot, DICT_SLOTS * 8, t, stride);
   else if (t == 0) { w.dict_hist[DH_N] = 0; w.dict_hist[DH_T] = 0; }  // no dictionary this pass
-  if (flags & INIT_MAP) {
+  if (flags & INIT_MAP) {  // reduce-only pass: no map regions, no split sample
     zero_words(w.cold_n, (uint64_t)w.map_grid * NB * 4, t, stride);
+    zero_words(w.samp, (uint64_t)w.map_grid * NB * SPLIT_PER_REGION * 4, t, stride);
     zero_words(w.spill_n, (uint64_t)w.map_grid * 4, t, stride);
   }
 }
@@ -1822,11 +1838,31 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   } while (__any(!done));
 }
 
+#ifndef MOX_RED_KEYPROBE
+#define MOX_RED_KEYPROBE 0  // A/B: fast path compares the home bucket's keys directly (1; 2: and the next bucket's)
+#endif
 // Fast path for records whose key is already published in its home bucket or
 // the next one (keys overflow at most one bucket at this table load): two tag
 // reads issued together, one key read, one add.  Returns false when the slow
 // path is needed (new key, further bucket, publication pending).
+// MOX_RED_KEYPROBE: the bucket's four keys are read at once and compared with
+// the record's (one LDS round trip instead of two); keys are zeroed with the
+// tags at every sub-pass, so a key equal to the record's was written in this
+// sub-pass by the slot's claimant, and adding to its count is exact whether or
+// not the claimant has published yet (the adds commute).
 __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
+#if MOX_RED_KEYPROBE
+  const uint32_t b = red_bucket(h);
+  uint4 kb[4 * MOX_RED_KEYPROBE];
+#pragma unroll
+  for (int i = 0; i < 4 * MOX_RED_KEYPROBE; i++) kb[i] = s.key[(4 * b + i) % RED_SLOTS];
+  int sl = -1;
+#pragma unroll
+  for (int i = 4 * MOX_RED_KEYPROBE - 1; i >= 0; i--) sl = key_eq16(kb[i], k) ? (int)((4 * b + i) % RED_SLOTS) : sl;
+  if (sl < 0) return false;
+  atomicAdd(&s.cnt[sl], (unsigned long long)c);
+  return true;
+#else
   const uint32_t b = red_bucket(h), b2 = b + 1 == RED_BK ? 0 : b + 1;
   const uint4 t = s.tag4[b], t2 = s.tag4[b2];
   int sl = t2.w == h ? (int)(4 * b2 + 3) : -1;
@@ -1844,6 +1880,7 @@ __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, ui
   if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
   else atomicAdd(&s.cnt[sl], (unsigned long long)c);
   return true;
+#endif
 }
 
 // Table order of short words: (h32, hash32b, key).  Every reduce kernel uses
@@ -1975,8 +2012,8 @@ __device__ __forceinline__ void split_count(const Work& w) {
   if (tid == 0) s_ones = 0;
   __syncthreads();
   // sample = the first SPLIT_PER_REGION cold records of every map workgroup's
-  // region (spread over the whole corpus, all loads issued at once), topped
-  // up with weighted records
+  // region (spread over the whole corpus; their key hashes, noted by k_map),
+  // topped up with weighted records
   const uint32_t G = w.map_grid;
   auto mark = [&](uint32_t h) {
     const uint32_t bit = hbits(h, NB_LOG2, 12);  // LC_BITS = 2^12
@@ -1985,18 +2022,15 @@ __device__ __forceinline__ void split_count(const Work& w) {
   uint32_t mine = 0;
   {
     constexpr int PER = (SPLIT_SAMPLE + SC_THREADS - 1) / SC_THREADS;  // sample slots per thread
-    uint4 v[PER];
-    bool ok[PER];
+    uint32_t v[PER];
 #pragma unroll
-    for (int j = 0; j < PER; j++) {
+    for (int j = 0; j < PER; j++) {  // k_map's note_sample: contiguous per partition, 0 = no record
       const uint32_t idx = tid + j * SC_THREADS;
-      const uint32_t g = idx / SPLIT_PER_REGION, i = idx % SPLIT_PER_REGION;
-      ok[j] = idx < SPLIT_SAMPLE && g < G && i < w.cold_n[(uint64_t)g * NB + b];
-      v[j] = ok[j] ? w.cold[((uint64_t)g * NB + b) * w.cold_cap + i] : make_uint4(0, 0, 0, 0);
+      v[j] = idx < SPLIT_SAMPLE && idx < G * SPLIT_PER_REGION ? w.samp[(uint64_t)b * G * SPLIT_PER_REGION + idx] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < PER; j++)
-      if (ok[j]) { mark(hash32(v[j].x, v[j].y, v[j].z, v[j].w)); mine++; }
+      if (v[j]) { mark(v[j]); mine++; }
   }
   uint64_t cs;
   (void)block_exscan(mine, wsum, cs);
@@ -2273,7 +2307,11 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     uint64_t written = 0, wbytes = 0;
     bool failed = false;
     for (uint32_t sub = 0; sub < (1u << kk);) {
-      for (int i = tid; i < RED_SLOTS; i += RED_THREADS) { tags[i] = 0; s.cnt[i] = 0; }
+      for (int i = tid; i < RED_SLOTS; i += RED_THREADS) {
+        tags[i] = 0;
+        s.cnt[i] = 0;
+        if (MOX_RED_KEYPROBE) s.key[i] = make_uint4(0, 0, 0, 0);
+      }
       if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
 #if MOX_RED_FLAT
       // region prefix of a whole partition (the map workgroups' regions one after
