@@ -337,7 +337,7 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = fals
   const uint64_t row0 = c.own_lo & ~15ull;
   const uint64_t nrows = c.own_hi > c.own_lo ? (c.own_hi - row0 + PAY - 1) / PAY : 0;
   const int grid = (int)w.map_grid;
-  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows);
+  hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows, 0u);
   q.step("k_map");
   q.rec(2);
   // 3. lanes
@@ -708,12 +708,18 @@ int stage_host_range(mox_engine* e, const uint8_t* text, size_t len) {
 
 // File -> HBM: FILE_READERS threads each pread their
 // chunks (c = t, t + FILE_READERS, ...) into two pinned buffers of their own and
-// copy them with hipMemcpyAsync on a stream of their own, so the page-cache /
-// disk reads of one chunk overlap the PCIe copies of the others.  Pinned
-// buffers and streams are engine-owned and reused across calls.
+// copy them with hipMemcpyAsync, so the page-cache / disk reads of one chunk
+// overlap the PCIe copies of the others.  All copies go to ONE stream (one DMA
+// queue): on the GPU box one stream moves 55 GB/s of pinned H2D copies and two
+// or more streams 47-53 GB/s, while 8 pread threads alone read 73 GB/s from the
+// page cache (profiles/r03_ingest_probe.txt), so per-reader streams left the
+// pipeline at 40-44 GB/s.  A reader refills a buffer once the event recorded
+// after its copy has completed.  Pinned buffers, stream and events are
+// engine-owned and reused across calls.
 constexpr int MAX_FILE_READERS = 16;
 // Reader threads and chunk size of mox_count_file: MOX_FILE_READERS (1..16,
-// default 8) and MOX_FILE_CHUNK_MIB (default 32) tune them (ingest A/B,
+// default 8) and MOX_FILE_CHUNK_MIB (default 32) tune them; MOX_FILE_STREAMS=0
+// gives every reader its own copy stream (the round-2 scheme, for A/B:
 // tools/ingest_bench.py).
 int file_readers() {
   static const int n = [] {
@@ -723,6 +729,13 @@ int file_readers() {
   }();
   return n;
 }
+bool file_shared_stream() {
+  static const bool one = [] {
+    const char* v = getenv("MOX_FILE_STREAMS");
+    return !(v && atoi(v) == 0);
+  }();
+  return one;
+}
 size_t file_chunk() {
   static const size_t c = [] {
     const char* v = getenv("MOX_FILE_CHUNK_MIB");
@@ -731,63 +744,199 @@ size_t file_chunk() {
   }();
   return c;
 }
-// Bytes [off, off + len) of the file -> d_text[0, len).
-int stage_file_range(mox_engine* e, int fd, uint64_t off0, size_t len) {
-  if (len > e->d_text_cap) {
-    dfree(e->d_text);
-    e->d_text = nullptr;
-    e->d_text_cap = 0;
-    int rc = dalloc(e, (void**)&e->d_text, len + 64);
-    if (rc) return rc;
-    e->d_text_cap = len;
-  }
-  const int FILE_READERS = file_readers();
-  const size_t FILE_CHUNK = file_chunk();
-  if (e->file_pin_bytes != FILE_CHUNK) {  // (re)size the pinned buffers
-    for (int t = 0; t < MAX_FILE_READERS; t++)
-      for (int k = 0; k < 2; k++)
-        if (e->file_pin[t][k]) { (void)hipHostFree(e->file_pin[t][k]); e->file_pin[t][k] = nullptr; }
-    e->file_pin_bytes = FILE_CHUNK;
-  }
-  for (int t = 0; t < FILE_READERS; t++) {
-    if (!e->file_stream[t]) HIPCHK(hipStreamCreateWithFlags(&e->file_stream[t], hipStreamNonBlocking));
-    for (int k = 0; k < 2; k++)
-      if (!e->file_pin[t][k]) HIPCHK(hipHostMalloc((void**)&e->file_pin[t][k], FILE_CHUNK, hipHostMallocDefault));
-  }
-  const auto t0 = std::chrono::steady_clock::now();
-  const size_t nchunks = (len + FILE_CHUNK - 1) / FILE_CHUNK;
-  std::vector<int> err(FILE_READERS, 0);
-  std::vector<std::string> msg(FILE_READERS);
-  auto reader = [&](int t) {
-    (void)hipSetDevice(e->device);
-    int k = 0;
-    size_t pending = 0;  // copies in flight on this reader's stream
-    for (size_t c = t; c < nchunks; c += FILE_READERS, k ^= 1) {
-      if (pending == 2) {  // the buffer about to be refilled was copied two chunks ago
-        if (hipStreamSynchronize(e->file_stream[t]) != hipSuccess) { err[t] = MOX_EHIP; msg[t] = "file copy failed"; return; }
-        pending = 0;
+// Bytes [off0, off0 + len) of a file -> d_text[0, len), by reader threads.
+// start() launches them; wait_bytes(b) blocks until the copies of the first b
+// bytes are enqueued (shared copy stream: an event recorded there afterwards
+// completes once they have landed); finish() joins them and waits for the
+// copies.  The destructor joins readers still running (an error path).
+struct FileStager {
+  mox_engine* e;
+  int fd;
+  uint64_t off0;
+  size_t len, chunk = 0, nchunks = 0;
+  int readers = 0;
+  bool shared = true;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<char> issued;
+  size_t prefix = 0;               // chunks 0 .. prefix - 1 enqueued
+  std::atomic<bool> failed{false};
+  std::vector<int> err;
+  std::vector<std::string> msg;
+  std::vector<std::thread> th;
+  std::chrono::steady_clock::time_point t0;
+
+  FileStager(mox_engine* e_, int fd_, uint64_t off0_, size_t len_) : e(e_), fd(fd_), off0(off0_), len(len_) {}
+  ~FileStager() { for (auto& x : th) if (x.joinable()) { failed = true; x.join(); } }
+  hipStream_t copy_stream() const { return e->file_stream[0]; }
+
+  int start() {
+    if (len > e->d_text_cap) {
+      dfree(e->d_text);
+      e->d_text = nullptr;
+      e->d_text_cap = 0;
+      int rc = dalloc(e, (void**)&e->d_text, len + 64);
+      if (rc) return rc;
+      e->d_text_cap = len;
+    }
+    readers = file_readers();
+    chunk = file_chunk();
+    shared = file_shared_stream();
+    if (e->file_pin_bytes != chunk) {  // (re)size the pinned buffers
+      for (int t = 0; t < MAX_FILE_READERS; t++)
+        for (int k = 0; k < 2; k++)
+          if (e->file_pin[t][k]) { (void)hipHostFree(e->file_pin[t][k]); e->file_pin[t][k] = nullptr; }
+      e->file_pin_bytes = chunk;
+    }
+    for (int t = 0; t < readers; t++) {
+      if (!e->file_stream[t]) HIPCHK(hipStreamCreateWithFlags(&e->file_stream[t], hipStreamNonBlocking));
+      for (int k = 0; k < 2; k++) {
+        if (!e->file_pin[t][k]) HIPCHK(hipHostMalloc((void**)&e->file_pin[t][k], chunk, hipHostMallocDefault));
+        if (!e->file_ev[t][k]) HIPCHK(hipEventCreateWithFlags(&e->file_ev[t][k], hipEventDisableTiming));
       }
-      const size_t off = c * FILE_CHUNK, n = std::min(FILE_CHUNK, len - off);
+    }
+    nchunks = (len + chunk - 1) / chunk;
+    issued.assign(nchunks, 0);
+    err.assign(readers, 0);
+    msg.assign(readers, std::string());
+    t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < readers; t++) th.emplace_back([this, t] { reader(t); });
+    return MOX_OK;
+  }
+
+  void abort_with(int t, int code, const char* m) {
+    err[t] = code;
+    msg[t] = m;
+    std::lock_guard<std::mutex> g(mu);
+    failed = true;
+    cv.notify_all();
+  }
+
+  void reader(int t) {
+    (void)hipSetDevice(e->device);
+    hipStream_t cs = e->file_stream[shared ? 0 : t];
+    int k = 0;
+    bool used[2] = {false, false};
+    for (size_t c = t; c < nchunks && !failed; c += readers, k ^= 1) {
+      if (used[k] && hipEventSynchronize(e->file_ev[t][k]) != hipSuccess)  // buffer k's previous copy
+        return abort_with(t, MOX_EHIP, "file copy failed");
+      const size_t off = c * chunk, n = std::min(chunk, len - off);
       size_t got = 0;
       while (got < n) {
         const ssize_t r = pread(fd, e->file_pin[t][k] + got, n - got, (off_t)(off0 + off + got));
         if (r < 0 && errno == EINTR) continue;
-        if (r <= 0) { err[t] = MOX_EIO; msg[t] = std::string("read failed: ") + (r < 0 ? strerror(errno) : "short file"); return; }
+        if (r <= 0) return abort_with(t, MOX_EIO, (std::string("read failed: ") + (r < 0 ? strerror(errno) : "short file")).c_str());
         got += (size_t)r;
       }
-      if (hipMemcpyAsync(e->d_text + off, e->file_pin[t][k], n, hipMemcpyHostToDevice, e->file_stream[t]) != hipSuccess) {
-        err[t] = MOX_EHIP; msg[t] = "hipMemcpyAsync failed"; return;
-      }
-      pending++;
+      // (another reader's copy may slip in between the copy and the record: the
+      // event then completes a little later, which only delays the refill)
+      if (hipMemcpyAsync(e->d_text + off, e->file_pin[t][k], n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+          hipEventRecord(e->file_ev[t][k], cs) != hipSuccess)
+        return abort_with(t, MOX_EHIP, "hipMemcpyAsync failed");
+      used[k] = true;
+      std::lock_guard<std::mutex> g(mu);
+      issued[c] = 1;
+      while (prefix < nchunks && issued[prefix]) prefix++;
+      cv.notify_all();
     }
-    if (hipStreamSynchronize(e->file_stream[t]) != hipSuccess) { err[t] = MOX_EHIP; msg[t] = "file copy failed"; }
+    if (!shared && hipStreamSynchronize(cs) != hipSuccess) abort_with(t, MOX_EHIP, "file copy failed");
+  }
+
+  // true once the copies of bytes [0, bytes) are enqueued; false on a reader error
+  bool wait_bytes(size_t bytes) {
+    std::unique_lock<std::mutex> g(mu);
+    cv.wait(g, [&] { return failed || prefix * chunk >= bytes || prefix == nchunks; });
+    return !failed;
+  }
+
+  int finish() {
+    for (auto& x : th) x.join();
+    th.clear();
+    if (shared) HIPCHK(hipStreamSynchronize(copy_stream()));
+    for (int t = 0; t < readers; t++)
+      if (err[t]) return fail(err[t], "%s", msg[t].c_str());
+    e->stats.ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return MOX_OK;
+  }
+};
+
+int stage_file_range(mox_engine* e, int fd, uint64_t off0, size_t len) {
+  FileStager st(e, fd, off0, len);
+  if (int rc = st.start()) return rc;
+  return st.finish();
+}
+
+// mox_count_file on one engine with the map overlapped with the ingest: the
+// file is read in chunks by the FileStager, and the map runs one launch per
+// MAP_RANGE bytes as soon as that range and the next one (its look-ahead for
+// tokens that cross the range end) have landed; the dictionary comes from a
+// sample of the first range.  After the last range: the reduce tail of an
+// ordinary pass over the whole file.  A token longer than the look-ahead or
+// an overflow re-runs the pass on the now resident file (run_corpus), so the
+// result is the ordinary pass's in every case.
+constexpr size_t MAP_RANGE = 64ull << 20;
+int run_file_overlapped(mox_engine* e, int fd, size_t len) {
+  FileStager st(e, fd, 0, len);
+  if (int rc = st.start()) return rc;
+  if (e->dstream) HIPCHK(hipStreamSynchronize(e->dstream));
+  e->have_result = false;
+  const Corpus whole = make_corpus(e->d_text, len, 0, len, 1);
+  Caps want = caps_max(initial_caps(len, e->n_cu), e->grow_hint);
+  want.cold_cap = std::max<uint64_t>(want.cold_cap, e->next_cold_cap);
+  if (int rc = ensure_caps(e, want)) return rc;
+  e->grow_hint = Caps{};
+  e->stats.retries = 0;
+  if (!e->file_land) HIPCHK(hipEventCreateWithFlags(&e->file_land, hipEventDisableTiming));
+  Work& w = e->w;
+  hipStream_t s = e->stream;
+  const Seq q = seq_of(e);
+  // the engine stream waits until bytes [0, b) have landed
+  auto land = [&](size_t b) -> int {
+    if (!st.wait_bytes(b)) return MOX_EIO;  // the reader's error is reported by finish()
+    HIPCHK(hipEventRecord(e->file_land, st.copy_stream()));
+    HIPCHK(hipStreamWaitEvent(s, e->file_land, 0));
+    return MOX_OK;
   };
-  std::vector<std::thread> th;
-  for (int t = 0; t < FILE_READERS; t++) th.emplace_back(reader, t);
-  for (auto& x : th) x.join();
-  for (int t = 0; t < FILE_READERS; t++)
-    if (err[t]) return fail(err[t], "%s", msg[t].c_str());
-  e->stats.ms_h2d = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  const size_t nr = (len + MAP_RANGE - 1) / MAP_RANGE;
+  int rc = land(std::min(len, 2 * MAP_RANGE));
+  if (!rc) {
+    q.rec(0);
+    const bool dict = !(e->flags & MOX_F_NO_DICT);
+    hipLaunchKernelGGL(k_init, dim3(256), dim3(256), 0, s, w, 0ull, dict ? 1u : 0u);  // INIT_DICT
+    if (dict) launch_dict(e, make_corpus(e->d_text, MAP_RANGE, 0, MAP_RANGE, 0), s, q);
+    q.rec(1);
+    for (size_t j = 0; j < nr && !rc; j++) {
+      const size_t lo = j * MAP_RANGE, hi = std::min(len, lo + MAP_RANGE), ahead = std::min(len, hi + MAP_RANGE);
+      if (j > 0) rc = land(ahead);
+      if (rc) break;
+      const Corpus cj = make_corpus(e->d_text, ahead, lo, hi, ahead == len);
+      const uint64_t row0 = cj.own_lo & ~15ull;
+      const uint64_t nrows = (cj.own_hi - row0 + PAY - 1) / PAY;
+      hipLaunchKernelGGL(k_map, dim3(w.map_grid), dim3(MAP_THREADS), map_lds_bytes(), s, cj, w, nrows, j > 0 ? 1u : 0u);
+    }
+    if (!rc) {
+      q.rec(2);
+      hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, whole, w, e->tables);
+      q.rec(3);
+      launch_reduce_tail(e, whole, q);
+    }
+  }
+  const int frc = st.finish();  // joins the readers: their error first
+  if (frc) { (void)hipStreamSynchronize(s); return frc; }
+  if (rc) { (void)hipStreamSynchronize(s); return fail(rc, "file ingest failed"); }
+  const double h2d = e->stats.ms_h2d;
+  if ((rc = finish_pass(e, q))) return rc;
+  e->stats.ms_h2d = h2d;
+  const Ctl& h = *e->h_ctl;
+  if ((rc = check_failed(h))) return rc;
+  if (h.err_utf8 != ~0ull) return fail(MOX_EUTF8, "stream did not contain valid UTF-8 (byte %llu)", h.err_utf8);
+  if (h.halo_err != ~0ull || h.overflow) {  // a token past the look-ahead, or buffers too small: the ordinary pass
+    if (h.overflow && !(h.overflow & OVF_REDUCE)) e->grow_hint = grow_for(e, h);
+    rc = run_corpus(e, whole);
+    e->stats.ms_h2d = h2d;
+    return rc;
+  }
+  commit_result(e, whole, h);
   return MOX_OK;
 }
 
@@ -858,8 +1007,12 @@ void mox_engine_destroy(mox_engine* e) {
   for (auto& ev : e->ev) if (ev) (void)hipEventDestroy(ev);
   for (int t = 0; t < 16; t++) {
     if (e->file_stream[t]) (void)hipStreamDestroy(e->file_stream[t]);
-    for (int k = 0; k < 2; k++) if (e->file_pin[t][k]) (void)hipHostFree(e->file_pin[t][k]);
+    for (int k = 0; k < 2; k++) {
+      if (e->file_ev[t][k]) (void)hipEventDestroy(e->file_ev[t][k]);
+      if (e->file_pin[t][k]) (void)hipHostFree(e->file_pin[t][k]);
+    }
   }
+  if (e->file_land) (void)hipEventDestroy(e->file_land);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->dstream) (void)hipStreamDestroy(e->dstream);
   for (hipEvent_t ev : {e->ev_dfree, e->ev_dready}) if (ev) (void)hipEventDestroy(ev);
@@ -1036,6 +1189,12 @@ int mox_count_file(mox_engine* e, const char* path, mox_table** out) {
   struct stat st;
   if (fstat(fd, &st) != 0) { close(fd); return fail(MOX_EIO, "cannot stat %s: %s", path, strerror(errno)); }
   const size_t len = (size_t)st.st_size;
+  if (len > 2 * MAP_RANGE && file_shared_stream()) {  // big file: the map overlaps the ingest
+    const int rc = run_file_overlapped(e, fd, len);
+    close(fd);
+    if (rc) return rc;
+    return mox_fetch_table(e, out);
+  }
   int rc = stage_file_range(e, fd, 0, len);
   close(fd);
   if (rc) return rc;

@@ -9,11 +9,14 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -27,7 +30,7 @@
 using namespace mox;
 
 extern "C" {
-__global__ void k_map(Corpus c, Work w, uint64_t ntiles);
+__global__ void k_map(Corpus c, Work w, uint64_t nrows, uint32_t resume);
 __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags);
 __global__ void k_ctl_out(const Ctl* src, Ctl* dst);
 __global__ void k_sample(Corpus c, Work w, uint32_t npieces);
@@ -117,7 +120,9 @@ struct mox_engine {
   // engine-owned corpus staging for host inputs
   uint8_t* d_text = nullptr;
   size_t d_text_cap = 0;
-  hipStream_t file_stream[16]{};  // mox_count_file readers (up to MAX_FILE_READERS)
+  hipStream_t file_stream[16]{};  // mox_count_file readers (up to MAX_FILE_READERS); [0] = the shared copy stream
+  hipEvent_t file_ev[16][2]{};    // copy of reader t's buffer k done (shared copy stream)
+  hipEvent_t file_land = nullptr; // overlapped file pass: copies of a byte prefix done (shared copy stream)
   uint8_t* file_pin[16][2]{};
   size_t file_pin_bytes = 0;      // size of each pinned reader buffer
   // last run

@@ -245,21 +245,12 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 // partition = top NB_LOG2 bits, dictionary home slot = low 12 bits, second
 // dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
 // bits.  Final table order is (h32, hash32b, key) (key_less), so it is deterministic.
-#ifndef MOX_HASH1
-#define MOX_HASH1 0  // A/B: one multiply in the key hash finaliser instead of two
-#endif
 __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   uint32_t a = k0 ^ __builtin_rotateleft32(k1, 11) ^ __builtin_rotateleft32(k2, 21) ^ __builtin_rotateleft32(k3, 6);
-#if MOX_HASH1
-  a ^= a >> 16;
-  a *= 0x7FEB352Du;
-  a ^= a >> 15;
-#else
   a *= 0x9E3779B1u;
   a ^= a >> 15;
   a *= 0x85EBCA6Bu;
   a ^= a >> 13;
-#endif
   // never 0: 0 marks a free slot in the dictionary and k_reduce tag arrays (a
   // key hashing to 0 would spin on a "free" slot); 1 simply shares its hash
   return max(collide32(a, MOX_H32_BITS), 1u);  // collide32: identity except in the collision build
@@ -587,12 +578,27 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
 }
 
 // Key of list entry e from the lowered slot: 24 bytes read at the 8-aligned
-// start, byte-aligned with v_alignbyte, masked to len bytes.
-__device__ __forceinline__ void key_at(const MapLds& s, const uint8_t* rowbuf, uint32_t e, uint32_t (&K)[4]) {
+// start, byte-aligned with v_alignbyte, masked to len bytes.  Split in two so
+// that a token pass can issue the LDS reads of all its batches before it uses
+// any of them (key_load for every batch, a scheduling barrier, then key_make):
+// left alone, the scheduler waited for each batch's reads before issuing the
+// next batch's, one LDS round trip per batch.
+struct KeyLd {
+  uint2 A, B, C;
+  uint4 M;
+};
+__device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf, uint32_t e, KeyLd& r) {
   const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
   const uint2* q = reinterpret_cast<const uint2*>(rowbuf + (pos & ~7u));
-  const uint2 A = q[0], B = q[1], C = q[2];
-  const uint4 M = s.masktab[len];
+  r.A = q[0];
+  r.B = q[1];
+  r.C = q[2];
+  r.M = s.masktab[len];
+}
+__device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
+  const uint32_t pos = e & 1023u;
+  const uint2 A = r.A, B = r.B, C = r.C;
+  const uint4 M = r.M;
   const bool o = (pos & 4u) != 0;
   const uint32_t E0 = o ? A.y : A.x, E1 = o ? B.x : A.y, E2 = o ? B.y : B.x, E3 = o ? C.x : B.y, E4 = o ? C.y : C.x;
   const uint32_t sh = pos & 3u;
@@ -601,6 +607,8 @@ __device__ __forceinline__ void key_at(const MapLds& s, const uint8_t* rowbuf, u
   K[2] = __builtin_amdgcn_alignbyte(E3, E2, sh) & M.z;
   K[3] = __builtin_amdgcn_alignbyte(E4, E3, sh) & M.w;
 }
+// compiler scheduling barrier: no instruction moves across it
+#define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
 // 16-byte key equality as one OR of XORs (kept opaque: the combiner would
 // otherwise split it into four compares and a boolean tree)
@@ -632,20 +640,27 @@ __device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbu
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
-    const uint32_t r = list[j < TOKMAX ? j : TOKMAX - 1];
-    e[u] = j < total ? r : 0x8000u;  // inactive = odd
+    e[u] = list[j < TOKMAX ? j : TOKMAX - 1];
   }
+  SCHED_FENCE();  // every batch's list read in flight before the first is used
+#pragma unroll
+  for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : 0x8000u;  // inactive = odd
+  KeyLd ld[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
+  SCHED_FENCE();
   uint32_t K[TU][4], home[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) key_at(m.s, rowbuf, e[u], K[u]);
+  for (int u = 0; u < TU; u++) key_make(e[u], ld[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) home[u] = dict_home(hash32(K[u][0], K[u][1], K[u][2], K[u][3]));
   uint4 dk[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) dk[u] = m.s.dkey[home[u]];
+  SCHED_FENCE();
   bool hit[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) hit[u] = !(e[u] & 0x8000u) && key_eq4(dk[u], K[u]);
+  for (int u = 0; u < TU; u++) hit[u] = !(e[u] & 0x8000u) & key_eq4(dk[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const bool valid = !(e[u] & 0x8000u);
@@ -669,20 +684,29 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
-    const uint32_t r = list[j < TOKMAX ? j : TOKMAX - 1];
-    valid[u] = j < nmiss;
-    e[u] = valid[u] ? r : 0u;
+    e[u] = list[j < TOKMAX ? j : TOKMAX - 1];
   }
+  SCHED_FENCE();
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    valid[u] = j0 + u * 64 + lane < nmiss;
+    e[u] = valid[u] ? e[u] : 0u;
+  }
+  KeyLd ld[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
+  SCHED_FENCE();
   uint32_t K[TU][4], h[TU];
   int slot[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    key_at(m.s, rowbuf, e[u], K[u]);
+    key_make(e[u], ld[u], K[u]);
     h[u] = hash32(K[u][0], K[u][1], K[u][2], K[u][3]);
   }
   uint4 t1[TU], t2[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) { t1[u] = m.s.dtag4[dict_g1(h[u])]; t2[u] = m.s.dtag4[dict_g2(h[u])]; }
+  SCHED_FENCE();
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t b1 = dict_g1(h[u]), b2 = dict_g2(h[u]);
@@ -699,9 +723,10 @@ __device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, c
   uint4 dk[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) dk[u] = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
+  SCHED_FENCE();
   bool hit[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) hit[u] = slot[u] >= 0 && key_eq4(dk[u], K[u]);
+  for (int u = 0; u < TU; u++) hit[u] = (slot[u] >= 0) & key_eq4(dk[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     if (!valid[u]) continue;
@@ -729,63 +754,24 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
-    const uint32_t r = list[j < TOKMAX ? j : TOKMAX - 1];
-    e[u] = j < total ? r : 0x8000u;  // inactive = odd
+    e[u] = list[j < TOKMAX ? j : TOKMAX - 1];
   }
+  SCHED_FENCE();  // every batch's list read in flight before the first is used
+#pragma unroll
+  for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : 0x8000u;  // inactive = odd
+  KeyLd ld[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
+  SCHED_FENCE();
   uint32_t K[TU][4];
 #pragma unroll
-  for (int u = 0; u < TU; u++) key_at(m.s, rowbuf, e[u], K[u]);
+  for (int u = 0; u < TU; u++) key_make(e[u], ld[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     if (e[u] & 0x8000u) continue;
     const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
     cold_word(m, hash32(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1);
   }
-}
-
-#ifndef MOX_MAP_DIRECT
-#define MOX_MAP_DIRECT 0  // A/B: pass A straight from the byte lanes' start masks, no token list
-#endif
-// Pass A without the token list (MOX_MAP_DIRECT): every lane walks its own
-// token starts (<= 16-byte tokens of its 16 bytes, `st`), two per iteration,
-// for the wave's largest start count; key, hash and home-slot probe as in
-// pass_a.  Misses are compacted into the list for pass B.
-__device__ __forceinline__ uint32_t direct_pass_a(const MapCtx& m, const uint8_t* rowbuf, uint16_t* list, uint32_t st,
-                                                  uint32_t ws32, uint32_t trips) {
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
-  const uint32_t lbase = (uint32_t)(lane * 16);
-  uint32_t nmiss = 0;
-  for (uint32_t it = 0; it < trips; it += 2) {
-    uint32_t e[2], K[2][4], home[2];
-    bool valid[2], hit[2];
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-      valid[u] = st != 0;
-      const uint32_t p = (uint32_t)__builtin_ctzg(st, -1) & 15u;
-      st &= st - 1;
-      const uint32_t len = (uint32_t)__builtin_ctzg(ws32 >> p, -1);
-      e[u] = valid[u] ? lbase + p + (len << 10) : 0x8000u;  // invalid: an empty key
-    }
-#pragma unroll
-    for (int u = 0; u < 2; u++) key_at(m.s, rowbuf, e[u], K[u]);
-#pragma unroll
-    for (int u = 0; u < 2; u++) home[u] = dict_home(hash32(K[u][0], K[u][1], K[u][2], K[u][3]));
-    uint4 dk[2];
-#pragma unroll
-    for (int u = 0; u < 2; u++) dk[u] = m.s.dkey[home[u]];
-#pragma unroll
-    for (int u = 0; u < 2; u++) hit[u] = valid[u] && key_eq4(dk[u], K[u]);
-#pragma unroll
-    for (int u = 0; u < 2; u++) {
-      if (hit[u]) atomicAdd(&m.s.dcnt[home[u]], 1u);
-      const bool miss = valid[u] && !hit[u];
-      const uint64_t bm = __ballot(miss);
-      if (miss) list[nmiss + (uint32_t)__popcll(bm & lt)] = (uint16_t)e[u];
-      nmiss += (uint32_t)__popcll(bm);
-    }
-  }
-  return nmiss;
 }
 
 // per-phase cycle accounting of a map consumer wave (-DMOX_STAMP builds only)
@@ -854,34 +840,6 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   const uint32_t pre = incl - cnt, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return;
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
-#if MOX_MAP_DIRECT
-  if (m.dict_n != 0 && !chk && !slow) {
-    uint32_t sm = ws32 >> 1;
-    sm |= sm >> 1;
-    sm |= sm >> 2;
-    sm |= sm >> 4;
-    sm |= sm >> 8;  // bit p: whitespace somewhere in bits p + 1 .. p + 16
-    uint32_t oddm = start & ~sm;  // tokens longer than 16 bytes
-    const uint32_t st = start & sm;
-    const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max((uint32_t)__popc(st)), 63);
-    wave_lds_fence();  // the lowered row before its key reads
-    if (__any(oddm != 0)) {
-      while (oddm) {
-        const uint32_t p = __builtin_ctz(oddm);
-        oddm &= oddm - 1;
-        generic_token(m, sbase + (uint64_t)lane * 16 + p);
-      }
-    }
-    const uint32_t nmiss = direct_pass_a(m, rowbuf, list, st, ws32, trips);
-    wave_lds_fence();
-    for (uint32_t j0 = 0; j0 < nmiss;) {
-      if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss); j0 += 128; }
-      else { pass_b<1>(m, rowbuf, list, j0, nmiss); j0 += 64; }
-    }
-    wave_lds_fence();
-    return;
-  }
-#endif
   // list entry (u16): slot offset (10 bits) | length (5 bits, <= 16) | odd (bit 15)
   uint32_t k = pre;
   bool any_odd = false;
@@ -969,7 +927,10 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
 //  * the other waves = consumers: take rows in order by ticket (dynamic load
 //    balance), process them from LDS (do_row) and release the slot.  Their
 //    cold-record stores are never waited for inside the loop.
-extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(Corpus c, Work w, uint64_t nrows) {
+// resume != 0: a further launch of the same pass over the next byte range (file
+// ingest overlapped with the map, mox_engine.hip run_file_overlapped): the
+// region and spill counters continue from what the earlier launches wrote.
+extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(Corpus c, Work w, uint64_t nrows, uint32_t resume) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   MapCtx m;
   m.c = c;
@@ -1009,10 +970,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     m.s.dcnt[i] = 0;
   }
   for (int i = tid; i < NB; i += MAP_THREADS) {
-    m.s.bcnt[i] = 0;
+    m.s.bcnt[i] = resume ? w.cold_n[(uint64_t)blockIdx.x * NB + i] : 0u;
     if (MOX_DICT_PAIRS) m.s.pst[i] = PS_EMPTY;
   }
-  if (tid < 4) m.s.misc[tid] = 0;
+  if (tid < 4) m.s.misc[tid] = (resume && tid == 0) ? w.spill_n[blockIdx.x] : 0u;
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
   if (tid < 17) {
     uint32_t mk[4];
@@ -1838,31 +1799,11 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   } while (__any(!done));
 }
 
-#ifndef MOX_RED_KEYPROBE
-#define MOX_RED_KEYPROBE 0  // A/B: fast path compares the home bucket's keys directly (1; 2: and the next bucket's)
-#endif
 // Fast path for records whose key is already published in its home bucket or
 // the next one (keys overflow at most one bucket at this table load): two tag
 // reads issued together, one key read, one add.  Returns false when the slow
 // path is needed (new key, further bucket, publication pending).
-// MOX_RED_KEYPROBE: the bucket's four keys are read at once and compared with
-// the record's (one LDS round trip instead of two); keys are zeroed with the
-// tags at every sub-pass, so a key equal to the record's was written in this
-// sub-pass by the slot's claimant, and adding to its count is exact whether or
-// not the claimant has published yet (the adds commute).
 __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
-#if MOX_RED_KEYPROBE
-  const uint32_t b = red_bucket(h);
-  uint4 kb[4 * MOX_RED_KEYPROBE];
-#pragma unroll
-  for (int i = 0; i < 4 * MOX_RED_KEYPROBE; i++) kb[i] = s.key[(4 * b + i) % RED_SLOTS];
-  int sl = -1;
-#pragma unroll
-  for (int i = 4 * MOX_RED_KEYPROBE - 1; i >= 0; i--) sl = key_eq16(kb[i], k) ? (int)((4 * b + i) % RED_SLOTS) : sl;
-  if (sl < 0) return false;
-  atomicAdd(&s.cnt[sl], (unsigned long long)c);
-  return true;
-#else
   const uint32_t b = red_bucket(h), b2 = b + 1 == RED_BK ? 0 : b + 1;
   const uint4 t = s.tag4[b], t2 = s.tag4[b2];
   int sl = t2.w == h ? (int)(4 * b2 + 3) : -1;
@@ -1880,7 +1821,52 @@ __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, ui
   if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
   else atomicAdd(&s.cnt[sl], (unsigned long long)c);
   return true;
-#endif
+}
+
+// red_try over a chunk's U records of one lane at once: every record's tag
+// reads are issued before any is used, then every key / count read (left to
+// itself, the scheduler probed the records one after the other: two LDS round
+// trips per record instead of two per chunk).  todo[u]: the record still needs
+// the slow path.
+template <int U>
+__device__ __forceinline__ void red_try_batch(const RedLds& s, const uint32_t (&h)[U], const uint4 (&k)[U], bool (&todo)[U]) {
+  uint4 t[U], t2[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t b = red_bucket(h[u]), b2 = b + 1 == RED_BK ? 0 : b + 1;
+    t[u] = s.tag4[b];
+    t2[u] = s.tag4[b2];
+  }
+  SCHED_FENCE();
+  int sl[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t b = red_bucket(h[u]), b2 = b + 1 == RED_BK ? 0 : b + 1;
+    int x = t2[u].w == h[u] ? (int)(4 * b2 + 3) : -1;
+    x = t2[u].z == h[u] ? (int)(4 * b2 + 2) : x;
+    x = t2[u].y == h[u] ? (int)(4 * b2 + 1) : x;
+    x = t2[u].x == h[u] ? (int)(4 * b2 + 0) : x;
+    x = t[u].w == h[u] ? (int)(4 * b + 3) : x;
+    x = t[u].z == h[u] ? (int)(4 * b + 2) : x;
+    x = t[u].y == h[u] ? (int)(4 * b + 1) : x;
+    x = t[u].x == h[u] ? (int)(4 * b + 0) : x;
+    sl[u] = x;
+  }
+  uint4 kk[U];
+  unsigned long long cv[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const int q = sl[u] < 0 ? 0 : sl[u];
+    kk[u] = s.key[q];
+    cv[u] = __hip_atomic_load(&s.cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  SCHED_FENCE();
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const bool ok = todo[u] & (sl[u] >= 0) & (cv[u] != 0) & key_eq16(kk[u], k[u]);
+    if (ok) atomicAdd(&s.cnt[sl[u]], 1ull);
+    todo[u] = todo[u] & !ok;
+  }
 }
 
 // Table order of short words: (h32, hash32b, key).  Every reduce kernel uses
@@ -2310,7 +2296,6 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       for (int i = tid; i < RED_SLOTS; i += RED_THREADS) {
         tags[i] = 0;
         s.cnt[i] = 0;
-        if (MOX_RED_KEYPROBE) s.key[i] = make_uint4(0, 0, 0, 0);
       }
       if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
 #if MOX_RED_FLAT
@@ -2380,9 +2365,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
+            if (!s.plain) red_try_batch<RED_UNROLL>(s, h, cur, todo);
+            else {
 #pragma unroll
-            for (int u2 = 0; u2 < RED_UNROLL; u2++)
-              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+              for (int u2 = 0; u2 < RED_UNROLL; u2++)
+                if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+            }
             RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
@@ -2458,9 +2446,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
+            if (!s.plain) red_try_batch<RED_UNROLL>(s, h, cur, todo);
+            else {
 #pragma unroll
-            for (int u2 = 0; u2 < RED_UNROLL; u2++)
-              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+              for (int u2 = 0; u2 < RED_UNROLL; u2++)
+                if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+            }
             RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)

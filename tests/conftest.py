@@ -49,9 +49,32 @@ def canon_table(counts, offs, raw):
     return keys[order], counts[order]
 
 
+def split_long(counts, offs, raw, width=64):
+    """(short table, long words): words longer than `width` bytes leave the table
+    as a sorted list of (bytes, count), so canon_table's fixed-width matrix
+    stays narrow when a corpus holds a few very long tokens."""
+    import numpy as np
+    counts = np.asarray(counts, dtype=np.uint64)
+    offs = np.asarray(offs, dtype=np.int64)
+    lens = np.diff(offs)
+    longi = np.nonzero(lens > width)[0]
+    if longi.size == 0:
+        return (counts, offs, raw), []
+    longw = sorted((raw[offs[i]:offs[i + 1]], int(counts[i])) for i in longi)
+    keep = np.nonzero(lens <= width)[0]
+    klen = lens[keep]
+    koffs = np.zeros(keep.size + 1, np.int64)
+    np.cumsum(klen, out=koffs[1:])
+    buf = np.frombuffer(raw, np.uint8)
+    idx = np.repeat(offs[keep], klen) + (np.arange(int(koffs[-1])) - np.repeat(koffs[:-1], klen))
+    return (counts[keep], koffs, buf[idx].tobytes()), longw
+
+
 def assert_tables_equal(a, b):
     """a, b: (counts, offs, raw) word tables; equal as (word, count) multisets."""
     import numpy as np
+    (a, la), (b, lb) = split_long(*a), split_long(*b)
+    assert la == lb
     ka, ca = canon_table(*a)
     kb, cb = canon_table(*b)
     assert ka.size == kb.size, (ka.size, kb.size)

@@ -336,6 +336,47 @@ def test_count_file_streamed_chunks(tmp_path, eng):
         eng.count_file(str(tmp_path / "missing.txt"))
 
 
+def test_count_file_overlapped_map(tmp_path, eng):
+    """Files over 128 MiB: the map runs one launch per 64 MiB range as soon as
+    that range and the next have landed, while later chunks are still being
+    read (mox_engine.hip run_file_overlapped), and the region counters carry
+    over between launches.  Tokens straddling the range ends (a 2-byte UTF-8
+    letter, a 5,100-byte long word), a ragged tail, a token longer than the
+    look-ahead (falls back to the ordinary pass) and an invalid byte in the
+    third range (error offset) must all match the ordinary pass."""
+    from conftest import assert_tables_equal
+    R = 64 << 20
+    n = 3 * R + 777777
+    data = bytearray(corpus.fill(corpus.ZIPF, 41, 0, n).tobytes())
+    data[R - 4:R + 4] = b" ab\xce\xa3cd "        # "ab\u03a3cd" across the first range end
+    data[2 * R - 100:2 * R + 5000] = b"x" * 5100     # a long word across the second
+    data[-3:] = b"Zq!"                                # ragged tail ending in a word
+    f = tmp_path / "big.txt"
+    f.write_bytes(bytes(data))
+    t = eng.count_file(str(f))
+    got = t.arrays()
+    t.close()
+    wc, wo, wraw, _ = coracle.count_arrays(np.frombuffer(bytes(data), np.uint8), nthreads=16)
+    assert_tables_equal(got, (wc, wo, wraw))
+    # a token running past the next range (the look-ahead): ordinary pass on the resident file
+    data2 = bytearray(data)
+    data2[R - 10:2 * R + 10] = b"y" * (R + 20)
+    f.write_bytes(bytes(data2))
+    t = eng.count_file(str(f))
+    got = t.arrays()
+    t.close()
+    wc, wo, wraw, _ = coracle.count_arrays(np.frombuffer(bytes(data2), np.uint8), nthreads=16)
+    assert_tables_equal(got, (wc, wo, wraw))
+    # invalid UTF-8 in the third range: the error names the file offset
+    bad = 2 * R + 12345
+    data[bad] = 0xFF
+    f.write_bytes(bytes(data))
+    with pytest.raises(mox.Utf8Error) as ei:
+        eng.count_file(str(f))
+    assert "byte %d" % bad in str(ei.value)
+    assert gpu_items(eng, b"a b a") == [(b"a", 2), (b"b", 1)]
+
+
 def test_async_passes():
     """mox_run_range_async: back-to-back passes, each completed by the next call
     (or run_wait / fetch); the table is the last pass's; overflow retries and
