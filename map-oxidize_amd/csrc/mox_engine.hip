@@ -213,9 +213,8 @@ int alloc_fixed(mox_engine* e) {
   return MOX_OK;
 }
 
-constexpr size_t map_lds_bytes() { return DICT_SLOTS * (4 + 16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX +
-                                 (MOX_DICT_PAIRS ? NB * 20 : 0); }
-static_assert(map_lds_bytes() <= 160 * 1024, "k_map LDS over 160 KiB (MOX_DICT_PAIRS needs MOX_RING <= 24)");
+constexpr size_t map_lds_bytes() { return DICT_SLOTS * (16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
+static_assert(map_lds_bytes() <= 160 * 1024, "k_map LDS over 160 KiB");
 size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
 
 float ev_ms(mox_engine* e, int a, int b) {
@@ -487,7 +486,7 @@ void debug_dump(mox_engine* e, const Ctl& h) {
       const int i = order[j];
       char wbuf[17] = {0};
       memcpy(wbuf, &dk[i], 16);
-      fprintf(stderr, "[mox]   slot %d home %d total %llu key '%s'\n", i, (int)(dt[i] & (DICT_SLOTS - 1)), tot[i], wbuf);
+      fprintf(stderr, "[mox]   slot %d tag %08x total %llu key '%s'\n", i, dt[i], tot[i], wbuf);
     }
   }
 }

@@ -7,16 +7,6 @@
 namespace mox {
 
 // ---- geometry ----
-#ifdef MOX_MAP2
-// experiment: two map workgroups per CU (1 loader + 9 consumers each, 2,048-slot dictionary)
-constexpr int MAP_THREADS = 640;
-constexpr int MAP_WG_PER_CU = 2;
-constexpr int MAP_MIN_WAVES = 5;            // per SIMD: 2 workgroups x 10 waves / 4 SIMDs
-constexpr int MAP_LOADERS = 1;
-constexpr int RING = 16;
-constexpr int DICT_BUCKETS = 512;
-constexpr int DICT_MAX_WORDS = 1792;
-#else
 constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
 constexpr int MAP_WG_PER_CU = 1;
 constexpr int MAP_MIN_WAVES = 1;
@@ -30,16 +20,18 @@ constexpr int MAP_LOADERS = MOX_MAP_LOADERS;  // loader waves (alternate row gro
 #ifndef MOX_CO_SLEEP
 #define MOX_CO_SLEEP 1  // k_map consumer's poll for a loaded row
 #endif
-#ifndef MOX_DICT_PAIRS
-#define MOX_DICT_PAIRS 0  // k_map pairs cold records with a dictionary too (own LDS slots: needs RING <= 24)
-#endif
 #ifndef MOX_RING
 #define MOX_RING 32
 #endif
 constexpr int RING = MOX_RING;              // k_map row ring slots (LDS)
-constexpr int DICT_BUCKETS = 1024;          // LDS hot dictionary: 2-choice buckets of 4 slots
-constexpr int DICT_MAX_WORDS = 3584;
+#ifndef MOX_DICT_SLOTS
+#define MOX_DICT_SLOTS 5120
 #endif
+// LDS hot dictionary: single-word slots, two choices per word (dict_s1 / dict_s2,
+// mox_kernels.hip); k_dict_pick picks up to DICT_MAX_WORDS candidates
+constexpr int DICT_SLOTS = MOX_DICT_SLOTS;
+constexpr int DICT_MAX_WORDS = 4096;
+static_assert(DICT_SLOTS % 32 == 0 && DICT_SLOTS <= 65536 && DICT_MAX_WORDS <= DICT_SLOTS, "dictionary geometry");
 constexpr int MAX_MAP_GRID = 1024;          // map workgroups
 constexpr int MAP_WAVES = MAP_THREADS / 64;
 constexpr int ROW = 1024;                   // bytes one wave classifies per step (64 lanes x 16 B)
@@ -61,7 +53,6 @@ constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
-constexpr int DICT_SLOTS = 4 * DICT_BUCKETS;
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;
 constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B
@@ -205,7 +196,7 @@ __host__ __device__ __forceinline__ uint64_t fnv_finish(uint64_t h) {
 // compiled in with -DMOX_PATHS (the collision build), so tests can assert that
 // the path they target ran.
 enum : uint32_t {
-  PATH_DICT_TAG = 0,      // k_map pass B: dictionary tag equal, key different -> full dictionary search
+  PATH_DICT_SAMEHASH = 0, // k_map: a slot holds another word with the token's 32-bit hash (key compare rejects it)
   PATH_LONG_EQHASH = 1,   // long-word table: equal FNV hash, different bytes -> probe on
   PATH_SORT_RESORT = 2,   // k_reduce_sort1/2: two keys share the 23-bit sort key -> 64-bit re-sort
   PATH_SORT_TO_RED = 3,   // k_reduce_sort1/2: two keys share (h32, hash32b) -> unit goes to k_reduce
@@ -326,7 +317,7 @@ struct Work {  // device buffers of one engine
   uint32_t* dict_hist;            // [256] candidate count histogram, [256] picked words (classes >= T), [257] class T - 1 words,
                                   // [DH_N] dictionary words, [DH_T] threshold (the pass's, read by k_map / k_unicode)
   WRec* dict_list;                // DICT_MAX_WORDS picked words
-  uint32_t* dict_tag;             // DICT_SLOTS key hashes (0 = empty), bucket b = slots 4b..4b+3
+  uint32_t* dict_tag;             // DICT_SLOTS key hashes (0 = empty slot)
   uint4* dict_key;                // DICT_SLOTS lowered 16-byte keys
   unsigned long long* dict_tot;   // DICT_SLOTS counts summed over map workgroups
   // cold records: region (map workgroup g, partition b) = cold[(g*NB + b)*cold_cap ...]

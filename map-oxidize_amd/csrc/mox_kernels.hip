@@ -259,28 +259,34 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   return hash32((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
 }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - NB_LOG2); }
+// Records map workgroup g wrote into its region of partition b.  Partition-major
+// (b * map_grid + g): a partition's row is contiguous for k_hist's sums, k_reduce's
+// region prefix and the split kernels' region lists.
+__device__ __forceinline__ uint32_t& cold_n_at(const Work& w, uint32_t g, uint32_t b) {
+  return w.cold_n[(uint64_t)b * w.map_grid + g];
+}
 // byte length of a short key (lowered word, zero padded to 16 bytes, no NUL inside)
 __device__ __forceinline__ uint32_t key_len16(uint4 k) {
   const uint64_t w0 = ((uint64_t)k.y << 32) | k.x, w1 = ((uint64_t)k.w << 32) | k.z;
   if (w1) return 16 - (__clzll(w1) >> 3);
   return 8 - (__clzll(w0) >> 3);
 }
-// Dictionary: DICT_SLOTS slots in groups of 4.  A word sits in its home slot
-// (h mod DICT_SLOTS) when that was free at build time (words are placed
-// hottest first), else in a free slot of its home group, else of its second
-// group.  The token phase checks the home slot first and the two groups only
-// for the tokens that miss there.
-__device__ __forceinline__ uint32_t dict_home(uint32_t h) { return h & (DICT_SLOTS - 1); }
-__device__ __forceinline__ uint32_t dict_g1(uint32_t h) { return (h & (DICT_SLOTS - 1)) >> 2; }
-__device__ __forceinline__ uint32_t dict_g2(uint32_t h) { return (h >> 12) & (DICT_BUCKETS - 1); }
+// Dictionary: DICT_SLOTS single-word slots, two choices per word (s1 from the
+// low 16 hash bits, s2 from the high 16).  k_dict_build places the words hottest
+// first into s1, else s2, else leaves the word cold (2-choice greedy: ~98 % of
+// the picked words' sampled tokens placed).  The token pass reads both slots'
+// keys at once and compares them with the token's key, so a lookup is one LDS
+// round trip and decides the token: a hit counts in LDS, a miss is cold.  No
+// tags, no second probe pass.
+__device__ __forceinline__ uint32_t dict_s1(uint32_t h) { return ((h & 0xFFFFu) * (uint32_t)DICT_SLOTS) >> 16; }
+__device__ __forceinline__ uint32_t dict_s2(uint32_t h) { return ((h >> 16) * (uint32_t)DICT_SLOTS) >> 16; }
 
 // LDS pair slot states (k_map without a dictionary, k_split_scatter): a
 // record waits in its slot until the next record for the same region arrives,
 // and the pair goes out as one aligned 32-byte sector.
 constexpr uint32_t PS_EMPTY = 0u, PS_BUSY = 1u, PS_FULL = 2u;
 struct MapLds {
-  uint4* dtag4;     // DICT_BUCKETS x 4 tags (0 = empty)
-  uint4* dkey;      // DICT_SLOTS 16-byte keys
+  uint4* dkey;      // DICT_SLOTS 16-byte keys (zero = empty: a real key is never zero)
   uint32_t* dcnt;   // DICT_SLOTS
   uint32_t* bcnt;   // NB: cold records this workgroup wrote per partition
   uint32_t* misc;   // [0] spills [1] row ticket
@@ -312,20 +318,12 @@ __device__ __forceinline__ KWork rare_ptr(const MapCtx& m) {
 __device__ __forceinline__ bool key_eq(uint4 k, uint64_t w0, uint64_t w1) {
   return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && k.w == (uint32_t)(w1 >> 32);
 }
-// slot of bucket b whose tag is h and whose key is (w0, w1), or -1
-__device__ __forceinline__ int bucket_find(const MapLds& s, uint32_t b, uint4 t, uint32_t h, uint64_t w0, uint64_t w1) {
-  if (t.x == h && key_eq(s.dkey[4 * b + 0], w0, w1)) return (int)(4 * b + 0);
-  if (t.y == h && key_eq(s.dkey[4 * b + 1], w0, w1)) return (int)(4 * b + 1);
-  if (t.z == h && key_eq(s.dkey[4 * b + 2], w0, w1)) return (int)(4 * b + 2);
-  if (t.w == h && key_eq(s.dkey[4 * b + 3], w0, w1)) return (int)(4 * b + 3);
-  return -1;
-}
-// Exact dictionary lookup over both groups of the key.
+// Exact dictionary lookup: the key's two slots.
 __device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w0, uint64_t w1) {
-  const uint32_t g1 = dict_g1(h), g2 = dict_g2(h);
-  int slot = bucket_find(s, g1, s.dtag4[g1], h, w0, w1);
-  if (slot < 0) slot = bucket_find(s, g2, s.dtag4[g2], h, w0, w1);
-  return slot;
+  const uint32_t s1 = dict_s1(h), s2 = dict_s2(h);
+  if (key_eq(s.dkey[s1], w0, w1)) return (int)s1;
+  if (key_eq(s.dkey[s2], w0, w1)) return (int)s2;
+  return -1;
 }
 
 __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1);
@@ -421,7 +419,7 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-  if (MOX_DICT_PAIRS || m.dict_n == 0) { cold_pair(m, b, h, key); return; }
+  if (m.dict_n == 0) { cold_pair(m, b, h, key); return; }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < SPLIT_PER_REGION) note_sample(m, b, pos, h);
   if (pos < m.w.cold_cap) {
@@ -624,18 +622,16 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
   return (o | d3) == 0;
 }
 
-// Token pass A over TU batches of 64 list entries (lane = token): key, hash,
-// one LDS read of the home slot.  Hits count in LDS; misses are compacted in
-// place to the front of the list (entry index <= read index, and every read of
-// this call precedes its writes).  Returns the new miss count.  Branch-free up
-// to the hit test, so the TU batches' LDS reads are issued together (the
-// dictionary arrays are zero when there is no dictionary: a real key is never
-// zero, so nothing hits).
+// Token pass over TU batches of 64 list entries (lane = token): key, hash, both
+// dictionary slots' keys read at once, then an LDS count (hit) or the cold
+// store (miss), so every token is decided in one LDS round trip.  All LDS reads
+// of a phase are issued before the first is used (SCHED_FENCE).  The
+// dictionary arrays are zero when there is no dictionary (a real key is never
+// zero, so nothing hits), but that case takes pass_c.
 template <int TU>
-__device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbuf, uint16_t* list, uint32_t j0,
-                                           uint32_t total, uint32_t nmiss) {
+__device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
+                                       uint32_t total) {
   const int lane = threadIdx.x & 63;
-  const uint64_t lt = (1ull << lane) - 1ull;
   uint32_t e[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
@@ -649,98 +645,31 @@ __device__ __forceinline__ uint32_t pass_a(const MapCtx& m, const uint8_t* rowbu
 #pragma unroll
   for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
   SCHED_FENCE();
-  uint32_t K[TU][4], home[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) key_make(e[u], ld[u], K[u]);
-#pragma unroll
-  for (int u = 0; u < TU; u++) home[u] = dict_home(hash32(K[u][0], K[u][1], K[u][2], K[u][3]));
-  uint4 dk[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) dk[u] = m.s.dkey[home[u]];
-  SCHED_FENCE();
-  bool hit[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) hit[u] = !(e[u] & 0x8000u) & key_eq4(dk[u], K[u]);
-#pragma unroll
-  for (int u = 0; u < TU; u++) {
-    const bool valid = !(e[u] & 0x8000u);
-    if (hit[u] && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[home[u]], 1u);
-    const bool miss = valid && !hit[u];
-    const uint64_t bm = __ballot(miss);
-    if (miss) list[nmiss + (uint32_t)__popcll(bm & lt)] = (uint16_t)e[u];
-    nmiss += (uint32_t)__popcll(bm);
-  }
-  return nmiss;
-}
-
-// Token pass B over TU batches of 64 compacted misses: both dictionary groups
-// (8 tags), key check, then an LDS count or the cold store.
-template <int TU>
-__device__ __forceinline__ void pass_b(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t nmiss) {
-  const int lane = threadIdx.x & 63;
-  uint32_t e[TU];
-  bool valid[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) {
-    const uint32_t j = j0 + u * 64 + lane;
-    e[u] = list[j < TOKMAX ? j : TOKMAX - 1];
-  }
-  SCHED_FENCE();
-#pragma unroll
-  for (int u = 0; u < TU; u++) {
-    valid[u] = j0 + u * 64 + lane < nmiss;
-    e[u] = valid[u] ? e[u] : 0u;
-  }
-  KeyLd ld[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
-  SCHED_FENCE();
-  uint32_t K[TU][4], h[TU];
-  int slot[TU];
+  uint32_t K[TU][4], h[TU], s1[TU], s2[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     key_make(e[u], ld[u], K[u]);
     h[u] = hash32(K[u][0], K[u][1], K[u][2], K[u][3]);
+    s1[u] = dict_s1(h[u]);
+    s2[u] = dict_s2(h[u]);
   }
-  uint4 t1[TU], t2[TU];
+  uint4 d1[TU], d2[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) { t1[u] = m.s.dtag4[dict_g1(h[u])]; t2[u] = m.s.dtag4[dict_g2(h[u])]; }
+  for (int u = 0; u < TU; u++) { d1[u] = m.s.dkey[s1[u]]; d2[u] = m.s.dkey[s2[u]]; }
   SCHED_FENCE();
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    const uint32_t b1 = dict_g1(h[u]), b2 = dict_g2(h[u]);
-    int sl = t2[u].w == h[u] ? (int)(4 * b2 + 3) : -1;
-    sl = t2[u].z == h[u] ? (int)(4 * b2 + 2) : sl;
-    sl = t2[u].y == h[u] ? (int)(4 * b2 + 1) : sl;
-    sl = t2[u].x == h[u] ? (int)(4 * b2 + 0) : sl;
-    sl = t1[u].w == h[u] ? (int)(4 * b1 + 3) : sl;
-    sl = t1[u].z == h[u] ? (int)(4 * b1 + 2) : sl;
-    sl = t1[u].y == h[u] ? (int)(4 * b1 + 1) : sl;
-    sl = t1[u].x == h[u] ? (int)(4 * b1 + 0) : sl;
-    slot[u] = sl;
-  }
-  uint4 dk[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) dk[u] = m.s.dkey[slot[u] < 0 ? 0 : slot[u]];
-  SCHED_FENCE();
-  bool hit[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) hit[u] = (slot[u] >= 0) & key_eq4(dk[u], K[u]);
-#pragma unroll
-  for (int u = 0; u < TU; u++) {
-    if (!valid[u]) continue;
-    const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
-    if (hit[u]) {
-      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot[u]], 1u);
-      continue;
+    const bool valid = !(e[u] & 0x8000u);
+    const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
+    if (valid & (hit1 | hit2)) {
+      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[hit1 ? s1[u] : s2[u]], 1u);
+    } else if (valid) {
+#if defined(MOX_PATHS) && MOX_PATHS
+      if ((d1[u].x | d1[u].y | d1[u].z | d1[u].w) && hash32(d1[u].x, d1[u].y, d1[u].z, d1[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
+      if ((d2[u].x | d2[u].y | d2[u].z | d2[u].w) && hash32(d2[u].x, d2[u].y, d2[u].z, d2[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
+#endif
+      cold_word(m, h[u], ((uint64_t)K[u][1] << 32) | K[u][0], ((uint64_t)K[u][3] << 32) | K[u][2]);
     }
-    if (slot[u] >= 0) {  // tag matched another word: full search (rare)
-      MOX_PATH(rare(m).ctl, PATH_DICT_TAG);
-      const int s2 = dict_find(m.s, h[u], w0, w1);
-      if (s2 >= 0) { atomicAdd(&m.s.dcnt[s2], 1u); continue; }
-    }
-    cold_word(m, h[u], w0, w1);
   }
 }
 
@@ -787,7 +716,8 @@ struct Cyc {
 //     Unicode walk on rows with non-ASCII bytes), the lowered slot back into LDS
 //     and a compacted list of token (slot offset, length) in row order (wave
 //     prefix sum of per-lane start counts from 5 bit-sliced ballots);
-//  2. token phase (lane = token): pass_a over all tokens, pass_b over its misses.
+//  2. token phase (lane = token): pass_a over all tokens (both dictionary slots
+//     read at once: an LDS count on a hit, the cold store on a miss).
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
                                        uint16_t* list, struct Cyc* cyc) {
   const int lane = threadIdx.x & 63;
@@ -898,21 +828,13 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     wave_lds_fence();
     return;
   }
-  uint32_t nmiss = 0;
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
-    if (rem > 128) { nmiss = pass_a<3>(m, rowbuf, list, j0, total, nmiss); j0 += 192; }
-    else if (rem > 64) { nmiss = pass_a<2>(m, rowbuf, list, j0, total, nmiss); j0 += 128; }
-    else { nmiss = pass_a<1>(m, rowbuf, list, j0, total, nmiss); j0 += 64; }
+    if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, total); j0 += 192; }
+    else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, total); j0 += 128; }
+    else { pass_a<1>(m, rowbuf, list, j0, total); j0 += 64; }
   }
-  wave_lds_fence();
-  uint64_t t2 = 0;
-  if (cyc) { t2 = __builtin_amdgcn_s_memtime(); cyc->pa += t2 - t1; }
-  for (uint32_t j0 = 0; j0 < nmiss;) {
-    if (nmiss - j0 > 64) { pass_b<2>(m, rowbuf, list, j0, nmiss); j0 += 128; }
-    else { pass_b<1>(m, rowbuf, list, j0, nmiss); j0 += 64; }
-  }
-  if (cyc) { cyc->pb += __builtin_amdgcn_s_memtime() - t2; cyc->miss += nmiss; }
+  if (cyc) cyc->pa += __builtin_amdgcn_s_memtime() - t1;
   wave_lds_fence();
 }
 
@@ -940,7 +862,6 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.wk = (KWork)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
                  ((sizeof(Corpus) + alignof(Work) - 1) & ~(alignof(Work) - 1)));
   uint8_t* sp = smem;
-  m.s.dtag4 = (uint4*)sp; sp += DICT_SLOTS * 4;
   m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
@@ -950,28 +871,20 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
   uint16_t* lists = (uint16_t*)sp; sp += MAP_CONSUMERS * 2 * TOKMAX;
-#if MOX_DICT_PAIRS
-  m.s.pend = (uint4*)sp; sp += NB * 16;              // pair slots of their own (dictionary path too)
-  m.s.pst = (uint32_t*)sp;
-#else
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB);       // = PS_EMPTY
   static_assert(NB * 16 + NB * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
-#endif
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
-  // the token passes probe unconditionally: without a dictionary the arrays are
-  // zero (no real key is zero, so nothing hits)
-  for (int i = tid; i < DICT_BUCKETS; i += MAP_THREADS)
-    m.s.dtag4[i] = m.dict_n ? reinterpret_cast<const uint4*>(w.dict_tag)[i] : make_uint4(0, 0, 0, 0);
+  // without a dictionary the key array is zero (no real key is zero, so nothing
+  // would hit; that case takes pass_c, and the pair slots live there)
   for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
     m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);
     m.s.dcnt[i] = 0;
   }
   for (int i = tid; i < NB; i += MAP_THREADS) {
-    m.s.bcnt[i] = resume ? w.cold_n[(uint64_t)blockIdx.x * NB + i] : 0u;
-    if (MOX_DICT_PAIRS) m.s.pst[i] = PS_EMPTY;
+    m.s.bcnt[i] = resume ? cold_n_at(w, blockIdx.x, i) : 0u;
   }
   if (tid < 4) m.s.misc[tid] = (resume && tid == 0) ? w.spill_n[blockIdx.x] : 0u;
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
@@ -1069,7 +982,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #endif
   }
   __syncthreads();
-  if (MOX_DICT_PAIRS || m.dict_n == 0) {  // records still parked in pair slots: written as singles
+  if (m.dict_n == 0) {  // records still parked in pair slots: written as singles
     for (int i = tid; i < NB; i += MAP_THREADS) {
       if (m.s.pst[i] != PS_FULL) continue;
       const uint32_t pos = atomicAdd(&m.s.bcnt[i], 1u);
@@ -1095,7 +1008,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint32_t cmax = 0;
   for (int i = tid; i < NB; i += MAP_THREADS) {
     const uint32_t cnt = m.s.bcnt[i];
-    w.cold_n[(uint64_t)blockIdx.x * NB + i] = cnt < w.cold_cap ? cnt : w.cold_cap;
+    cold_n_at(w, blockIdx.x, i) = cnt < w.cold_cap ? cnt : w.cold_cap;
     for (uint32_t j = cnt; j < SPLIT_PER_REGION; j++) note_sample(m, i, j, 0u);  // no record there (0 = none)
     cmax = cnt > cmax ? cnt : cmax;
   }
@@ -1390,13 +1303,17 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
 
 extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t max_words) {
   __shared__ uint32_t ltag[DICT_SLOTS];
+  __shared__ uint16_t lword[DICT_SLOTS];                      // word (dict_list index) in each slot
+  __shared__ uint32_t klock[DICT_SLOTS / 32];                 // relocation locks, one bit per slot (one phase)
   __shared__ uint2 lk0[DICT_MAX_WORDS], lk1[DICT_MAX_WORDS];  // picked keys, staged once
   __shared__ uint8_t lcl[DICT_MAX_WORDS];                     // log2 count class
   __shared__ uint16_t order[DICT_MAX_WORDS];                  // words grouped by class, hottest first
+  __shared__ uint16_t fails[DICT_MAX_WORDS];                  // words of the current class with both slots taken
   __shared__ uint32_t ccnt[32], cstart[33], cfill[32];
-  __shared__ uint32_t nsel;
+  __shared__ uint32_t nsel, nfail;
   const int tid = threadIdx.x;
-  for (int i = tid; i < DICT_SLOTS; i += 1024) { ltag[i] = 0; w.dict_key[i] = make_uint4(0, 0, 0, 0); }
+  for (int i = tid; i < DICT_SLOTS; i += 1024) ltag[i] = 0;
+  for (int i = tid; i < DICT_SLOTS / 32; i += 1024) klock[i] = 0;
   if (tid < 32) { ccnt[tid] = 0; cfill[tid] = 0; }
   if (tid == 0) nsel = 0;
   uint32_t n = w.dict_hist[256] + w.dict_hist[257];  // classes >= T, then the partial class T - 1
@@ -1420,33 +1337,66 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_build(Work w, uint32_t
   for (uint32_t i = tid; i < n; i += 1024) order[cstart[lcl[i]] + atomicAdd(&cfill[lcl[i]], 1u)] = (uint16_t)i;
   __syncthreads();
   // insert by descending log2 count class, so that a word dropped because both
-  // of its groups are full is never hotter than the words that filled them;
-  // one barrier per non-empty class
+  // of its slots are taken is never hotter than the words that took them.  Per
+  // class: every word claims its first free slot of (s1, s2); then a word with
+  // both taken tries one relocation (cuckoo step): the occupant of one of its
+  // slots moves to that occupant's other slot if it is free, and the word takes
+  // its place.  A slot is touched by at most one relocation per phase (klock:
+  // the kicked slot and the occupant's new slot are both locked), so no
+  // relocation reads a slot another one is rewriting.
   for (int cl = 31; cl >= 0; cl--) {
     const uint32_t c0 = cstart[cl], c1 = c0 + ccnt[cl];
     if (c0 == c1) continue;  // uniform
+    if (tid == 0) nfail = 0;
+    __syncthreads();
     for (uint32_t j = c0 + tid; j < c1; j += 1024) {
       const uint32_t i = order[j];
       const uint2 a = lk0[i], b = lk1[i];
       const uint32_t h = hash32(a.x, a.y, b.x, b.y);
-      if (h == 0) continue;  // tag 0 marks an empty slot
       int slot = -1;
-      if (atomicCAS(&ltag[dict_home(h)], 0u, h) == 0u) slot = (int)dict_home(h);
-      for (int k = 0; k < 4 && slot < 0; k++) {
-        const uint32_t s1 = 4 * dict_g1(h) + k;
-        if (atomicCAS(&ltag[s1], 0u, h) == 0u) slot = (int)s1;
-      }
-      for (int k = 0; k < 4 && slot < 0; k++) {
-        const uint32_t s2 = 4 * dict_g2(h) + k;
-        if (atomicCAS(&ltag[s2], 0u, h) == 0u) slot = (int)s2;
-      }
-      if (slot < 0) continue;  // both groups full: this word stays cold
-      w.dict_key[slot] = make_uint4(a.x, a.y, b.x, b.y);
-      atomicAdd(&nsel, 1u);
+      if (atomicCAS(&ltag[dict_s1(h)], 0u, h) == 0u) slot = (int)dict_s1(h);
+      else if (atomicCAS(&ltag[dict_s2(h)], 0u, h) == 0u) slot = (int)dict_s2(h);
+      if (slot < 0) { fails[atomicAdd(&nfail, 1u)] = (uint16_t)i; continue; }
+      lword[slot] = (uint16_t)i;
     }
     __syncthreads();
+    const uint32_t nf = nfail;
+    for (uint32_t j = tid; j < nf; j += 1024) {
+      const uint32_t i = fails[j];
+      const uint2 a = lk0[i], b = lk1[i];
+      const uint32_t h = hash32(a.x, a.y, b.x, b.y);
+      const uint32_t xs[2] = {dict_s1(h), dict_s2(h)};
+      for (int q = 0; q < 2; q++) {
+        const uint32_t x = xs[q];
+        if (atomicOr(&klock[x >> 5], 1u << (x & 31)) & (1u << (x & 31))) continue;  // test-and-set
+        const uint32_t ho = ltag[x];
+        const uint32_t alt = dict_s1(ho) == x ? dict_s2(ho) : dict_s1(ho);
+        if (alt == x) continue;
+        if (atomicOr(&klock[alt >> 5], 1u << (alt & 31)) & (1u << (alt & 31))) continue;
+        if (atomicCAS(&ltag[alt], 0u, ho) != 0u) continue;
+        lword[alt] = lword[x];
+        ltag[x] = h;
+        lword[x] = (uint16_t)i;
+        break;
+      }
+    }
+    __syncthreads();
+    for (int k = tid; k < DICT_SLOTS / 32; k += 1024) klock[k] = 0;
+    __syncthreads();
   }
-  for (int i = tid; i < DICT_SLOTS; i += 1024) w.dict_tag[i] = ltag[i];
+  // keys of the placed words (one writer per slot)
+  for (int s2 = tid; s2 < DICT_SLOTS; s2 += 1024) {
+    const uint32_t t = ltag[s2];
+    uint4 key = make_uint4(0, 0, 0, 0);
+    if (t) {
+      const uint32_t i = lword[s2];
+      key = make_uint4(lk0[i].x, lk0[i].y, lk1[i].x, lk1[i].y);
+      atomicAdd(&nsel, 1u);
+    }
+    w.dict_key[s2] = key;
+    w.dict_tag[s2] = t;
+  }
+  __syncthreads();
   if (tid == 0) w.dict_hist[DH_N] = nsel;  // outside the control block: a side-stream build may precede k_init
 }
 
@@ -1617,13 +1567,17 @@ __device__ void bucket_scan(const Work& w) {
 // spills, and a grid-strided share of the weighted records.
 extern "C" __global__ __launch_bounds__(1024) void k_hist(Work w) {
   __shared__ uint32_t hw[NB];
-  const uint32_t g = blockIdx.x;
+  __shared__ uint64_t hsum[16];
+  const uint32_t g = blockIdx.x, G = gridDim.x;
   for (int i = threadIdx.x; i < NB; i += blockDim.x) hw[i] = 0;
-  __syncthreads();
-  for (int i = threadIdx.x; i < NB; i += blockDim.x) {
-    const uint32_t n = w.cold_n[(uint64_t)g * NB + i];
-    if (n) atomicAdd((unsigned long long*)&w.b_recs[i], (unsigned long long)n);
+  // partitions g, g + G, ...: the sum of their contiguous cold_n rows (one plain
+  // agent-scope store each instead of a global atomic per (workgroup, partition))
+  for (uint32_t b = g; b < NB; b += G) {
+    uint64_t tot;
+    (void)block_exscan(threadIdx.x < G ? cold_n_at(w, threadIdx.x, b) : 0u, hsum, tot);
+    if (threadIdx.x == 0) st_agent((unsigned long long*)&w.b_recs[b], (unsigned long long)tot);
   }
+  __syncthreads();
   uint64_t nw = w.ctl->w_n; if (nw > w.w_cap) nw = w.w_cap;
   for (uint64_t i = (uint64_t)g * blockDim.x + threadIdx.x; i < nw; i += (uint64_t)gridDim.x * blockDim.x) {
     const WRec r = w.w[i];
@@ -1729,6 +1683,10 @@ struct RedLds {
   bool plain;
 };
 
+// LDS-only workgroup barrier: the DS queue drained, no wait on global stores
+// still in flight (a __syncthreads fence would wait for them).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // hash bits used: partition = top NB_LOG2 bits, sub-pass = the next kk bits,
 // bucket = a multiplicative hash of the low bits
 __device__ __forceinline__ uint32_t red_bucket(uint32_t h) {
@@ -1823,52 +1781,6 @@ __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, ui
   return true;
 }
 
-// red_try over a chunk's U records of one lane at once: every record's tag
-// reads are issued before any is used, then every key / count read (left to
-// itself, the scheduler probed the records one after the other: two LDS round
-// trips per record instead of two per chunk).  todo[u]: the record still needs
-// the slow path.
-template <int U>
-__device__ __forceinline__ void red_try_batch(const RedLds& s, const uint32_t (&h)[U], const uint4 (&k)[U], bool (&todo)[U]) {
-  uint4 t[U], t2[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const uint32_t b = red_bucket(h[u]), b2 = b + 1 == RED_BK ? 0 : b + 1;
-    t[u] = s.tag4[b];
-    t2[u] = s.tag4[b2];
-  }
-  SCHED_FENCE();
-  int sl[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const uint32_t b = red_bucket(h[u]), b2 = b + 1 == RED_BK ? 0 : b + 1;
-    int x = t2[u].w == h[u] ? (int)(4 * b2 + 3) : -1;
-    x = t2[u].z == h[u] ? (int)(4 * b2 + 2) : x;
-    x = t2[u].y == h[u] ? (int)(4 * b2 + 1) : x;
-    x = t2[u].x == h[u] ? (int)(4 * b2 + 0) : x;
-    x = t[u].w == h[u] ? (int)(4 * b + 3) : x;
-    x = t[u].z == h[u] ? (int)(4 * b + 2) : x;
-    x = t[u].y == h[u] ? (int)(4 * b + 1) : x;
-    x = t[u].x == h[u] ? (int)(4 * b + 0) : x;
-    sl[u] = x;
-  }
-  uint4 kk[U];
-  unsigned long long cv[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const int q = sl[u] < 0 ? 0 : sl[u];
-    kk[u] = s.key[q];
-    cv[u] = __hip_atomic_load(&s.cnt[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  SCHED_FENCE();
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    const bool ok = todo[u] & (sl[u] >= 0) & (cv[u] != 0) & key_eq16(kk[u], k[u]);
-    if (ok) atomicAdd(&s.cnt[sl[u]], 1ull);
-    todo[u] = todo[u] & !ok;
-  }
-}
-
 // Table order of short words: (h32, hash32b, key).  Every reduce kernel uses
 // it (k_reduce, k_reduce_small, k_reduce_sort1), so the order does not depend
 // on which kernel a key's unit went to, nor on whether its partition was split.
@@ -1918,7 +1830,7 @@ template <class F>
 __device__ __forceinline__ void for_cold_group(const Work& w, uint32_t b, F f, uint32_t g0, uint32_t nreg, int lane,
                                                int nwv) {
   const int wv = 0;  // regions g0 + k nwv
-  const uint32_t myn = lane < (int)nreg ? w.cold_n[(uint64_t)(g0 + lane * nwv) * NB + b] : 0u;
+  const uint32_t myn = lane < (int)nreg ? cold_n_at(w, g0 + lane * nwv, b) : 0u;
   const uint64_t nonempty = __ballot(myn != 0);
   auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
     const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
@@ -2303,7 +2215,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       // another), in the sort index / bin space, which is free until the sort
       if (!split) {
         uint64_t tot;
-        const uint64_t ex = block_exscan(tid < (int)G ? w.cold_n[(uint64_t)tid * NB + b] : 0u, red_wsum, tot);
+        const uint64_t ex = block_exscan(tid < (int)G ? cold_n_at(w, tid, b) : 0u, red_wsum, tot);
         if (tid < (int)G) rpre[tid] = (uint32_t)ex;
         if (tid == 0) rpre[G] = (uint32_t)tot;
       }
@@ -2365,12 +2277,9 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
-            if (!s.plain) red_try_batch<RED_UNROLL>(s, h, cur, todo);
-            else {
 #pragma unroll
-              for (int u2 = 0; u2 < RED_UNROLL; u2++)
-                if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
-            }
+            for (int u2 = 0; u2 < RED_UNROLL; u2++)
+              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
             RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
@@ -2407,7 +2316,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           myn = lane == 0 && a < kin_n ? (uint32_t)(kin_n - a < kchunk ? kin_n - a : kchunk) : 0u;
         } else {
           nreg = G > (uint32_t)wv ? (G - wv + NWV - 1) / NWV : 0;  // <= 64 (G <= MAX_MAP_GRID)
-          myn = lane < (int)nreg ? w.cold_n[(uint64_t)(wv + lane * NWV) * NB + b] : 0u;
+          myn = lane < (int)nreg ? cold_n_at(w, wv + lane * NWV, b) : 0u;
         }
         const uint64_t nonempty = __ballot(myn != 0);
         auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
@@ -2446,12 +2355,9 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
-            if (!s.plain) red_try_batch<RED_UNROLL>(s, h, cur, todo);
-            else {
 #pragma unroll
-              for (int u2 = 0; u2 < RED_UNROLL; u2++)
-                if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
-            }
+            for (int u2 = 0; u2 < RED_UNROLL; u2++)
+              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
             RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
@@ -2566,7 +2472,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       if (lb) atomicAdd(&s.misc[3], lb);
       written += nu;
       sub++;
-      __syncthreads();
+      lds_barrier();  // the table is re-zeroed next: LDS only, the uk / uc stores need not land first
       if (tid == 0) wbytes += s.misc[3];  // read (and reset at the next sub-pass) by tid 0 only
     }
     if (stamp) {
@@ -2604,9 +2510,6 @@ constexpr int SR_BIN_BITS = 9;
 constexpr int SR_BINS = 1 << SR_BIN_BITS;  // hash bits right below the unit bits
 static_assert(SR_PER * SR_THREADS == (int)SMALL_CAP && SR_BINS == 4 * SR_THREADS, "k_reduce_small geometry");
 
-// LDS-only workgroup barrier: the DS queue drained, no wait on global stores
-// still in flight (a __syncthreads fence would wait for them).
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 struct SmallIn {  // prefetched keys (weighted counts are read at use: rare outside exchange passes)
   uint4 k[SR_PER];

@@ -133,7 +133,7 @@ _A2A_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctype
                            ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64))
 
 # exactness-fallback counters (mox_stats.path_hits; collision check build only)
-PATH_DICT_TAG, PATH_LONG_EQHASH, PATH_SORT_RESORT, PATH_SORT_TO_RED, PATH_RED_TAG, PATH_SMALL_TAG = range(6)
+PATH_DICT_SAMEHASH, PATH_LONG_EQHASH, PATH_SORT_RESORT, PATH_SORT_TO_RED, PATH_RED_TAG, PATH_SMALL_TAG = range(6)
 HC_LIB_PATH = os.path.join(_HERE, "libmox_hc.so")  # forced-collision check build (Makefile `hc`)
 CHECK_LIB_PATH = os.path.join(_HERE, "libmox_check.so")  # bounds-check build (Makefile `check`)
 

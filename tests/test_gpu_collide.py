@@ -1,7 +1,8 @@
 """GPU: the forced-collision check build (libmox_hc.so).
 
 Every exactness fallback of the engine runs only when two different words
-share a hash: the dictionary's full search after a tag match (k_map pass B),
+share a hash: the token pass's full-key compare against a dictionary word of
+the same hash (k_map),
 the long-word table's byte compare behind an equal FNV-1a hash, the one-wave
 sort reduce's 64-bit re-sort and its hand-off to k_reduce, and the key
 compares of the k_reduce / k_reduce_small tables.  With full hashes these are
@@ -88,15 +89,16 @@ def test_fuzz_collide(hc):
         assert items(hc, data) == oracle_items(data), data
 
 
-def test_zipf_dictionary_tag_false_matches(hc):
-    """Zipf text with the dictionary: ~1e5 distinct words share a 22-bit key
-    hash with one of the ~3,500 dictionary words; each such token has its tag
-    matched in pass B and takes the full dictionary search before going cold."""
+def test_zipf_dictionary_same_hash_words(hc):
+    """Zipf text with the dictionary: with 22-bit key hashes many distinct words
+    share their hash (and so both dictionary slots) with a dictionary word; the
+    token pass compares the full 16-byte keys, so each such token is counted as
+    its own (cold) word, never as the dictionary word."""
     data = corpus.fill(corpus.ZIPF, 0xC011, 0, 24 << 20)
     got = arrays(hc, data.tobytes())
     ph = hits(hc)
     assert hc.stats()["dict_words"] > 1000
-    assert ph[mox.PATH_DICT_TAG] > 0, ph
+    assert ph[mox.PATH_DICT_SAMEHASH] > 0, ph
     assert_tables_equal(got, coracle.count_arrays(data, nthreads=16)[:3])
 
 
