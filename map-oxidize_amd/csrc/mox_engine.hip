@@ -140,16 +140,32 @@ int ensure_caps(mox_engine* e, const Caps& need) {
   return realloc_sized(e, c);
 }
 
+// Dictionary buffer set i becomes the one the next enqueued kernels use.
+void use_dset(mox_engine* e, int i) {
+  const mox_engine::DictSet& d = e->dsets[i];
+  e->w.cand = d.cand;
+  e->w.dict_hist = d.dict_hist;
+  e->w.dict_list = d.dict_list;
+  e->w.dict_tag = d.dict_tag;
+  e->w.dict_key = d.dict_key;
+  e->w.dict_tot = d.dict_tot;
+  e->dcur = i;
+}
+
 int alloc_fixed(mox_engine* e) {
   Work& w = e->w;
   int rc;
   if ((rc = dalloc(e, (void**)&w.ctl, sizeof(Ctl)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.cand, (size_t)GC_SLOTS * sizeof(WRec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dict_hist, 260 * 4))) return rc;  // 257 used, zeroed as 260 (k_init)
-  if ((rc = dalloc(e, (void**)&w.dict_list, (size_t)DICT_MAX_WORDS * sizeof(WRec)))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dict_tag, DICT_SLOTS * 4))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dict_key, DICT_SLOTS * 16))) return rc;
-  if ((rc = dalloc(e, (void**)&w.dict_tot, DICT_SLOTS * 8))) return rc;
+  for (auto& d : e->dsets) {  // two dictionary sets (async passes alternate, mox_host.h)
+    if ((rc = dalloc(e, (void**)&d.cand, (size_t)GC_SLOTS * sizeof(WRec)))) return rc;
+    if ((rc = dalloc(e, (void**)&d.dict_hist, 260 * 4))) return rc;  // 257 used, zeroed as 260 (k_init)
+    if ((rc = dalloc(e, (void**)&d.dict_list, (size_t)DICT_MAX_WORDS * sizeof(WRec)))) return rc;
+    if ((rc = dalloc(e, (void**)&d.dict_tag, DICT_SLOTS * 4))) return rc;
+    if ((rc = dalloc(e, (void**)&d.dict_key, DICT_SLOTS * 16))) return rc;
+    if ((rc = dalloc(e, (void**)&d.dict_tot, DICT_SLOTS * 8))) return rc;
+    HIPCHK(hipMemset(d.dict_tag, 0, DICT_SLOTS * 4));
+  }
+  use_dset(e, 0);
   w.map_grid = (uint32_t)std::min(e->n_cu * MAP_WG_PER_CU, MAX_MAP_GRID);
   if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.samp, (size_t)w.map_grid * NB * SPLIT_PER_REGION * 4))) return rc;
@@ -168,6 +184,7 @@ int alloc_fixed(mox_engine* e) {
   w.uniq_off = (uint64_t*)d; d += (NB + 1) * 8;
   // reduce units (high-cardinality split)
   if ((rc = dalloc(e, (void**)&w.b_kk, NB * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.red_order, NB * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.u_base, (NB + 1) * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.sub_hist, (size_t)NB * 2 * SUB_N * 4))) return rc;
   if ((rc = dalloc(e, (void**)&w.sp_off, (NB + 1) * 8))) return rc;
@@ -209,7 +226,6 @@ int alloc_fixed(mox_engine* e) {
   memset(e->h_ctl_init, 0, sizeof(Ctl));
   e->h_ctl_init->err_utf8 = ~0ull;
   e->h_ctl_init->halo_err = ~0ull;
-  HIPCHK(hipMemset(w.dict_tag, 0, DICT_SLOTS * 4));
   return MOX_OK;
 }
 
@@ -311,8 +327,8 @@ void launch_dict(mox_engine* e, const Corpus& c, hipStream_t s, const Seq& q) {
 }
 
 // side: build the dictionary on e->dstream, overlapping the previous pass's
-// reduce tail (async passes).  The dictionary buffers (sampling table,
-// histogram, tags, keys, size) are read by a pass up to its k_unicode only.
+// reduce tail (async passes), in the dictionary set the previous pass did not
+// use (mox_host.h dsets: no cross-stream wait on the previous pass).
 void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = false) {
   Work& w = e->w;
   hipStream_t s = e->stream;
@@ -321,7 +337,7 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = fals
   const bool sided = side && dict && !q.timing && !q.sync_each;
   // 1. hot dictionary from a sample
   if (sided) {
-    if (e->dfree_recorded) (void)hipStreamWaitEvent(e->dstream, e->ev_dfree, 0);
+    use_dset(e, e->dcur ^ 1);
     hipLaunchKernelGGL(k_dict_zero, dim3(64), dim3(256), 0, e->dstream, w);
     launch_dict(e, c, e->dstream, q);
     (void)hipEventRecord(e->ev_dready, e->dstream);
@@ -343,10 +359,6 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = fals
   hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);  // + dictionary totals
   q.step("k_unicode");
   q.rec(3);
-  if (e->dstream) {  // the dictionary buffers are free for the next pass's side build
-    (void)hipEventRecord(e->ev_dfree, s);
-    e->dfree_recorded = true;
-  }
   // 4-5. shuffle directory + bucket reduce, table
   launch_reduce_tail(e, c, q);
 }
@@ -658,7 +670,6 @@ int engine_create_one(const mox_config* cfg, int dev, mox_engine** out) {
   }
   for (auto& ev : e->ev) (void)hipEventCreate(&ev);
   if (hipStreamCreateWithFlags(&e->dstream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_dfree, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_dready, hipEventDisableTiming) != hipSuccess) {
     mox_engine_destroy(e);
     return fail(MOX_EHIP, "side stream / events: creation failed");
@@ -987,10 +998,12 @@ void mox_engine_destroy(mox_engine* e) {
   }
   if (e->comm) ncclCommDestroy(e->comm);
   Work& w = e->w;
-  void* ptrs[] = {w.ctl, w.cand, w.dict_hist, w.dict_list, w.dict_tag, w.dict_key, w.dict_tot, w.cold_n, w.samp, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
+  for (auto& d : e->dsets)
+    for (void* p : {(void*)d.cand, (void*)d.dict_hist, (void*)d.dict_list, (void*)d.dict_tag, (void*)d.dict_key, (void*)d.dict_tot}) dfree(p);
+  void* ptrs[] = {w.ctl, w.cold_n, w.samp, w.spill_n, w.b_recs, (void*)e->tables.lower_src,
                   w.cold, w.spill, w.w, w.w_sorted, w.u, w.arena, w.ltab, w.lpos,
                   w.uk, w.uc, w.ui, w.t_counts, w.t_offs, w.t_bytes, e->d_text,
-                  w.b_kk, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.mid_units, w.small_units, w.u_uniq, w.u_uniq_off,
+                  w.b_kk, w.red_order, w.u_base, w.sub_hist, w.sp_off, w.spw_off, w.udesc, w.big_units, w.mid_units, w.small_units, w.u_uniq, w.u_uniq_off,
                   w.u_bytes, w.u_bytes_off, w.b_bytes, w.split_k, w.split_w};
   for (void* p : ptrs) dfree(p);
   for (DevBuf* b : {&e->x_send_short, &e->x_send_blob, &e->x_recv_short, &e->x_recv_blob, &e->g_counts, &e->g_offs,
@@ -1014,7 +1027,7 @@ void mox_engine_destroy(mox_engine* e) {
   if (e->file_land) (void)hipEventDestroy(e->file_land);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->dstream) (void)hipStreamDestroy(e->dstream);
-  for (hipEvent_t ev : {e->ev_dfree, e->ev_dready}) if (ev) (void)hipEventDestroy(ev);
+  if (e->ev_dready) (void)hipEventDestroy(e->ev_dready);
   delete e;
 }
 

@@ -101,11 +101,22 @@ struct mox_engine {
   int device = 0;
   hipStream_t stream = nullptr;
   // async passes: pass k + 1's dictionary is built on dstream while pass k's
-  // reduce tail runs on stream (ev_dfree: pass k's k_unicode has read the
-  // dictionary buffers; ev_dready: the next dictionary is built)
+  // reduce tail runs on stream (ev_dready: the next dictionary is built).  The
+  // dictionary buffers are double-buffered (dsets): a side build writes the set
+  // the previous pass did not use, and the pass before that one has completed
+  // on the host by then (mox_run_range_async completes pass k - 1 before it
+  // returns), so the side stream waits for nothing.
   hipStream_t dstream = nullptr;
-  hipEvent_t ev_dfree = nullptr, ev_dready = nullptr;
-  bool dfree_recorded = false;
+  hipEvent_t ev_dready = nullptr;
+  struct DictSet {
+    WRec* cand = nullptr;
+    uint32_t* dict_hist = nullptr;
+    WRec* dict_list = nullptr;
+    uint32_t* dict_tag = nullptr;
+    uint4* dict_key = nullptr;
+    unsigned long long* dict_tot = nullptr;
+  } dsets[2];
+  int dcur = 0;  // the set the last enqueued pass used (it is in e->w)
   uint32_t flags = 0, dict_words = DICT_MAX_WORDS, sample_pieces = 192;
   int n_cu = 256;
   bool sync_each = false;

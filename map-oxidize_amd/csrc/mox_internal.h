@@ -353,6 +353,7 @@ struct Work {  // device buffers of one engine
   // reduce units (partition b = units u_base[b] .. u_base[b+1]-1; one unit
   // unless b was split into 2^b_kk[b] sub-buckets)
   uint32_t* b_kk;                 // NB
+  uint32_t* red_order;            // NB: partitions by descending record count (k_unit_scan), k_reduce workgroup i takes red_order[i]
   uint32_t* u_base;               // NB + 1
   uint32_t* sub_hist;             // NB x 2 x SUB_N: cold, weighted records per sub-bucket
   uint64_t* sp_off;               // NB + 1: first split_k record of partition b

@@ -657,19 +657,35 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 #pragma unroll
   for (int u = 0; u < TU; u++) { d1[u] = m.s.dkey[s1[u]]; d2[u] = m.s.dkey[s2[u]]; }
   SCHED_FENCE();
+  // hits count in LDS; every miss reserves its region slot (the LDS returning
+  // atomics of all batches issued together), then the misses are stored
+  bool miss[TU];
+  uint32_t pos[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const bool valid = !(e[u] & 0x8000u);
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
-    if (valid & (hit1 | hit2)) {
-      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[hit1 ? s1[u] : s2[u]], 1u);
-    } else if (valid) {
+    miss[u] = valid & !(hit1 | hit2);
+    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[hit1 ? s1[u] : s2[u]], 1u);
 #if defined(MOX_PATHS) && MOX_PATHS
+    if (miss[u]) {
       if ((d1[u].x | d1[u].y | d1[u].z | d1[u].w) && hash32(d1[u].x, d1[u].y, d1[u].z, d1[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
       if ((d2[u].x | d2[u].y | d2[u].z | d2[u].w) && hash32(d2[u].x, d2[u].y, d2[u].z, d2[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
-#endif
-      cold_word(m, h[u], ((uint64_t)K[u][1] << 32) | K[u][0], ((uint64_t)K[u][3] << 32) | K[u][2]);
     }
+#endif
+  }
+  if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) return;
+#pragma unroll
+  for (int u = 0; u < TU; u++) pos[u] = miss[u] ? atomicAdd(&m.s.bcnt[bucket_of(h[u])], 1u) : 0u;
+  SCHED_FENCE();
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    if (!miss[u]) continue;
+    const uint32_t b = bucket_of(h[u]);
+    const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
+    if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, pos[u], h[u]);
+    if (pos[u] < m.w.cold_cap) m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos[u]] = key;
+    else cold_spill(m, key);
   }
 }
 
@@ -1976,20 +1992,64 @@ __device__ __forceinline__ uint64_t split_span(uint64_t n, uint32_t kk) { return
 // units per partition, split-buffer offsets, the reduce work-queue reset, and
 // the output region of every whole partition.
 constexpr int SC_PER = NB / SC_THREADS;
+constexpr int SC_BINS = 256;  // size classes of the k_reduce order (one per thread)
+static_assert(SC_BINS == SC_THREADS && SC_PER * SC_THREADS == NB, "k_unit_scan geometry");
 __device__ void unit_scan(const Work& w) {
   __shared__ uint64_t wsum[16];
+  __shared__ uint32_t smax, smin, bins[SC_BINS], fill[SC_BINS];
   const int t = threadIdx.x;
-  uint32_t kk[SC_PER];
+  uint32_t kk[SC_PER], sz[SC_PER];
   uint64_t nu = 0, nk = 0, nw = 0, nwh = 0;
+  if (t == 0) { smax = 0; smin = 0xFFFFFFFFu; }
+  bins[t] = 0;
+  fill[t] = 0;
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < SC_PER; j++) {
     const uint32_t b = SC_PER * t + j;
     kk[j] = w.b_kk[b];
+    const uint64_t nr = w.b_recs[b], nwb = w.b_w[b];
+    sz[j] = kk[j] ? 0u : (uint32_t)min(nr + nwb, 0x7FFFFFFFull);  // split partitions: their units go to the queues
     nu += 1ull << kk[j];
-    nk += kk[j] ? split_span(w.b_recs[b], kk[j]) : 0;
-    nw += kk[j] ? w.b_w[b] : 0;
+    nk += kk[j] ? split_span(nr, kk[j]) : 0;
+    nw += kk[j] ? nwb : 0;
     nwh += kk[j] ? 0 : 1;
   }
+  {  // size range of the whole partitions: wave max / min on the VALU, one LDS atomic per wave
+    uint32_t mx = 0, mn = 0xFFFFFFFFu;
+#pragma unroll
+    for (int j = 0; j < SC_PER; j++) {
+      mx = max(mx, sz[j]);
+      mn = kk[j] ? mn : min(mn, sz[j]);
+    }
+    mx = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(mx), 63);
+    mn = ~(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(~mn), 63);
+    if ((t & 63) == 0) { atomicMax(&smax, mx); atomicMin(&smin, mn); }
+  }
+  // k_reduce order: whole partitions by descending size class (workgroup i of
+  // k_reduce takes red_order[i]; the first resident round gets the biggest, the
+  // second the smallest: the two rounds balance instead of a big partition
+  // starting late), split partitions last (their workgroups go straight to the
+  // work queue)
+  __syncthreads();
+  const uint32_t lo = smin <= smax ? smin : 0u, span = smax - lo + 1;  // sizes of whole partitions spread over the bins
+  uint32_t bin[SC_PER];
+#pragma unroll
+  for (int j = 0; j < SC_PER; j++) {
+    const uint32_t r = kk[j] ? 0u : sz[j] - lo;  // split partitions: smallest class (their workgroups take queued units)
+    bin[j] = SC_BINS - 1 - (uint32_t)(((uint64_t)r * SC_BINS) / span);  // 0 = biggest
+    atomicAdd(&bins[bin[j]], 1u);
+  }
+  __syncthreads();
+  {
+    uint64_t tot;
+    const uint32_t c = bins[t];
+    const uint32_t ex = (uint32_t)block_exscan(c, wsum, tot);
+    bins[t] = ex;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SC_PER; j++) w.red_order[bins[bin[j]] + atomicAdd(&fill[bin[j]], 1u)] = SC_PER * t + j;
   uint64_t U, tk, tw, nwhole;
   uint64_t ub = block_exscan(nu, wsum, U);
   uint64_t ok = block_exscan(nk, wsum, tk);
@@ -2170,11 +2230,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 #else
 #define RED_MARK(k) do { } while (0)
 #endif
-  bool own = blockIdx.x < NB && w.b_kk[blockIdx.x] == 0;
+  const uint32_t ob = blockIdx.x < NB ? w.red_order[blockIdx.x] : 0u;  // k_unit_scan: biggest partitions first
+  bool own = blockIdx.x < NB && w.b_kk[ob] == 0;
   for (;;) {
     uint32_t u;
     if (own) {
-      u = w.u_base[blockIdx.x];
+      u = w.u_base[ob];
       own = false;
     } else {
       if (tid == 0) {
