@@ -13,4 +13,4 @@ for cfg in "0 8" "1 8" "1 12" "1 16" "0 16"; do
   tail -2 $O/ing_$1_$2.txt | cut -c1-160
 done
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_group.py -x -q --timeout 200 --timeout-method thread \
-  -k "file or cli" > $O/par_file.log 2>&1; step "file parity $(tail -1 $O/par_file.log)" $?
+  -k "file or cli" > $O/par_file.log 2>&1; rc=$?; step "file parity $(tail -1 $O/par_file.log)" $rc

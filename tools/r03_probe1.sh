@@ -9,7 +9,7 @@ step() { echo "== $1 rc=$2"; [ "$2" -eq 0 ] || exit "$2"; }
 for v in direct hash1; do
   MOX_LIB=build/var_$v/libmox.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 \
     --timeout-method thread -k "kats or fuzz or tile or corpora or misaligned" > $O/par_$v.log 2>&1
-  step "parity $v $(tail -1 $O/par_$v.log)" $?
+  rc=$?; step "parity $v $(tail -1 $O/par_$v.log)" $rc
 done
 bash tools/ab_kernel.sh "base direct hash1" "0" "k_map k_reduce" > $O/abk1.txt 2>&1; step "abk round 1" $?
 cat $O/abk1.txt
@@ -23,7 +23,7 @@ cat $O/stamps_summary.txt
 bash tools/pmc_sq.sh k_map p1/sqmap > $O/sqmap.txt 2>&1; step "sq k_map" $?
 bash tools/pmc_sq.sh 'k_reduce$' p1/sqred > $O/sqred.txt 2>&1; step "sq k_reduce" $?
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_exchange.py tests/test_gpu_collide.py -x -q --timeout 150 \
-  --timeout-method thread > $O/par_main.log 2>&1; step "parity main $(tail -1 $O/par_main.log)" $?
+  --timeout-method thread > $O/par_main.log 2>&1; rc=$?; step "parity main $(tail -1 $O/par_main.log)" $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o run -- python3 bench.py --steps 10 --warmup 2 \
   --no-cpu-baseline > $O/c2_under_rocprof.log 2>&1; step "rocprof C2" $?
 python3 tools/trace_timeline.py $O/c2 > $O/c2_timeline.txt; step "timeline C2" $?

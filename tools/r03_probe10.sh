@@ -6,7 +6,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/p10; mkdir -p $O/st
 step() { echo "== $1 rc=$2"; [ "$2" -eq 0 ] || exit "$2"; }
-timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1; step "gpu fast $(tail -1 $O/gpu_fast.log)" $?
+timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1; rc=$?; step "gpu fast $(tail -1 $O/gpu_fast.log)" $rc
 bash tools/ab.sh "kick lpt cbatch" 2 > $O/ab.txt 2>&1; step "ab bench" $?
 cat $O/ab.txt
 bash tools/ab_kernel.sh "dset lpt cbatch" "0" "k_reduce k_unit_scan k_map" > $O/abk1.txt 2>&1; step "abk 1" $?

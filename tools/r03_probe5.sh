@@ -7,7 +7,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/p5; mkdir -p $O
 step() { echo "== $1 rc=$2"; [ "$2" -eq 0 ] || exit "$2"; }
-timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1; step "gpu fast $(tail -1 $O/gpu_fast.log)" $?
+timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1; rc=$?; step "gpu fast $(tail -1 $O/gpu_fast.log)" $rc
 bash tools/ab_kernel.sh "old pm lb new" "0" "k_map k_reduce k_hist" > $O/abk1.txt 2>&1; step "abk round 1" $?
 cat $O/abk1.txt
 bash tools/ab_kernel.sh "new lb pm old" "0" "k_map k_reduce k_hist" > $O/abk2.txt 2>&1; step "abk round 2" $?

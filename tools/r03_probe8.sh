@@ -6,7 +6,7 @@ set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/p8; mkdir -p $O/st
 step() { echo "== $1 rc=$2"; [ "$2" -eq 0 ] || exit "$2"; }
-timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1; step "gpu fast $(tail -1 $O/gpu_fast.log)" $?
+timeout -k 10 600 python -u -m pytest tests -m "gpu and not slow" -x -q --timeout 300 --timeout-method thread > $O/gpu_fast.log 2>&1; rc=$?; step "gpu fast $(tail -1 $O/gpu_fast.log)" $rc
 MOX_LIB=build/var_stamp/libmox.so MOX_DBG=1024 MOX_DEBUG_DIR=$O/st timeout -k 10 200 python -u bench.py --steps 2 --warmup 1 \
   --no-cpu-baseline > $O/stamp.log 2>&1; step "stamp bench" $?
 python3 tools/mapcyc.py $O/st/mapcyc.csv; step "mapcyc" $?
