@@ -550,6 +550,13 @@ __device__ __forceinline__ uint32_t wave_incl_max(uint32_t x) {
   x = max(x, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false));
   return x;
 }
+// v_ffbl_b32: index of the lowest set bit, ~0 for 0 (the hardware result; a
+// __builtin_ctzg fallback costs a compare + select per use)
+__device__ __forceinline__ uint32_t ffbl(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
 // compiler + LDS ordering between lanes of one wave (LDS executes a wave's
 // instructions in order; this keeps the compiler from reordering across it)
 __device__ __forceinline__ void wave_lds_fence() {
@@ -805,14 +812,13 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(cnt), 63);
     uint32_t st = start;
     uint16_t* const sink = list + (TOKMAX - 1);
+    uint16_t* const mine = list + pre;  // this lane's entries: mine[0 .. cnt)
     const uint32_t lbase = (uint32_t)(lane * 16);
     for (uint32_t it = 0; it < trips; it++) {
-      const bool valid = it < cnt;
-      const uint32_t p = (uint32_t)__builtin_ctzg(st, -1);
+      const uint32_t p = ffbl(st);  // ~0 once the lane has run out of starts
       st &= st - 1;
-      const uint32_t len = (uint32_t)__builtin_ctzg(ws32 >> (p & 31u), -1);
-      *(valid ? list + k : sink) = (uint16_t)(lbase + p + (len > 16 ? 0x8000u : (len << 10)));
-      k += valid ? 1u : 0u;
+      const uint32_t len = ffbl(ws32 >> (p & 31u));
+      *(it < cnt ? mine + it : sink) = (uint16_t)(lbase + p + (len > 16 ? 0x8000u : (len << 10)));
     }
   } else {
     while (start) {
