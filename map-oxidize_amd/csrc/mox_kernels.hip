@@ -614,6 +614,17 @@ __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&
 }
 // compiler scheduling barrier: no instruction moves across it
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// A sched_barrier orders only what the selection DAG left on each side of it,
+// and the DAG hoists arithmetic whose operands are ready: key_make of batch 0
+// landed above the fence and the mask-table reads of batches 1.. after it (one
+// LDS round trip per batch).  Passing the entries through a volatile asm after
+// the fence makes everything computed from them follow it.
+template <int TU>
+__device__ __forceinline__ void after_fence(uint32_t (&v)[TU]) {
+#pragma unroll
+  for (int u = 0; u < TU; u++) asm volatile("" : "+v"(v[u]));
+}
+#define AFTER_FENCE(v) after_fence(v)
 
 // 16-byte key equality as one OR of XORs (kept opaque: the combiner would
 // otherwise split it into four compares and a boolean tree)
@@ -652,6 +663,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 #pragma unroll
   for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
   SCHED_FENCE();
+  AFTER_FENCE(e);
   uint32_t K[TU][4], h[TU], s1[TU], s2[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
@@ -715,6 +727,7 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
 #pragma unroll
   for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
   SCHED_FENCE();
+  AFTER_FENCE(e);
   uint32_t K[TU][4];
 #pragma unroll
   for (int u = 0; u < TU; u++) key_make(e[u], ld[u], K[u]);
