@@ -153,9 +153,9 @@ def roofline_fields(per_rank, map_avg, workload, traffic_json):
         # is priced against HBM (no dense contraction) but the binding unit is named
         "bound": "hbm",
         "binding_resource": "VALU issue + LDS latency (1 loader + 15 consumer waves per CU), not HBM bandwidth",
-        "limiter": "k_map moves ~2.6 TB/s of HBM traffic of 8; SQ counters: ~510 VALU instructions per 992-byte row at "
-                   "~50 % VALU issue, LDS array ~39 % busy, waves parked on s_waitcnt ~35 % of their cycles "
-                   "(profiles/r03_sq_k_map_dict2.txt; DESIGN.md §4, §8)",
+        "limiter": "k_map moves ~2.7 TB/s of HBM traffic of 8; SQ counters: ~461 VALU instructions per 992-byte row at "
+                   "~48 % VALU issue, LDS array ~46 % busy (43 % of it bank conflicts), waves parked on s_waitcnt ~33 % "
+                   "of their cycles (profiles/r03_sq_k_map_final.txt; DESIGN.md §4, §8)",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
