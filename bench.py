@@ -134,6 +134,21 @@ def local_tokens(eng, d_buf, n, own_b, own_e, at_end):
     return eng.stats()["tokens"]
 
 
+def limiter_fields(workload):
+    """What binds k_map for this workload, as measured (SQ counters) and recorded
+    in profiles/limiter_<workload>.json; omitted when no measurement of this
+    workload exists."""
+    f = os.path.join(ROOT, "profiles", "limiter_%s.json" % workload)
+    try:
+        lj = json.load(open(f))
+    except Exception:
+        return {}
+    if lj.get("workload") != workload:
+        return {}
+    return {"binding_unit": lj.get("binding_unit"), "limiter": lj.get("limiter"),
+            "limiter_source": os.path.relpath(f, ROOT)}
+
+
 def roofline_fields(per_rank, map_avg, workload, traffic_json):
     achieved = per_rank / (map_avg * 1e-3) / 1e9
     traffic = None
@@ -147,15 +162,12 @@ def roofline_fields(per_rank, map_avg, workload, traffic_json):
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    return {
+    r = {
         "kernel": "k_map",
-        # what binds k_map is issue and LDS latency, not HBM bandwidth: the roofline
-        # is priced against HBM (no dense contraction) but the binding unit is named
+        # priced against HBM (no dense contraction: the contract's "hbm" roofline);
+        # the unit that actually binds k_map, where measured for this workload,
+        # is in binding_unit / limiter (limiter_fields)
         "bound": "hbm",
-        "binding_resource": "VALU issue + LDS latency (1 loader + 15 consumer waves per CU), not HBM bandwidth",
-        "limiter": "k_map moves ~2.7 TB/s of HBM traffic of 8; SQ counters: ~461 VALU instructions per 992-byte row at "
-                   "~48 % VALU issue, LDS array ~46 % busy (43 % of it bank conflicts), waves parked on s_waitcnt ~33 % "
-                   "of their cycles (profiles/r03_sq_k_map_final.txt; DESIGN.md §4, §8)",
         "achieved": round(achieved, 1),
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
@@ -164,10 +176,17 @@ def roofline_fields(per_rank, map_avg, workload, traffic_json):
         "algorithmic_bytes_per_launch": per_rank,
         "avg_launch_ms": round(map_avg, 4),
     }
+    r.update(limiter_fields(workload))
+    return r
 
 
 def main_group(a):
-    """--gpus N > 1 without torchrun: one process, one engine group over N GPUs."""
+    """--gpus N > 1 without torchrun: one process, one engine group over N GPUs.
+    A timed step is one mox_run_shards call with MOX_F_SORT_BYTES: local passes,
+    exchange, per-owner reduce, gather at GPU 0 and the bytewise sort of the
+    gathered table (north_star: "a gather of the sorted result").  The same K
+    steps without the sort (gathered table in engine / hash order) are timed
+    after them and reported beside the value."""
     n = a.gpus
     if not a.workload:
         a.workload = "C3"
@@ -176,9 +195,10 @@ def main_group(a):
         per_rank = a.bytes_per_gpu
     total = per_rank * n
     devices = [a.device] * n if a.device >= 0 else None
+    n_dev = len(set(devices)) if devices else n  # distinct GPUs (members may share one in tests)
     xport = mox.XPORT_COPY if a.xport == "host" else mox.XPORT_RCCL
-    base_flags = mox.MOX_F_NO_DICT if a.no_dict else 0
-    g = mox.Engine(n_gpus=n, transport=xport, devices=devices, flags=base_flags | mox.MOX_F_TIMING_MAP,
+    base_flags = (mox.MOX_F_NO_DICT if a.no_dict else 0) | mox.MOX_F_TIMING_MAP
+    g = mox.Engine(n_gpus=n, transport=xport, devices=devices, flags=base_flags | mox.MOX_F_SORT_BYTES,
                    sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
     shards, bufs = [], []
     for r in range(n):
@@ -190,23 +210,23 @@ def main_group(a):
         del host
         bufs.append((m, d))
         shards.append((d, hi - lo, ob, oe, end))
-    for _ in range(a.warmup):
-        g.run_shards(shards)
-    rows = []
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        g.run_shards(shards)  # synchronous: returns with the sorted table on GPU 0
-        rows.append(g.stats())
-    elapsed = time.perf_counter() - t0
+
+    def timed(flags):
+        g.set_flags(flags)
+        for _ in range(a.warmup):
+            g.run_shards(shards)
+        rows = []
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            g.run_shards(shards)  # synchronous: returns with the gathered table on GPU 0
+            rows.append(g.stats())
+        return time.perf_counter() - t0, rows
+
+    el_hash, rows_hash = timed(base_flags)
+    elapsed, rows = timed(base_flags | mox.MOX_F_SORT_BYTES)  # the value: sorted result inside the step
     last = rows[-1]
-    # untimed: one call with the bytewise sort of the gathered table on GPU 0
-    # (MOX_F_SORT_BYTES), reported beside the step (the timed steps leave the
-    # gathered table in engine order, as the one-process-per-GPU path does)
-    g.set_flags(base_flags | mox.MOX_F_TIMING_MAP | mox.MOX_F_SORT_BYTES)
-    g.run_shards(shards)
-    sort_ms = g.stats()["ms_sort"]
-    t = g.fetch()
-    counts, offs, _ = t.arrays()
+    t = g.fetch()  # bytewise order (sorted on GPU 0 by the last timed step)
+    counts, offs, raw = t.arrays()
     table_n, table_bytes, table_tokens = t.n, int(offs[-1]) if t.n else 0, t.tokens
     ok = int(counts.sum()) == t.tokens == last["tokens"]
     t.close()
@@ -214,7 +234,7 @@ def main_group(a):
     gbs = total / (elapsed / a.steps) / 1e9
     map_avg = statistics.mean(r["ms_map"] for r in rows)
     b_alg = total + table_bytes + 8 * table_n
-    mean = lambda k: round(statistics.mean(r[k] for r in rows), 4)  # noqa: E731
+    mean = lambda rr, k: round(statistics.mean(r[k] for r in rr), 4)  # noqa: E731
     line = {
         "metric": METRIC,
         "value": round(gbs, 3),
@@ -230,18 +250,25 @@ def main_group(a):
         "data": "synthetic: mox_corpus kind=%d seed=%#x (%s, host-generated, copied to HBM before timing)"
                 % (kind, seed, KIND_DESC.get(kind, "?")),
         "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
-                   "parallelism": "dp%d byte-range shards + %s all-to-all + gather at GPU 0 "
-                                  "(one process, engine group)" % (n, "RCCL" if xport == mox.XPORT_RCCL else "device-copy")},
+                   "parallelism": "dp%d byte-range shards + %s all-to-all + gather and bytewise sort at GPU 0 "
+                                  "(one process, engine group%s)" % (
+                                      n, "RCCL" if xport == mox.XPORT_RCCL else "device-copy",
+                                      "" if n_dev == n else "; %d members on %d GPU(s)" % (n, n_dev))},
         "words_per_s": round(last["tokens"] / (elapsed / a.steps), 1),
-        "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * n), 2),
+        # against the HBM peak of the GPUs actually used (members sharing one GPU share its HBM)
+        "pct_hbm_peak": round(100.0 * gbs / (HBM_PEAK_GBS * n_dev), 2),
         "algorithmic_bytes_per_step": b_alg,
-        "roofline_end_to_end": {"achieved": round(b_alg / (elapsed / a.steps) / 1e9, 1), "peak": HBM_PEAK_GBS * n,
-                                "unit": "GB/s", "frac": round(b_alg / (elapsed / a.steps) / 1e9 / (HBM_PEAK_GBS * n), 4)},
+        "roofline_end_to_end": {"achieved": round(b_alg / (elapsed / a.steps) / 1e9, 1), "peak": HBM_PEAK_GBS * n_dev,
+                                "unit": "GB/s", "frac": round(b_alg / (elapsed / a.steps) / 1e9 / (HBM_PEAK_GBS * n_dev), 4)},
         "roofline": roofline_fields(per_rank, map_avg, a.workload, a.traffic_json),
-        "pass_mode": "sync (mox_run_shards per step)",
-        "phases_ms": {"local_passes": mean("ms_local"), "map_mean_over_gpus": mean("ms_map"), "exchange": mean("ms_exchange"),
-                      "gather": mean("ms_gather"), "step_wall": mean("ms_run"),
-                      "sort_bytes_untimed": round(sort_ms, 4)},
+        "pass_mode": "sync (mox_run_shards per step, MOX_F_SORT_BYTES)",
+        "phases_ms": {"local_passes": mean(rows, "ms_local"), "map_mean_over_gpus": mean(rows, "ms_map"),
+                      "exchange": mean(rows, "ms_exchange"), "gather": mean(rows, "ms_gather"),
+                      "sort_bytes": mean(rows, "ms_sort"), "step_wall": mean(rows, "ms_run")},
+        "hash_order": {"value": round(total / (el_hash / a.steps) / 1e9, 3), "ms_per_step": round(el_hash / a.steps * 1e3, 4),
+                       "note": "the same steps without the bytewise sort (gathered table in engine order)",
+                       "phases_ms": {"local_passes": mean(rows_hash, "ms_local"), "exchange": mean(rows_hash, "ms_exchange"),
+                                     "gather": mean(rows_hash, "ms_gather"), "step_wall": mean(rows_hash, "ms_run")}},
         "stats": {k: last[k] for k in ("tokens", "uniques", "cold_records", "weighted_records")},
         "multi_gpu": {
             "mode": "engine group (one process)",
@@ -250,11 +277,11 @@ def main_group(a):
             "devices": devices if devices else list(range(n)),
             "all_to_all_bytes": int(last["x_bytes_sent"]),
             "all_to_all_bytes_recv": int(last["x_bytes_recv"]),
-            "exchange_ms": mean("ms_exchange"),
-            "gather_ms": mean("ms_gather"),
+            "exchange_ms": mean(rows, "ms_exchange"),
+            "gather_ms": mean(rows, "ms_gather"),
             "gather_bytes": int(last["gather_bytes"]),
             "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens,
-                               "order": "bytewise (device sort on GPU 0, untimed call: phases_ms.sort_bytes_untimed)"},
+                               "order": "bytewise (device sort on GPU 0 inside the timed step)"},
         },
         "check_sum_counts_eq_tokens": ok,
         "cpu_baseline": None,
@@ -311,7 +338,7 @@ def main():
 
     gather = world > 1 and not a.no_gather
 
-    def step(sync=False):
+    def step(sync=False, sort=True):
         if use_async and not sync:
             eng.run_range_async(d_buf, hi - lo, own_b, own_e, at_end)
             return
@@ -321,11 +348,13 @@ def main():
                 eng.exchange_host(world, rank, a2a)
             else:
                 eng.exchange()
-            if gather:  # the whole table at rank 0 (mox_gather: device to device)
+            if gather:  # the whole table at rank 0 (mox_gather: device to device) ...
                 if a2a:
                     eng.gather_host(world, rank, a2a, root=0)
                 else:
                     eng.gather(0)
+                if sort and rank == 0:  # ... sorted bytewise on its GPU (north_star: "a gather of the sorted result")
+                    eng.sort_result()
 
     for _ in range(a.warmup):
         step()
@@ -348,15 +377,28 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    sort_ms = eng.stats()["ms_sort"] if gather and rank == 0 else 0.0
+    el_hash = None
+    if world > 1 and gather:  # the same steps without the sort, reported beside the value
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(a.steps):
+            step(sort=False)
+        eng.synchronize()
+        if dist:
+            dist.barrier()
+        el_hash = time.perf_counter() - t1
     eng.set_flags(base_flags | mox.MOX_F_TIMING)  # untimed diagnostic step: per-phase events
     step(sync=True)
     eng.synchronize()
     phases = [eng.stats()]
     if dist:
         import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
+        t = torch.tensor([elapsed, el_hash or 0.0], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = float(t[0].item())
+        el_hash = float(t[1].item()) if el_hash is not None else None
     last = eng.stats()
     t = eng.fetch()
     counts, offs, _ = t.arrays()
@@ -386,9 +428,14 @@ def main():
             "all_to_all_bytes_recv": int(sum(r[2] for r in rows)),
             "exchange_ms_max_over_ranks": round(max(r[3] for r in rows), 4),
             "gather_ms_max_over_ranks": round(max(r[4] for r in rows), 4) if gather else None,
-            "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens} if gather else None,
+            "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens,
+                               "order": "bytewise (mox_sort_result on rank 0's GPU inside the timed step)"} if gather else None,
+            "sort_bytes_ms_rank0": round(sort_ms, 4) if gather else None,
+            "hash_order": {"value": round(total / (el_hash / a.steps) / 1e9, 3), "ms_per_step": round(el_hash / a.steps * 1e3, 4),
+                           "note": "the same steps without the sort at rank 0"} if el_hash else None,
             "note": "exchange = counts all-to-all + pack + payload all-to-all (RCCL send/recv in one group) + "
-                    "reduce-only pass; gather = every rank's final table to rank 0 (mox_gather)",
+                    "reduce-only pass; gather = every rank's final table to rank 0 (mox_gather), then the bytewise "
+                    "device sort at rank 0 (mox_sort_result), both inside the timed step",
         }
     else:
         tokens_all = last["tokens"]

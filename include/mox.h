@@ -69,7 +69,7 @@ extern "C" {
 typedef struct mox_config {
   int device;             /* HIP device ordinal; -1 = current device */
   uint32_t flags;         /* MOX_F_* */
-  uint32_t dict_words;    /* hot dictionary capacity; 0 = default (3584, also the maximum) */
+  uint32_t dict_words;    /* hot dictionary capacity; 0 = default (4096, also the maximum) */
   uint32_t sample_pieces; /* 4 KiB pieces sampled to build the dictionary; 0 = default (192), max 1024 */
   uint64_t reserve_bytes; /* pre-size device buffers for corpora of this size (per GPU); 0 = grow on demand */
   /* engine group: n_gpus > 1 makes ONE engine that
@@ -163,7 +163,8 @@ const char* mox_last_error(void);
 int mox_abi_version(void);
 
 int mox_engine_create(const mox_config* cfg, mox_engine** out);
-/* Replace the engine's MOX_F_* flags (e.g. switch timing modes between runs). */
+/* Replace the engine's MOX_F_* flags (e.g. switch timing modes between runs); an
+ * engine group applies them to every member. */
 int mox_set_flags(mox_engine* e, uint32_t flags);
 void mox_engine_destroy(mox_engine* e);
 
@@ -215,6 +216,12 @@ int mox_group_size(const mox_engine* e);
 mox_engine* mox_group_member(mox_engine* e, int i);
 /* Copy the table of the last run (or of the last exchange) to the host. */
 int mox_fetch_table(mox_engine* e, mox_table** out);
+/* Reorder the device-resident result table bytewise ascending (Rust String
+ * Ord) on the GPU, without fetching it (e.g. the root's table after
+ * mox_gather, inside a timed multi-GPU step).  MOX_ENOMEM when the sort's
+ * device scratch cannot be allocated: the table then stays in engine order
+ * (mox_fetch_table with MOX_F_SORT_BYTES still sorts it, on the host). */
+int mox_sort_result(mox_engine* e);
 int mox_get_stats(const mox_engine* e, mox_stats* out);
 
 /* device memory helpers so callers need no HIP headers */

@@ -4,23 +4,27 @@
 // §8(b).  The reference's own table order is HashMap-random
 // (/root/reference/src/main.rs:177-179); this is presentation, not counting.
 //
-// Records (32 B) = the word's 16-byte window at the current level as four
-// big-endian u32 (so numeric order = byte order, zero padded), a length class
-// aux = min(bytes left in the window's suffix, 17), the word's table index and
-// a run id.  An LSD radix sort over 8-bit digits, least significant first:
-// aux, window bytes 15..0, run id bytes 0..3.  Per digit pass: per-tile
-// histograms (tile = 8,192 records), one exclusive scan of the digit-major
-// tile counts, and a stable scatter (16-element wave match by 8 ballots,
-// per-wave digit counts in LDS, 32 ordered rounds per tile).  Digits whose
-// value is the same for every record (read from one up-front histogram of all
-// 21 digits) are skipped: zero padding and the run id of level 0 cost nothing.
+// Records (16 B) = {key, run, idx}: key = the word's 7-byte window at the
+// current level, big-endian in bits 63..8, and in bits 7..0 a length class
+// aux = min(bytes left from the window start, 8) (8 = the word goes on past
+// the window); run = the tie run the record belongs to (0 at level 0); idx =
+// the word's table index.  Numeric order of (run, key) is String Ord on the
+// window: equal window bytes order the shorter remainder first.
 //
-// Ties after level 0 are words that share their first 16 bytes and are both
-// longer than 16 bytes (aux == 17 on both sides).  Their maximal runs are
-// re-sorted on the next 16 bytes (level 1, 2, ...), with the run id as the
-// most significant key so runs stay where they are, until no run is left.
-// Two words that agree on every compared byte and differ in length are
-// ordered by aux (the shorter one is a proper prefix: first).
+// Each level is an LSD radix sort over 8-bit digits (key bytes 0..7, then run
+// bytes 0..3), one ONESWEEP pass per digit (k_os_pass): a tile of 4,096
+// records ranks itself stably (bit-sliced ballot match per wave, per-wave digit
+// counters in LDS), publishes its digit counts and finds its global offsets by
+// a decoupled look-back over the tiles before it (agent-scope status words),
+// stages the tile in LDS in digit order and writes each digit's run with
+// consecutive stores.  One up-front kernel histograms every digit; digits whose
+// value is the same for every record are skipped (the run id at level 0, zero
+// bytes every word shares).
+//
+// Ties after a level are words that share the window and both go on past it
+// (aux == 8 on both sides).  Their maximal runs are re-sorted on the next 7
+// bytes (level 1, 2, ...), with the run id as the most significant key so
+// runs stay where they are, until no run is left.
 #include <algorithm>
 #include <cstring>
 
@@ -28,35 +32,47 @@
 
 namespace {
 
-struct BRec {
-  uint4 k;  // big-endian window bytes
-  uint32_t aux, idx, run, pad;
+struct __attribute__((aligned(16))) BRec {
+  uint64_t key;  // window bytes big-endian in bits 63..8, aux in bits 7..0
+  uint32_t run, idx;
 };
-constexpr int BS_THREADS = 256;
-constexpr int BS_ROUNDS = 32;
-constexpr int BS_TILE = BS_THREADS * BS_ROUNDS;  // 8,192 records per tile
-constexpr int BS_DIGITS = 21;                    // aux, 16 window bytes, 4 run id bytes
+static_assert(sizeof(BRec) == 16, "BRec is one 16-byte load");
+constexpr uint32_t WIN = 7;                      // window bytes per level
+constexpr uint32_t AUX_MORE = 8;                 // aux: the word continues past the window
+constexpr int OS_THREADS = 256;
+constexpr int OS_ITEMS = 16;                     // records per thread
+constexpr int OS_TILE = OS_THREADS * OS_ITEMS;   // 4,096 records per tile
+constexpr int OS_WAVES = OS_THREADS / 64;
+constexpr int OS_DIGITS = 12;                    // key bytes 0..7 (0 = aux), run bytes 0..3
 constexpr int SCAN_T = 1024, SCAN_PER = 8, SCAN_TILE = SCAN_T * SCAN_PER;
+// look-back status word of (tile, digit): flag in bits 63..62, count below
+constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_VAL = (1ull << 62) - 1;
+constexpr uint32_t OS_SPIN_MAX = 1u << 22;       // a look-back that waits longer reports a failure (never expected)
 
 __device__ __forceinline__ uint32_t digit_of(const BRec& r, int d) {
-  if (d == 0) return r.aux;
-  if (d <= 16) {  // window byte 16 - d (d = 1: byte 15, the least significant)
-    const int b = 16 - d;
-    const uint32_t w = b < 4 ? r.k.x : b < 8 ? r.k.y : b < 12 ? r.k.z : r.k.w;
-    return (w >> (8 * (3 - (b & 3)))) & 0xFFu;
-  }
-  return (r.run >> (8 * (d - 17))) & 0xFFu;
+  if (d < 8) return (uint32_t)(r.key >> (8 * d)) & 0xFFu;
+  return (r.run >> (8 * (d - 8))) & 0xFFu;
 }
 
-// Window bytes [16 level, 16 level + 16) of word i, big-endian, zero padded.
-__device__ __forceinline__ void window(const uint64_t* offs, const uint8_t* bytes, uint64_t i, uint32_t level, BRec& r) {
-  const uint64_t o = offs[i], len = offs[i + 1] - o, a = 16ull * level;
-  uint32_t w[4] = {0, 0, 0, 0};
+// Window bytes [WIN level, WIN level + WIN) of word i and its length class.
+__device__ __forceinline__ uint64_t window(const uint64_t* offs, const uint8_t* bytes, uint64_t i, uint32_t level) {
+  const uint64_t o = offs[i], len = offs[i + 1] - o, a = (uint64_t)WIN * level;
   const uint64_t have = len > a ? len - a : 0;
-  const uint32_t nb = have < 16 ? (uint32_t)have : 16u;
-  for (uint32_t j = 0; j < nb; j++) w[j >> 2] |= (uint32_t)bytes[o + a + j] << (8 * (3 - (j & 3)));
-  r.k = make_uint4(w[0], w[1], w[2], w[3]);
-  r.aux = have > 16 ? 17u : (uint32_t)have;
+  const uint32_t nb = have < WIN ? (uint32_t)have : WIN;
+  uint64_t k = 0;
+  for (uint32_t j = 0; j < nb; j++) k |= (uint64_t)bytes[o + a + j] << (8 * (7 - j));
+  return k | (have > WIN ? AUX_MORE : (uint32_t)have);
+}
+
+template <class T>
+__device__ __forceinline__ void st_agent(T* p, T v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <class T>
+__device__ __forceinline__ T ld_agent(const T* p) { return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 }  // namespace
@@ -64,89 +80,154 @@ __device__ __forceinline__ void window(const uint64_t* offs, const uint8_t* byte
 extern "C" __global__ __launch_bounds__(256) void k_bs_init(const uint64_t* offs, const uint8_t* bytes, uint64_t n, BRec* out) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     BRec r;
-    window(offs, bytes, i, 0, r);
-    r.idx = (uint32_t)i;
+    r.key = window(offs, bytes, i, 0);
     r.run = 0;
-    r.pad = 0;
+    r.idx = (uint32_t)i;
     out[i] = r;
   }
 }
 
-// Histograms of all BS_DIGITS digits over every record (gh[d * 256 + v]).
+// Histograms of all OS_DIGITS digits over every record: gh[d * 256 + v].
 extern "C" __global__ __launch_bounds__(256) void k_bs_ghist(const BRec* in, uint64_t n, unsigned long long* gh) {
-  __shared__ uint32_t h[BS_DIGITS * 256];
-  for (int i = threadIdx.x; i < BS_DIGITS * 256; i += 256) h[i] = 0;
+  __shared__ uint32_t h[OS_DIGITS * 256];
+  for (int i = threadIdx.x; i < OS_DIGITS * 256; i += 256) h[i] = 0;
   __syncthreads();
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     const BRec r = in[i];
 #pragma unroll
-    for (int d = 0; d < BS_DIGITS; d++) atomicAdd(&h[d * 256 + digit_of(r, d)], 1u);
+    for (int d = 0; d < OS_DIGITS; d++) atomicAdd(&h[d * 256 + digit_of(r, d)], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < BS_DIGITS * 256; i += 256)
+  for (int i = threadIdx.x; i < OS_DIGITS * 256; i += 256)
     if (h[i]) atomicAdd(&gh[i], (unsigned long long)h[i]);
 }
 
-// Per-tile digit counts, digit-major: bh[v * ntiles + tile].
-extern "C" __global__ __launch_bounds__(BS_THREADS) void k_bs_bhist(const BRec* in, uint64_t n, int d, uint64_t* bh, uint64_t ntiles) {
-  __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
-  __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * BS_TILE;
-  for (int r = 0; r < BS_ROUNDS; r++) {
-    const uint64_t i = t0 + (uint64_t)r * BS_THREADS + threadIdx.x;
-    if (i < n) atomicAdd(&h[digit_of(in[i], d)], 1u);
+// Exclusive scans of the global digit histograms: gs[d * 256 + v] = first
+// output position of digit value v in the pass over digit d.
+extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const unsigned long long* gh, uint64_t* gs) {
+  __shared__ uint64_t ws[4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  for (int d = 0; d < OS_DIGITS; d++) {
+    const uint64_t x = gh[d * 256 + t];
+    uint64_t inc = x;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) ws[wv] = inc;
+    __syncthreads();
+    uint64_t pre = 0;
+    for (int k = 0; k < wv; k++) pre += ws[k];
+    gs[d * 256 + t] = pre + inc - x;
+    __syncthreads();
   }
-  __syncthreads();
-  bh[(uint64_t)threadIdx.x * ntiles + blockIdx.x] = h[threadIdx.x];
 }
 
-// Stable scatter of one tile by digit d: records in input order get
-// consecutive positions per digit starting at the tile's scanned offset.
-extern "C" __global__ __launch_bounds__(BS_THREADS) void k_bs_scatter(const BRec* in, BRec* out, uint64_t n, int d, const uint64_t* bo,
-                                                                      uint64_t ntiles) {
-  __shared__ uint32_t wc[BS_THREADS / 64][256];  // this round's per-wave digit counts
-  __shared__ uint64_t base[256];                 // next position of each digit
+// One onesweep pass: records in -> out, stably ordered by digit d.  Tile =
+// blockIdx.x (tiles are dispatched in order, so every tile a look-back waits
+// on has been dispatched before it: the wait ends).  status[tile * 256 + v]
+// is zero at launch.
+extern "C" __global__ __launch_bounds__(OS_THREADS, 2) void k_os_pass(const BRec* __restrict__ in, BRec* __restrict__ out,
+                                                                       uint64_t n, int d, const uint64_t* __restrict__ gs,
+                                                                       uint64_t* status, unsigned int* err) {
+  __shared__ __attribute__((aligned(16))) BRec stage[OS_TILE];
+  __shared__ uint32_t wcnt[OS_WAVES][256];  // per-wave digit counters, then per-wave offsets inside the digit
+  __shared__ uint32_t lstart[256];          // first tile position of each digit
+  __shared__ uint64_t gbase[256];           // first output position of this tile's records of each digit
+  __shared__ uint32_t ws[OS_WAVES];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  base[tid] = bo[(uint64_t)tid * ntiles + blockIdx.x];
-  for (int w = 0; w < BS_THREADS / 64; w++) wc[w][tid] = 0;
+  const uint64_t t0 = (uint64_t)blockIdx.x * OS_TILE;
+  const uint32_t tn = (uint32_t)(n - t0 < (uint64_t)OS_TILE ? n - t0 : (uint64_t)OS_TILE);
+  for (int w = 0; w < OS_WAVES; w++) wcnt[w][tid] = 0;
+  // records of wave wv: tile positions wv * 64 ITEMS + i * 64 + lane (input order = (wv, i, lane))
+  BRec rec[OS_ITEMS];
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int i = 0; i < OS_ITEMS; i++) {
+    const uint32_t p = (uint32_t)(wv * 64 * OS_ITEMS + i * 64 + lane);
+    const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(in + t0 + (p < tn ? p : 0u)));
+    rec[i].key = ((uint64_t)x.y << 32) | x.x;
+    rec[i].run = x.z;
+    rec[i].idx = x.w;
+  }
   __syncthreads();
-  const uint64_t t0 = (uint64_t)blockIdx.x * BS_TILE;
+  // stable rank inside the wave: lanes with the same digit by 8 bit-sliced
+  // ballots; the lowest such lane advances the wave's counter for the digit
   const uint64_t lt = (1ull << lane) - 1ull;
-  for (int r = 0; r < BS_ROUNDS; r++) {
-    const uint64_t i = t0 + (uint64_t)r * BS_THREADS + tid;
-    const bool ok = i < n;
-    BRec rec;
-    uint32_t v = 0;
-    if (ok) {
-      rec = in[i];
-      v = digit_of(rec, d);
-    }
-    // lanes of this wave with the same digit: 8 ballots
+  uint32_t rank[OS_ITEMS];
+#pragma unroll
+  for (int i = 0; i < OS_ITEMS; i++) {
+    const uint32_t p = (uint32_t)(wv * 64 * OS_ITEMS + i * 64 + lane);
+    const bool ok = p < tn;
+    const uint32_t v = digit_of(rec[i], d);
     uint64_t eq = __ballot(ok);
 #pragma unroll
     for (int b = 0; b < 8; b++) {
-      const uint64_t bal = __ballot(((v >> b) & 1u) != 0);
+      const uint64_t bal = __ballot((v >> b) & 1u);
       eq &= ((v >> b) & 1u) ? bal : ~bal;
     }
-    const uint32_t rank = (uint32_t)__popcll(eq & lt);
-    if (ok && rank == 0) wc[wv][v] = (uint32_t)__popcll(eq);
-    __syncthreads();
-    // thread t = digit t: wave prefixes, in wave order
-    uint32_t pre[BS_THREADS / 64];
-    uint32_t run = 0;
+    const uint32_t before = ok ? wcnt[wv][v] : 0u;
+    wave_lds_fence();
+    if (ok && (eq & lt) == 0) wcnt[wv][v] = before + (uint32_t)__popcll(eq);
+    wave_lds_fence();
+    rank[i] = before + (uint32_t)__popcll(eq & lt);
+  }
+  __syncthreads();
+  // thread t = digit t: per-wave offsets, the tile's count, its tile start
+  uint32_t cnt = 0;
 #pragma unroll
-    for (int w = 0; w < BS_THREADS / 64; w++) { pre[w] = run; run += wc[w][tid]; }
+  for (int w = 0; w < OS_WAVES; w++) {
+    const uint32_t c = wcnt[w][tid];
+    wcnt[w][tid] = cnt;
+    cnt += c;
+  }
+  {
+    uint32_t inc = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(inc, o);
+      if (lane >= o) inc += y;
+    }
+    if (lane == 63) ws[wv] = inc;
     __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < wv; k++) pre += ws[k];
+    lstart[tid] = pre + inc - cnt;
+  }
+  // decoupled look-back: publish the tile's count, sum the counts of the
+  // tiles before it back to the first inclusive prefix, publish that
+  uint64_t* st = status + (uint64_t)blockIdx.x * 256 + tid;
+  uint64_t sum = 0;
+  if (blockIdx.x == 0) {
+    st_agent(st, ST_INC | cnt);
+  } else {
+    st_agent(st, ST_AGG | cnt);
+    const uint64_t* q = st - 256;
+    uint32_t spins = 0;
+    for (;;) {
+      const uint64_t s = ld_agent(q);
+      if (s & ST_INC) { sum += s & ST_VAL; break; }
+      if (s & ST_AGG) { sum += s & ST_VAL; q -= 256; continue; }
+      if (++spins > OS_SPIN_MAX) { atomicOr(err, 1u); break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    st_agent(st, ST_INC | (sum + cnt));
+  }
+  gbase[tid] = gs[d * 256 + tid] + sum;
+  __syncthreads();
+  // the tile in digit order in LDS, then each digit's run to its place
 #pragma unroll
-    for (int w = 0; w < BS_THREADS / 64; w++) wc[w][tid] = pre[w];
-    __syncthreads();
-    if (ok) out[base[v] + wc[wv][v] + rank] = rec;
-    __syncthreads();
-    base[tid] += run;
-#pragma unroll
-    for (int w = 0; w < BS_THREADS / 64; w++) wc[w][tid] = 0;
-    __syncthreads();
+  for (int i = 0; i < OS_ITEMS; i++) {
+    const uint32_t p = (uint32_t)(wv * 64 * OS_ITEMS + i * 64 + lane);
+    if (p < tn) {
+      const uint32_t v = digit_of(rec[i], d);
+      stage[lstart[v] + wcnt[wv][v] + rank[i]] = rec[i];
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = tid; j < tn; j += OS_THREADS) {
+    const BRec r = stage[j];
+    const uint32_t v = digit_of(r, d);
+    out[gbase[v] + (j - lstart[v])] = r;
   }
 }
 
@@ -211,9 +292,9 @@ extern "C" __global__ __launch_bounds__(SCAN_T) void k_scan_fin(uint64_t* a, uin
 }
 
 // Tie runs after a level: sorted records j - 1 and j are tied when they carry
-// the same run id and window and both continue past the window (aux 17).
+// the same run id and window and both continue past the window.
 __device__ __forceinline__ bool tied(const BRec& a, const BRec& b) {
-  return a.aux == 17 && b.aux == 17 && a.run == b.run && a.k.x == b.k.x && a.k.y == b.k.y && a.k.z == b.k.z && a.k.w == b.k.w;
+  return (a.key & 0xFFu) == AUX_MORE && a.key == b.key && a.run == b.run;
 }
 // in[j] = record j belongs to a run of >= 2 tied records; hd[j] = it starts one.
 extern "C" __global__ __launch_bounds__(256) void k_bs_ties(const BRec* r, uint64_t n, uint64_t* in, uint64_t* hd) {
@@ -236,10 +317,9 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r
     const BRec b = r[j];
     const bool head = !(j > 0 && tied(r[j - 1], b));
     BRec o;
-    window(offs, bytes, b.idx, level, o);
+    o.key = window(offs, bytes, b.idx, level);
     o.idx = b.idx;
     o.run = run_base + (uint32_t)(hx[j] + (head ? 1 : 0));
-    o.pad = 0;
     sub[c] = o;
     pos[c] = j;
   }
@@ -271,10 +351,10 @@ namespace {
 
 int grid_for(uint64_t n) { return (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, (n + 255) / 256)); }
 
-// Exclusive scan of a[0, n) in place on stream s; *total (device) = the sum.
-int scan_u64(mox_engine* e, uint64_t* a, uint64_t n, uint64_t* d_total) {
+// Exclusive scan of a[0, n) in place on the engine stream; *d_total (device) =
+// the sum.  sums: scratch of (n + SCAN_TILE - 1) / SCAN_TILE words.
+int scan_u64(mox_engine* e, uint64_t* a, uint64_t n, uint64_t* d_total, uint64_t* sums) {
   const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
-  uint64_t* sums = (uint64_t*)e->s_tmp.p;  // bsort_table sizes s_tmp for the largest scan
   if (n == 0) {
     HIPCHK(hipMemsetAsync(d_total, 0, 8, e->stream));
     return MOX_OK;
@@ -287,31 +367,33 @@ int scan_u64(mox_engine* e, uint64_t* a, uint64_t n, uint64_t* d_total) {
 }
 
 struct BSort {
-  BRec *a, *b;          // records, ping-pong
-  uint64_t *bh;         // tile digit counts (256 x tiles)
-  unsigned long long* gh;  // BS_DIGITS x 256 global histograms (device) ...
-  unsigned long long* h_gh;  // ... and their pinned host copy
-  uint64_t* total;      // scan totals (device), 2 words
-  uint64_t* h_total;    // pinned
+  BRec *a, *b;                // records, ping-pong
+  unsigned long long* gh;     // OS_DIGITS x 256 global histograms (device)
+  uint64_t* gs;               // ... their exclusive scans
+  uint64_t* status;           // look-back status words, 256 per tile
+  unsigned int* err;          // look-back timeout flag
+  unsigned long long* h_gh;   // pinned host copy of gh
 };
 
-// LSD radix sort of recs[0, n) (result in s.a) by (run, window, aux).
+// LSD radix sort of s.a[0, n) by (run, key), one onesweep pass per digit that
+// is not the same for every record; the result ends in s.a.
 int radix_sort(mox_engine* e, BSort& s, uint64_t n) {
   if (n < 2) return MOX_OK;
   hipStream_t st = e->stream;
-  HIPCHK(hipMemsetAsync(s.gh, 0, BS_DIGITS * 256 * 8, st));
+  HIPCHK(hipMemsetAsync(s.gh, 0, OS_DIGITS * 256 * 8, st));
   hipLaunchKernelGGL(k_bs_ghist, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)s.a, n, s.gh);
-  HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, BS_DIGITS * 256 * 8, hipMemcpyDeviceToHost, st));
+  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const unsigned long long*)s.gh, s.gs);
+  HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, OS_DIGITS * 256 * 8, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
-  const uint64_t ntiles = (n + BS_TILE - 1) / BS_TILE;
-  for (int d = 0; d < BS_DIGITS; d++) {
+  const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
+  if (ntiles > 0x7FFFFFFFull) return fail(MOX_EINVAL, "bytewise sort: too many tiles");
+  for (int d = 0; d < OS_DIGITS; d++) {
     bool uniform = false;
     for (int v = 0; v < 256; v++) uniform |= s.h_gh[d * 256 + v] == n;
     if (uniform) continue;  // every record has the same digit: the order stays
-    hipLaunchKernelGGL(k_bs_bhist, dim3((uint32_t)ntiles), dim3(BS_THREADS), 0, st, (const BRec*)s.a, n, d, s.bh, ntiles);
-    if (int rc = scan_u64(e, s.bh, 256 * ntiles, s.total)) return rc;
-    hipLaunchKernelGGL(k_bs_scatter, dim3((uint32_t)ntiles), dim3(BS_THREADS), 0, st, (const BRec*)s.a, s.b, n, d,
-                       (const uint64_t*)s.bh, ntiles);
+    HIPCHK(hipMemsetAsync(s.status, 0, ntiles * 256 * 8, st));
+    hipLaunchKernelGGL(k_os_pass, dim3((uint32_t)ntiles), dim3(OS_THREADS), 0, st, (const BRec*)s.a, s.b, n, d,
+                       (const uint64_t*)s.gs, s.status, s.err);
     HIPCHK(hipGetLastError());
     std::swap(s.a, s.b);
   }
@@ -326,10 +408,14 @@ void bsort_free(mox_engine* e) {
     b->p = nullptr;
     b->cap = 0;
   }
+  if (e->h_bsort) (void)hipHostFree(e->h_bsort);
+  e->h_bsort = nullptr;
 }
 
 // The engine's result table (e->res) in bytewise order, on its GPU: the
 // sorted copy lives in s_counts / s_offs / s_bytes and becomes the result.
+// Scratch (s_tmp) is engine-owned and reused across calls: about 72 bytes per
+// word plus the look-back status (0.5 byte per word).
 int bsort_table(mox_engine* e) {
   HIPCHK(hipSetDevice(e->device));
   auto& r = e->res;
@@ -337,64 +423,56 @@ int bsort_table(mox_engine* e) {
   if (n < 2) return MOX_OK;
   if (n >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: %llu words (at most 2^32 - 1)", (unsigned long long)n);
   hipStream_t st = e->stream;
-  const uint64_t ntiles = (n + BS_TILE - 1) / BS_TILE;
-  const uint64_t scan_n = std::max<uint64_t>(256 * ntiles, n);
-  // scratch: 2 record arrays | bh | 3 u64 arrays of n (flags, heads, positions) | subset records x 2 | scan sums | gh | totals
-  const uint64_t rec = 32 * n, u64n = 8 * n, bhb = 8 * 256 * ntiles, sums = 8 * ((scan_n + SCAN_TILE - 1) / SCAN_TILE + 16);
-  const uint64_t need = 4 * rec + 3 * u64n + bhb + BS_DIGITS * 256 * 8 + 64 + 4096;
+  const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
+  // scratch: records A, B, subset S | flags, heads, positions | status | gh, gs | scan sums | totals, err
+  const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
+  const uint64_t need = 3 * rec + 3 * u64n + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
   int rc;
-  if ((rc = grow_dev(e->s_tmp, sums)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
+  if ((rc = grow_dev(e->s_tmp, need)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
       (rc = grow_dev(e->s_bytes, nb + 64)))
     return rc;
-  uint8_t* pool = nullptr;
-  if (hipMalloc((void**)&pool, need) != hipSuccess) return fail(MOX_ENOMEM, "bytewise sort: hipMalloc(%llu) failed", (unsigned long long)need);
-  uint8_t* q = pool;
-  BSort s;
+  if (!e->h_bsort) HIPCHK(hipHostMalloc((void**)&e->h_bsort, OS_DIGITS * 256 * 8 + 64, hipHostMallocDefault));
+  uint8_t* q = (uint8_t*)e->s_tmp.p;
   BRec* A = (BRec*)q; q += rec;
   BRec* B = (BRec*)q; q += rec;
   BRec* S = (BRec*)q; q += rec;
-  BRec* S2 = (BRec*)q; q += rec;
   uint64_t* fin = (uint64_t*)q; q += u64n;
   uint64_t* fhd = (uint64_t*)q; q += u64n;
   uint64_t* pos = (uint64_t*)q; q += u64n;
-  s.bh = (uint64_t*)q; q += bhb;
-  s.gh = (unsigned long long*)q; q += BS_DIGITS * 256 * 8;
-  s.total = (uint64_t*)q;
-  static thread_local unsigned long long* h_gh = nullptr;  // pinned, per host thread (engine groups sort from one thread)
-  static thread_local uint64_t* h_tot = nullptr;
-  if (!h_gh) {
-    if (hipHostMalloc((void**)&h_gh, BS_DIGITS * 256 * 8 + 64, hipHostMallocDefault) != hipSuccess) h_gh = nullptr;
-    if (hipHostMalloc((void**)&h_tot, 64, hipHostMallocDefault) != hipSuccess) h_tot = nullptr;
-  }
-  auto done = [&](int code) {
-    (void)hipStreamSynchronize(st);
-    (void)hipFree(pool);
-    return code;
-  };
-  if (!h_gh || !h_tot) return done(fail(MOX_ENOMEM, "bytewise sort: pinned host allocation failed"));
-  s.h_gh = h_gh;
-  s.h_total = h_tot;
-  // level 0: every word by its first 16 bytes and length class
+  BSort s;
+  s.status = (uint64_t*)q; q += stb;
+  s.gh = (unsigned long long*)q; q += OS_DIGITS * 256 * 8;
+  s.gs = (uint64_t*)q; q += OS_DIGITS * 256 * 8;
+  uint64_t* ssum = (uint64_t*)q; q += sums;
+  uint64_t* total = (uint64_t*)q; q += 64;
+  s.err = (unsigned int*)q;
+  s.h_gh = e->h_bsort;
+  uint64_t* h_tot = (uint64_t*)(e->h_bsort + OS_DIGITS * 256);
+  HIPCHK(hipMemsetAsync(s.err, 0, 4, st));
+  // level 0: every word by its first 7 bytes and length class
   hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, n, A);
   s.a = A;
   s.b = B;
-  if ((rc = radix_sort(e, s, n))) return done(rc);
-  BRec* R = s.a;  // sorted (A or B)
+  if ((rc = radix_sort(e, s, n))) return rc;
+  BRec* R = s.a;                 // sorted (A or B)
+  BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner
   // levels 1, 2, ...: runs of words sharing all compared bytes
   uint32_t run_base = 1;
   for (uint32_t level = 1;; level++) {
     hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin, fhd);
-    if ((rc = scan_u64(e, fin, n, s.total)) || (rc = scan_u64(e, fhd, n, s.total + 1))) return done(rc);
-    HIPCHK(hipMemcpyAsync(h_tot, s.total, 16, hipMemcpyDeviceToHost, st));
+    if ((rc = scan_u64(e, fin, n, total, ssum)) || (rc = scan_u64(e, fhd, n, total + 1, ssum))) return rc;
+    HIPCHK(hipMemcpyAsync(h_tot, total, 16, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
+    if ((uint32_t)h_tot[2]) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
     const uint64_t m = h_tot[0], runs = h_tot[1];
     if (m == 0) break;
-    if ((uint64_t)run_base + runs >= (1ull << 32)) return done(fail(MOX_EINVAL, "bytewise sort: too many tie runs"));
+    if ((uint64_t)run_base + runs >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
     hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin,
                        (const uint64_t*)fhd, m, run_base, r.offs, r.bytes, level, S, pos);
     s.a = S;
     s.b = S2;
-    if ((rc = radix_sort(e, s, m))) return done(rc);
+    if ((rc = radix_sort(e, s, m))) return rc;
     hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)s.a, m, (const uint64_t*)pos, R);
     HIPCHK(hipGetLastError());
     run_base += (uint32_t)runs;
@@ -403,16 +481,15 @@ int bsort_table(mox_engine* e) {
   uint64_t* oc = (uint64_t*)e->s_counts.p;
   uint64_t* oo = (uint64_t*)e->s_offs.p;
   hipLaunchKernelGGL(k_bs_out1, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, r.counts, r.offs, oc, oo);
-  if ((rc = scan_u64(e, oo, n, oo + n))) return done(rc);
+  if ((rc = scan_u64(e, oo, n, oo + n, ssum))) return rc;
   hipLaunchKernelGGL(k_bs_out2, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, r.offs, r.bytes, (const uint64_t*)oo,
                      (uint8_t*)e->s_bytes.p);
   HIPCHK(hipGetLastError());
-  rc = done(MOX_OK);
   r.counts = oc;
   r.offs = oo;
   r.bytes = (const uint8_t*)e->s_bytes.p;
   r.sorted = true;
-  return rc;
+  return MOX_OK;
 }
 
 }  // namespace mox_host

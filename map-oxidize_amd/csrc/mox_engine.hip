@@ -961,6 +961,9 @@ int mox_abi_version(void) { return MOX_ABI_VERSION; }
 int mox_set_flags(mox_engine* e, uint32_t flags) {
   if (!e) return fail(MOX_EINVAL, "NULL engine");
   e->flags = flags;
+  // an engine group: every member runs its shard's pass with the same flags
+  // (timing modes, dictionary); the group's result flags live in member 0
+  for (int i = 1; i < mox_group_size(e); i++) mox_group_member(e, i)->flags = flags;
   return MOX_OK;
 }
 
@@ -1150,6 +1153,17 @@ int mox_fetch_table(mox_engine* e, mox_table** out) {
   }
   *out = t;
   return MOX_OK;
+}
+
+int mox_sort_result(mox_engine* e) {
+  if (!e) return fail(MOX_EINVAL, "NULL argument");
+  if (int rc = drain_async(e)) return rc;
+  if (!e->have_result) return fail(MOX_ESTATE, "no result: run first");
+  if (e->res.sorted) return MOX_OK;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = bsort_table(e);
+  e->stats.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  return rc;
 }
 
 void mox_table_free(mox_table* t) { free(t); }

@@ -150,6 +150,7 @@ struct mox_engine {
   } res;
   DevBuf g_counts, g_offs, g_bytes, g_recv;  // mox_gather (root)
   DevBuf s_counts, s_offs, s_bytes, s_tmp;    // device bytewise sort (mox_bsort.hip): output + scratch
+  unsigned long long* h_bsort = nullptr;      // pinned: the sort's digit histograms + totals
   Corpus last_corpus{};
   mox_stats stats{};
   hipEvent_t ev[12]{};

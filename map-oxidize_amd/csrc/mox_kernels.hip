@@ -1006,7 +1006,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
       if (sbase < c.lo || sbase + SLOT > c.hi) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
       if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
-      do_row(m, sbase, a, ntok, sl, list, cp);
+      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp);
+      else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
@@ -1739,7 +1740,7 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   uint32_t b = red_bucket(h);
   if (s.dbg) atomicAdd(&s.dbg[0], 1u);
   const uint32_t* tags = reinterpret_cast<const uint32_t*>(s.tag4);
-  uint32_t it = 0;
+  uint32_t it = 0, eqtag = 0;
   bool done = false;
   // wave-level loop (see long_insert): a lane that claims a slot stores the key
   // and publishes its count inside the iteration, never past the loop exit
@@ -1758,7 +1759,7 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
           atomicAdd(&s.cnt[sl], (unsigned long long)c);
           done = true;
         } else {
-          MOX_PATH(s.ctl, PATH_RED_TAG);  // same tag, another key
+          eqtag++;  // same tag, another key (counted after the loop, as in long_insert)
         }
       }
       if (!done) {
@@ -1792,6 +1793,8 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
     }
     __builtin_amdgcn_wave_barrier();
   } while (__any(!done));
+  if (eqtag) MOX_PATH_ADD(s.ctl, PATH_RED_TAG, eqtag);
+  (void)eqtag;
 }
 
 // Fast path for records whose key is already published in its home bucket or

@@ -724,8 +724,11 @@ int group_run(mox_engine* e, const std::vector<Corpus>& c, const std::vector<uin
   const double ms_g = ms_since(t2);
   double ms_s = 0;
   if (e->flags & MOX_F_SORT_BYTES) {
+    // a table too big for the sort's device scratch stays in engine order here:
+    // mox_fetch_table then sorts it on the host, as for one engine
     const auto t3 = std::chrono::steady_clock::now();
-    if ((rc = bsort_table(e))) return rc;
+    rc = bsort_table(e);
+    if (rc != MOX_OK && rc != MOX_ENOMEM) return rc;
     ms_s = ms_since(t3);
   }
   mox_stats& st = e->stats;  // member 0's pass stats are replaced by the group's

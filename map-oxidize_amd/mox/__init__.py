@@ -167,6 +167,7 @@ def lib(path=None):
             "mox_run_range_async": ([VP, VP, sz, sz, sz, I], I),
             "mox_run_wait": ([VP], I),
             "mox_fetch_table": ([VP, P(P(_Table))], I),
+            "mox_sort_result": ([VP], I),
             "mox_get_stats": ([VP, P(Stats)], I),
             "mox_device_alloc": ([VP, sz, P(VP)], I),
             "mox_device_free": ([VP, VP], I),
@@ -345,6 +346,10 @@ class Engine:
         t = ctypes.POINTER(_Table)()
         self._c(self._L.mox_fetch_table(self._h, ctypes.byref(t)))
         return Table(t, self._L)
+
+    def sort_result(self):
+        """Sort the device-resident result bytewise on the GPU (mox_sort_result)."""
+        self._c(self._L.mox_sort_result(self._h))
 
     def stats(self):
         s = Stats()

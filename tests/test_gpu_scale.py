@@ -21,6 +21,7 @@ import coracle
 import mox
 from mox import corpus
 from conftest import assert_tables_equal
+from mox import dist as mdist
 
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
@@ -88,3 +89,47 @@ def test_c5_full_16gib_exact():
     wc, wo, wraw, wtok = coracle.count_arrays(data, nthreads=16)
     assert tokens == wtok
     assert_tables_equal((counts, offs, raw), (wc, wo, wraw))
+
+
+def test_c3_group_two_8gib_shards_exact():
+    """C3 at its per-GPU size: the engine group (2 members on device 0, copy
+    transport) over two 8 GiB byte-range shards of the C3 stream, cut with
+    the bench's left context and 64 KiB look-ahead (mox_run_shards), then the
+    exchange, per-owner reduce, gather and the device bytewise sort
+    (MOX_F_SORT_BYTES).  The gathered table must be the oracle's table of the
+    16 GiB: its digest, and row for row in bytewise order."""
+    n, per = 2, 8 << 30
+    cfg = corpus.CONFIGS["C3"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, n * per)
+    g = mox.Engine(device=0, n_gpus=n, transport=mox.XPORT_COPY, devices=[0] * n, flags=mox.MOX_F_SORT_BYTES,
+                   reserve_bytes=per)
+    bufs = []
+    try:
+        shards = []
+        for r in range(n):
+            lo, hi, ob, oe, end = mdist.shard_range(n * per, n, r, per_rank=per)
+            m = g.member(r)
+            d = m.alloc(hi - lo)
+            bufs.append((m, d))
+            m.h2d(d, data[lo:hi])
+            shards.append((d, hi - lo, ob, oe, end))
+        g.run_shards(shards)
+        st = g.stats()
+        t = g.fetch()
+        counts, offs, raw = t.arrays()
+        tokens = t.tokens
+        t.close()
+    finally:
+        for m, d in bufs:
+            m.free(d)
+        g.close()
+    assert st["n_gpus"] == n and st["ms_sort"] > 0 and st["x_bytes_sent"] > 0
+    assert int(counts.sum()) == tokens == st["tokens"]
+    want, wtok = coracle.count_digest(data, nthreads=16)
+    assert tokens == wtok
+    assert coracle.table_digest(counts, offs, raw) == want
+    # device bytewise order: the rows ARE the oracle's sorted rows
+    wc, wo, wraw, _ = coracle.count_arrays(data, nthreads=16)
+    del data
+    assert counts.size == wc.size
+    assert np.array_equal(counts, wc) and np.array_equal(offs, wo) and raw == wraw
