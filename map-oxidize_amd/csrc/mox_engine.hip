@@ -85,7 +85,9 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   (void)hipDeviceSynchronize();
   free_sized(e);
   Work n = e->w;
-  n.cold_cap = (uint32_t)std::min<uint64_t>((c.cold_cap + 1) & ~1ull, 0xFFFFFFF0u);  // even: k_map's paired records stay sector-aligned
+  // a multiple of 2 QF_MAX: every one of a region's QF_MAX slices holds an even
+  // number of records, so k_map's paired records stay sector-aligned
+  n.cold_cap = (uint32_t)std::min<uint64_t>((c.cold_cap + 2 * QF_MAX - 1) & ~(uint64_t)(2 * QF_MAX - 1), 0xFFFFFFF0u);
   n.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
   n.w_cap = c.w_cap;
   n.u_cap = c.u_cap;
@@ -167,9 +169,10 @@ int alloc_fixed(mox_engine* e) {
   }
   use_dset(e, 0);
   w.map_grid = (uint32_t)std::min(e->n_cu * MAP_WG_PER_CU, MAX_MAP_GRID);
-  if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * 4))) return rc;
-  if ((rc = dalloc(e, (void**)&w.samp, (size_t)w.map_grid * NB * SPLIT_PER_REGION * 4))) return rc;
-  HIPCHK(hipMemset(w.samp, 0, (size_t)w.map_grid * NB * SPLIT_PER_REGION * 4));
+  // region counters and split samples for up to QF_MAX regions per (map workgroup, partition)
+  if ((rc = dalloc(e, (void**)&w.cold_n, (size_t)w.map_grid * NB * QF_MAX * 4))) return rc;
+  if ((rc = dalloc(e, (void**)&w.samp, (size_t)w.map_grid * NB * QF_MAX * SPLIT_PER_REGION * 4))) return rc;
+  HIPCHK(hipMemset(w.samp, 0, (size_t)w.map_grid * NB * QF_MAX * SPLIT_PER_REGION * 4));
   if ((rc = dalloc(e, (void**)&w.spill_n, (size_t)w.map_grid * 4))) return rc;
   // bucket directory block: one allocation, zeroed per run
   size_t dir_bytes = NB * 8 + NB * 4 + NB * 4 + 2 * (NB + 1) * 8 + NB * 8 + (NB + 1) * 8;

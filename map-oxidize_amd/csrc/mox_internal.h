@@ -53,6 +53,7 @@ constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
+constexpr uint32_t QF_MAX = 4;              // most cold regions per (map workgroup, partition) (k_map without a dictionary)
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;
 constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B
@@ -141,7 +142,7 @@ struct Ctl {
   unsigned long long split_k;     // cold records of split partitions
   unsigned long long split_w;     // weighted records of split partitions
   unsigned int n_split;           // partitions split
-  unsigned int pad2;
+  unsigned int qf;                // cold regions per (map workgroup, partition): k_map's QF (0 = 1; mox_kernels.hip)
   unsigned long long n_big;       // entries of big_units (k_reduce work list)
   unsigned long long short_bytes; // table bytes of the short words (long words follow)
   unsigned long long n_mid;       // entries of mid_units (k_reduce_sort2 work list)
@@ -323,8 +324,8 @@ struct Work {  // device buffers of one engine
   unsigned long long* dict_tot;   // DICT_SLOTS counts summed over map workgroups
   // cold records: region (map workgroup g, partition b) = cold[(g*NB + b)*cold_cap ...]
   uint4* cold;                    // map_grid * NB * cold_cap records of 16 B
-  uint32_t* cold_n;               // map_grid * NB records written per region
-  uint32_t* samp;                 // NB * map_grid * SPLIT_PER_REGION: key hashes of every region's first records
+  uint32_t* cold_n;               // map_grid * NB * QF records written per region (ctl->qf regions per map workgroup)
+  uint32_t* samp;                 // NB * map_grid * QF * SPLIT_PER_REGION: key hashes of every region's first records
                                   // (k_map writes them, 0 = none; k_split_count's sample)
   uint32_t cold_cap;
   uint32_t map_grid;

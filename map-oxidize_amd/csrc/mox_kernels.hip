@@ -263,11 +263,26 @@ __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   return hash32((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
 }
 __device__ __forceinline__ uint32_t bucket_of(uint32_t h) { return h >> (32 - NB_LOG2); }
-// Records map workgroup g wrote into its region of partition b.  Partition-major
-// (b * map_grid + g): a partition's row is contiguous for k_hist's sums, k_reduce's
-// region prefix and the split kernels' region lists.
-__device__ __forceinline__ uint32_t& cold_n_at(const Work& w, uint32_t g, uint32_t b) {
-  return w.cold_n[(uint64_t)b * w.map_grid + g];
+// Cold-record regions.  Map workgroup g writes partition b's records to its
+// region (g, b).  Without a dictionary (high-cardinality input) it keeps QF
+// regions per partition instead, one per value q of the log2(QF) hash bits
+// right below the partition bits, of cold_cap / QF records each, so that
+// k_split_scatter can move a partition one q-slice at a time (a QF-th of its
+// sub-buckets open at once).  Readers see RG = QF x map_grid regions per
+// partition ("virtual map workgroups" g' = QF g + q) of RC = cold_cap / QF
+// records: region (g', b) starts at cold + (g' NB + b) RC.  k_map records QF
+// in ctl->qf (0 = 1: dictionary passes and reduce-only passes).
+__device__ __forceinline__ uint32_t hc_qf(uint32_t map_grid) {
+  return map_grid * 4u <= (uint32_t)MAX_MAP_GRID ? 4u : (map_grid * 2u <= (uint32_t)MAX_MAP_GRID ? 2u : 1u);
+}
+__device__ __forceinline__ uint32_t reg_qf(const Work& w) { const uint32_t q = w.ctl->qf; return q ? q : 1u; }
+__device__ __forceinline__ uint32_t reg_grid(const Work& w) { return w.map_grid * reg_qf(w); }
+__device__ __forceinline__ uint32_t reg_cap(const Work& w) { return w.cold_cap / reg_qf(w); }
+// Records written into region (g, b) of a grid of RG regions per partition.
+// Partition-major (b RG + g): a partition's row is contiguous for k_hist's
+// sums, k_reduce's region prefix and the split kernels' region lists.
+__device__ __forceinline__ uint32_t& cold_n_at(const Work& w, uint32_t RG, uint32_t g, uint32_t b) {
+  return w.cold_n[(uint64_t)b * RG + g];
 }
 // byte length of a short key (lowered word, zero padded to 16 bytes, no NUL inside)
 __device__ __forceinline__ uint32_t key_len16(uint4 k) {
@@ -292,12 +307,12 @@ constexpr uint32_t PS_EMPTY = 0u, PS_BUSY = 1u, PS_FULL = 2u;
 struct MapLds {
   uint4* dkey;      // DICT_SLOTS 16-byte keys (zero = empty: a real key is never zero)
   uint32_t* dcnt;   // DICT_SLOTS
-  uint32_t* bcnt;   // NB: cold records this workgroup wrote per partition
+  uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's space)
   uint32_t* misc;   // [0] spills [1] row ticket
   uint4* masktab;   // [17]: byte masks keeping the first len bytes of a 16-byte key
-  // no dictionary (dict_n == 0): pair slots per partition, inside dkey's space
-  uint4* pend;      // NB parked records
-  uint32_t* pst;    // NB slot states (PS_*)
+  // no dictionary (dict_n == 0): pair slots per region, inside dkey's space
+  uint4* pend;      // NB x qf parked records
+  uint32_t* pst;    // NB x qf slot states (PS_*)
 };
 
 typedef const __attribute__((address_space(4))) Work* KWork;  // constant (kernarg) address space: scalar loads
@@ -307,7 +322,13 @@ struct MapCtx {
   KWork wk;          // the kernel argument itself (kernarg segment), for the rare paths
   MapLds s;
   uint32_t dict_n;
+  uint32_t qf, qb;   // regions per partition (QF, 1 with a dictionary) and log2(qf)
+  uint32_t rg, rc;   // regions per partition over the grid (qf map_grid), records per region (cold_cap / qf)
 };
+// This workgroup's region q of partition b.
+__device__ __forceinline__ uint4* region_of(const MapCtx& m, uint32_t b, uint32_t q) {
+  return m.w.cold + ((uint64_t)(blockIdx.x * m.qf + q) * NB + b) * m.rc;
+}
 // Work fields of the rare paths (spills, Unicode lane, long words, error
 // flags), loaded where they are used: the opaque pointer keeps the compiler from
 // hoisting these loads to the kernel entry, where ~20 more SGPRs would stay live
@@ -390,23 +411,27 @@ __device__ __forceinline__ int pair_try(uint32_t* pst, uint4* pend, uint32_t slo
 // of every (workgroup, partition) region, written when a record lands at such a
 // position (rare: 4 of ~150 records per region at C2), so that the split
 // decision reads 4 KiB per partition instead of 1,024 scattered records.
-__device__ __forceinline__ void note_sample(const MapCtx& m, uint32_t b, uint32_t pos, uint32_t h) {
-  if (pos < SPLIT_PER_REGION) rare(m).samp[((uint64_t)b * rare(m).map_grid + blockIdx.x) * SPLIT_PER_REGION + pos] = h;
+__device__ __forceinline__ void note_sample(const MapCtx& m, uint32_t b, uint32_t q, uint32_t pos, uint32_t h) {
+  if (pos < SPLIT_PER_REGION)
+    rare(m).samp[((uint64_t)b * m.rg + blockIdx.x * m.qf + q) * SPLIT_PER_REGION + pos] = h;
 }
-__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t b, uint32_t h, uint4 key) {
+// No dictionary: slot B = the partition bits and the qb bits below them
+// (partition b = B >> qb, region q = B & (qf - 1)).
+__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t h, uint4 key) {
+  const uint32_t b = B >> m.qb, qr = B & (m.qf - 1);
   bool done = false;
   do {
     if (!done) {
       uint4 q;
-      const int r = pair_try(m.s.pst, m.s.pend, b, key, &q);
+      const int r = pair_try(m.s.pst, m.s.pend, B, key, &q);
       if (r == 2) {
-        const uint32_t pos = atomicAdd(&m.s.bcnt[b], 2u);
+        const uint32_t pos = atomicAdd(&m.s.bcnt[B], 2u);
         if (pos < SPLIT_PER_REGION) {
-          note_sample(m, b, pos, hash32(q.x, q.y, q.z, q.w));
-          note_sample(m, b, pos + 1, h);
+          note_sample(m, b, qr, pos, hash32(q.x, q.y, q.z, q.w));
+          note_sample(m, b, qr, pos + 1, h);
         }
-        if (pos + 1 < m.w.cold_cap) {
-          uint4* o = m.w.cold + ((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos;
+        if (pos + 1 < m.rc) {
+          uint4* o = region_of(m, b, qr) + pos;
           o[0] = q;
           o[1] = key;
         } else {
@@ -423,11 +448,11 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-  if (m.dict_n == 0) { cold_pair(m, b, h, key); return; }
+  if (m.dict_n == 0) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key); return; }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
-  if (pos < SPLIT_PER_REGION) note_sample(m, b, pos, h);
-  if (pos < m.w.cold_cap) {
-    m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos] = key;
+  if (pos < SPLIT_PER_REGION) note_sample(m, b, 0, pos, h);
+  if (pos < m.rc) {
+    region_of(m, b, 0)[pos] = key;
     return;
   }
   cold_spill(m, key);
@@ -704,8 +729,8 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     if (!miss[u]) continue;
     const uint32_t b = bucket_of(h[u]);
     const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
-    if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, pos[u], h[u]);
-    if (pos[u] < m.w.cold_cap) m.w.cold[((uint64_t)blockIdx.x * NB + b) * m.w.cold_cap + pos[u]] = key;
+    if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, 0, pos[u], h[u]);
+    if (pos[u] < m.rc) region_of(m, b, 0)[pos[u]] = key;
     else cold_spill(m, key);
   }
 }
@@ -909,19 +934,27 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint8_t* ring = sp; sp += RING * SLOT;
   uint16_t* lists = (uint16_t*)sp; sp += MAP_CONSUMERS * 2 * TOKMAX;
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
-  m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB);       // = PS_EMPTY
-  static_assert(NB * 16 + NB * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
+  m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
+  static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
+  static_assert(NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
+  m.qf = m.dict_n ? 1u : hc_qf(w.map_grid);
+  m.qb = m.qf == 4u ? 2u : (m.qf == 2u ? 1u : 0u);
+  m.rg = w.map_grid * m.qf;
+  m.rc = w.cold_cap / m.qf;
+  if (!m.dict_n) m.s.bcnt = m.s.dcnt;  // NB x qf region counters
   // without a dictionary the key array is zero (no real key is zero, so nothing
   // would hit; that case takes pass_c, and the pair slots live there)
   for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
     m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);
     m.s.dcnt[i] = 0;
   }
-  for (int i = tid; i < NB; i += MAP_THREADS) {
-    m.s.bcnt[i] = resume ? cold_n_at(w, blockIdx.x, i) : 0u;
+  __syncthreads();  // (no dictionary: the region counters live in dcnt's space)
+  for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {
+    const uint32_t b = i >> m.qb, q = i & (m.qf - 1);
+    m.s.bcnt[i] = resume ? cold_n_at(w, m.rg, blockIdx.x * m.qf + q, b) : 0u;
   }
   if (tid < 4) m.s.misc[tid] = (resume && tid == 0) ? w.spill_n[blockIdx.x] : 0u;
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
@@ -1021,13 +1054,14 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   }
   __syncthreads();
   if (m.dict_n == 0) {  // records still parked in pair slots: written as singles
-    for (int i = tid; i < NB; i += MAP_THREADS) {
+    for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {
       if (m.s.pst[i] != PS_FULL) continue;
+      const uint32_t b = i >> m.qb, qr = i & (m.qf - 1);
       const uint32_t pos = atomicAdd(&m.s.bcnt[i], 1u);
       const uint4 q = m.s.pend[i];
-      note_sample(m, i, pos, hash32(q.x, q.y, q.z, q.w));
-      if (pos < w.cold_cap) w.cold[((uint64_t)blockIdx.x * NB + i) * w.cold_cap + pos] = m.s.pend[i];
-      else cold_spill(m, m.s.pend[i]);
+      note_sample(m, b, qr, pos, hash32(q.x, q.y, q.z, q.w));
+      if (pos < m.rc) region_of(m, b, qr)[pos] = q;
+      else cold_spill(m, q);
     }
     __syncthreads();
   }
@@ -1044,10 +1078,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   if (tid == 0) { s_tok = 0; s_cmax = 0; }
   __syncthreads();
   uint32_t cmax = 0;
-  for (int i = tid; i < NB; i += MAP_THREADS) {
-    const uint32_t cnt = m.s.bcnt[i];
-    cold_n_at(w, blockIdx.x, i) = cnt < w.cold_cap ? cnt : w.cold_cap;
-    for (uint32_t j = cnt; j < SPLIT_PER_REGION; j++) note_sample(m, i, j, 0u);  // no record there (0 = none)
+  for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {
+    const uint32_t cnt = m.s.bcnt[i], b = i >> m.qb, q = i & (m.qf - 1);
+    cold_n_at(w, m.rg, blockIdx.x * m.qf + q, b) = cnt < m.rc ? cnt : m.rc;
+    for (uint32_t j = cnt; j < SPLIT_PER_REGION; j++) note_sample(m, b, q, j, 0u);  // no record there (0 = none)
     cmax = cnt > cmax ? cnt : cmax;
   }
   for (int off = 32; off > 0; off >>= 1) {
@@ -1064,8 +1098,9 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     const uint32_t sn = m.s.misc[0];
     w.spill_n[blockIdx.x] = sn < w.spill_cap ? sn : w.spill_cap;
     if (sn) atomicMax(&w.ctl->spill_need, sn);
-    if (s_cmax) atomicMax(&w.ctl->cold_need, (unsigned long long)s_cmax);
+    if (s_cmax) atomicMax(&w.ctl->cold_need, (unsigned long long)s_cmax * m.qf);  // cold_cap that covers it
     if (s_tok) atomicAdd(&w.ctl->tokens, s_tok);
+    if (blockIdx.x == 0) w.ctl->qf = m.qf;  // region geometry for the readers
   }
 }
 
@@ -1116,8 +1151,8 @@ extern "C" __global__ void k_init(Work w, unsigned long long w_n, uint32_t flags
   if (flags & (INIT_DICT | INIT_DICT_SIDE)) zero_words(w.dict_tot, DICT_SLOTS * 8, t, stride);
   else if (t == 0) { w.dict_hist[DH_N] = 0; w.dict_hist[DH_T] = 0; }  // no dictionary this pass
   if (flags & INIT_MAP) {  // reduce-only pass: no map regions, no split sample
-    zero_words(w.cold_n, (uint64_t)w.map_grid * NB * 4, t, stride);
-    zero_words(w.samp, (uint64_t)w.map_grid * NB * SPLIT_PER_REGION * 4, t, stride);
+    zero_words(w.cold_n, (uint64_t)w.map_grid * NB * QF_MAX * 4, t, stride);
+    zero_words(w.samp, (uint64_t)w.map_grid * NB * QF_MAX * SPLIT_PER_REGION * 4, t, stride);
     zero_words(w.spill_n, (uint64_t)w.map_grid * 4, t, stride);
   }
 }
@@ -1610,9 +1645,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_hist(Work w) {
   for (int i = threadIdx.x; i < NB; i += blockDim.x) hw[i] = 0;
   // partitions g, g + G, ...: the sum of their contiguous cold_n rows (one plain
   // agent-scope store each instead of a global atomic per (workgroup, partition))
+  const uint32_t RG = reg_grid(w);  // <= MAX_MAP_GRID = blockDim (hc_qf)
   for (uint32_t b = g; b < NB; b += G) {
     uint64_t tot;
-    (void)block_exscan(threadIdx.x < G ? cold_n_at(w, threadIdx.x, b) : 0u, hsum, tot);
+    (void)block_exscan(threadIdx.x < RG ? cold_n_at(w, RG, threadIdx.x, b) : 0u, hsum, tot);
     if (threadIdx.x == 0) st_agent((unsigned long long*)&w.b_recs[b], (unsigned long long)tot);
   }
   __syncthreads();
@@ -1701,9 +1737,6 @@ constexpr int RED_SLOTS = 4 * RED_BK;
 constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort width
 #ifndef MOX_RED_UNROLL
 #define MOX_RED_UNROLL 2
-#endif
-#ifndef MOX_RED_FLAT
-#define MOX_RED_FLAT 1  // k_reduce streams a unit's records as one flat range, equal shares per wave
 #endif
 constexpr int RED_UNROLL = MOX_RED_UNROLL;
 constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
@@ -1868,9 +1901,9 @@ __device__ __forceinline__ uint32_t red_bin(uint32_t h, uint32_t shift) { return
 // regions go in groups of 64: lane k holds the size of the group's k-th region.
 template <class F>
 __device__ __forceinline__ void for_cold_group(const Work& w, uint32_t b, F f, uint32_t g0, uint32_t nreg, int lane,
-                                               int nwv) {
+                                               int nwv, uint32_t RG, uint32_t RC) {
   const int wv = 0;  // regions g0 + k nwv
-  const uint32_t myn = lane < (int)nreg ? cold_n_at(w, g0 + lane * nwv, b) : 0u;
+  const uint32_t myn = lane < (int)nreg ? cold_n_at(w, RG, g0 + lane * nwv, b) : 0u;
   const uint64_t nonempty = __ballot(myn != 0);
   auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
     const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
@@ -1880,7 +1913,7 @@ __device__ __forceinline__ void for_cold_group(const Work& w, uint32_t b, F f, u
   auto load = [&](uint32_t kq, uint32_t iq, uint4 (&v)[4]) {  // unconditional: uniform vmcnt
     const uint32_t kc = kq < nreg ? kq : 0u;
     const uint32_t n = __builtin_amdgcn_readlane(myn, kc);
-    const uint4* reg = w.cold + ((uint64_t)(g0 + wv + kc * nwv) * NB + b) * w.cold_cap;
+    const uint4* reg = w.cold + ((uint64_t)(g0 + wv + kc * nwv) * NB + b) * RC;
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       const uint32_t i = iq + u * 64 + lane;
@@ -1921,10 +1954,22 @@ __device__ __forceinline__ void for_cold_group(const Work& w, uint32_t b, F f, u
 template <class F>
 __device__ __forceinline__ void for_partition_cold(const Work& w, uint32_t b, F f) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
-  const uint32_t G = w.map_grid;
+  const uint32_t G = reg_grid(w), RC = reg_cap(w);
   const uint32_t nall = G > (uint32_t)wv ? (G - wv + nwv - 1) / nwv : 0;
   for (uint32_t r0 = 0; r0 < nall; r0 += 64)
-    for_cold_group(w, b, f, wv + r0 * nwv, nall - r0 < 64 ? nall - r0 : 64u, lane, nwv);
+    for_cold_group(w, b, f, wv + r0 * nwv, nall - r0 < 64 ? nall - r0 : 64u, lane, nwv, G, RC);
+}
+
+// The cold records of partition b in the regions q, q + qf, ... (slice q of
+// every map workgroup: the records whose qb hash bits below the partition bits
+// are q), one wave per region as in for_partition_cold.
+template <class F>
+__device__ __forceinline__ void for_partition_cold_q(const Work& w, uint32_t b, uint32_t q, uint32_t qf, F f) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+  const uint32_t G = reg_grid(w), RC = reg_cap(w), M = w.map_grid;
+  const uint32_t nall = M > (uint32_t)wv ? (M - wv + nwv - 1) / nwv : 0;
+  for (uint32_t r0 = 0; r0 < nall; r0 += 64)
+    for_cold_group(w, b, f, q + qf * (wv + r0 * nwv), nall - r0 < 64 ? nall - r0 : 64u, lane, qf * nwv, G, RC);
 }
 
 // ------------------------------------------------------------------ high-cardinality split
@@ -1952,7 +1997,9 @@ __device__ __forceinline__ void split_count(const Work& w) {
   // sample = the first SPLIT_PER_REGION cold records of every map workgroup's
   // region (spread over the whole corpus; their key hashes, noted by k_map),
   // topped up with weighted records
-  const uint32_t G = w.map_grid;
+  const uint32_t G = reg_grid(w);
+  // sample slots spread over all regions (QF regions per map workgroup: every QF-th region's first records)
+  const uint32_t sstride = G * SPLIT_PER_REGION > SPLIT_SAMPLE ? G * SPLIT_PER_REGION / SPLIT_SAMPLE : 1u;  // QF when RG = 4 x 256
   auto mark = [&](uint32_t h) {
     const uint32_t bit = hbits(h, NB_LOG2, 12);  // LC_BITS = 2^12
     atomicOr(&bm[bit >> 5], 1u << (bit & 31));
@@ -1964,7 +2011,8 @@ __device__ __forceinline__ void split_count(const Work& w) {
 #pragma unroll
     for (int j = 0; j < PER; j++) {  // k_map's note_sample: contiguous per partition, 0 = no record
       const uint32_t idx = tid + j * SC_THREADS;
-      v[j] = idx < SPLIT_SAMPLE && idx < G * SPLIT_PER_REGION ? w.samp[(uint64_t)b * G * SPLIT_PER_REGION + idx] : 0u;
+      const uint32_t rj = idx / SPLIT_PER_REGION, reg = rj * sstride + rj % sstride;  // every map workgroup, every q
+      v[j] = idx < SPLIT_SAMPLE && reg < G ? w.samp[((uint64_t)b * G + reg) * SPLIT_PER_REGION + idx % SPLIT_PER_REGION] : 0u;
     }
 #pragma unroll
     for (int j = 0; j < PER; j++)
@@ -2120,10 +2168,98 @@ extern "C" __global__ __launch_bounds__(SC_THREADS) void k_unit_scan(Work w) { u
 // retries, and the BUSY holder finishes within the same loop iteration, so no
 // lane ever waits on another wave's progress.  Leftover single records are
 // written after the stream.
+#ifndef MOX_SPLIT_STAGE
+#define MOX_SPLIT_STAGE 1  // slices of QF-region partitions go out LDS-staged (0: record pairs, the round-3 scheme)
+#endif
+// LDS-staged scatter of slice q (regions q, q + qf, ...) of partition b: the
+// slice's records in chunks of SST_CH, each chunk counting-sorted by sub-bucket
+// in LDS, then every sub-bucket's run of the chunk written with consecutive
+// stores (a slice opens nsub / qf sub-buckets: ~6 records, 96 B, per run at
+// C4 16 GiB instead of one 32-byte pair per store).
+constexpr int SST_CH = 6144;
+constexpr int SST_PER = SST_CH / 1024;
+struct SplitStage {
+  uint4* stage;      // SST_CH records of the chunk, by sub-bucket
+  uint16_t* sidx;    // SST_CH: each staged record's sub-bucket (slice-local)
+  uint32_t* lcnt;    // 1024: the chunk's records per slice-local sub-bucket
+  uint32_t* lst;     // 1024: their first stage position
+  uint32_t* gb;      // 1024: their first output record (split_k, partition-relative)
+  uint32_t* rpre;    // MAX_MAP_GRID + 1: prefix of the slice's region sizes
+};
+__device__ void split_stage_slice(const Work& w, uint32_t b, uint32_t q, uint32_t qf, uint32_t kk, uint32_t* cc, uint4* ok,
+                                  uint64_t tc, uint64_t kb, const SplitStage& S, uint64_t* wsum) {
+  const int tid = threadIdx.x;
+  const uint32_t G = reg_grid(w), RC = reg_cap(w), M = w.map_grid;
+  const uint32_t qb = qf == 4u ? 2u : 1u, F = (1u << kk) >> qb, sb0 = q * F;
+  {
+    uint64_t tot;
+    const uint32_t n = tid < (int)M ? cold_n_at(w, G, q + qf * tid, b) : 0u;
+    const uint64_t ex = block_exscan(n, wsum, tot);
+    if (tid < (int)M) S.rpre[tid] = (uint32_t)ex;
+    if (tid == 0) S.rpre[M] = (uint32_t)tot;
+    if (tid < (int)F) S.lcnt[tid] = 0;
+  }
+  __syncthreads();
+  const uint32_t n = S.rpre[M];
+  uint32_t r = 0, rs = 0, re = S.rpre[1];  // this thread's region walk (its indices only grow)
+  for (uint32_t c0 = 0; c0 < n; c0 += SST_CH) {
+    uint4 k[SST_PER];
+    uint32_t sub[SST_PER], rk[SST_PER];
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int j = 0; j < SST_PER; j++) {
+      const uint32_t i = c0 + j * 1024 + tid;
+      const bool ok_i = i < n;
+      while (ok_i && i >= re) { r++; rs = re; re = S.rpre[r + 1]; }
+      const uint4* p = w.cold + ((uint64_t)(q + qf * r) * NB + b) * RC + (ok_i ? i - rs : 0u);
+      const u32x4 x = *reinterpret_cast<const u32x4*>(ok_i ? p : w.cold);
+      k[j] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+#pragma unroll
+    for (int j = 0; j < SST_PER; j++) {
+      const uint32_t i = c0 + j * 1024 + tid;
+      sub[j] = i < n ? hbits(hash32(k[j].x, k[j].y, k[j].z, k[j].w), NB_LOG2, kk) - sb0 : 0xFFFFu;
+      rk[j] = i < n ? atomicAdd(&S.lcnt[sub[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    {  // slice-local sub-bucket starts in the stage; their output cursors advance
+      uint64_t tot;
+      const uint32_t cnt = tid < (int)F ? S.lcnt[tid] : 0u;
+      const uint32_t ex = (uint32_t)block_exscan(cnt, wsum, tot);
+      if (tid < (int)F) {
+        S.lst[tid] = ex;
+        S.gb[tid] = cc[sb0 + tid];
+        cc[sb0 + tid] += cnt;
+        S.lcnt[tid] = 0;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SST_PER; j++)
+      if (sub[j] != 0xFFFFu) {
+        const uint32_t pos = S.lst[sub[j]] + rk[j];
+        S.stage[pos] = k[j];
+        S.sidx[pos] = (uint16_t)sub[j];
+      }
+    __syncthreads();
+    const uint32_t nc = n - c0 < (uint32_t)SST_CH ? n - c0 : (uint32_t)SST_CH;
+    for (uint32_t j = tid; j < nc; j += 1024) {
+      const uint32_t sb = S.sidx[j];
+      const uint32_t d = S.gb[sb] + (j - S.lst[sb]);
+      if (MOX_CHK(w, d < tc && kb + d < w.split_k_cap, CHK_SPLIT_K)) ok[d] = S.stage[j];
+    }
+    __syncthreads();  // the stage is rewritten by the next chunk
+  }
+}
+
 extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   __shared__ uint32_t cc[SUB_N], cw[SUB_N];
-  __shared__ uint32_t pst[SUB_N];
-  __shared__ uint4 pend[SUB_N];
+  // pair slots, or (staged slices) the stage: one LDS area
+  constexpr int PAIR_B = SUB_N * 4 + SUB_N * 16;
+  constexpr int STAGE_B = SST_CH * 16 + SST_CH * 2 + 3 * 1024 * 4 + (MAX_MAP_GRID + 4) * 4;
+  __shared__ __attribute__((aligned(16))) uint8_t xs[PAIR_B > STAGE_B ? PAIR_B : STAGE_B];
+  uint32_t* pst = reinterpret_cast<uint32_t*>(xs);
+  uint4* pend = reinterpret_cast<uint4*>(xs + SUB_N * 4);
   __shared__ uint64_t wsum[16];
   const uint32_t b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -2175,7 +2311,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   uint4* ok = w.split_k + kb;
   // (the lambda runs under a per-record lane mask; the pair loop is the same
   // wave-level loop as k_map's cold_pair)
-  for_partition_cold(w, b, [&](uint4 k) {
+  auto put = [&](uint4 k) {
     const uint32_t sb = hbits(hash32(k.x, k.y, k.z, k.w), NB_LOG2, kk);
     bool done = false;
     do {
@@ -2193,7 +2329,30 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
       }
       __builtin_amdgcn_wave_barrier();
     } while (__any(!done));
-  });
+  };
+  // slice by slice (k_map without a dictionary keeps qf slices per region, by
+  // the hash bits right below the partition bits = the top sub-bucket bits): a
+  // slice's records go to a qf-th of the sub-buckets, so fewer output lines are
+  // open at once
+  const uint32_t qf = reg_qf(w);
+  const bool sliced = qf > 1 && kk >= (qf == 4u ? 2u : 1u);
+  if (sliced && MOX_SPLIT_STAGE) {
+    SplitStage S;
+    S.stage = reinterpret_cast<uint4*>(xs);
+    S.sidx = reinterpret_cast<uint16_t*>(xs + SST_CH * 16);
+    S.lcnt = reinterpret_cast<uint32_t*>(xs + SST_CH * 18);
+    S.lst = S.lcnt + 1024;
+    S.gb = S.lst + 1024;
+    S.rpre = S.gb + 1024;
+    for (uint32_t q = 0; q < qf; q++) split_stage_slice(w, b, q, qf, kk, cc, ok, tc, kb, S, wsum);
+  } else if (sliced) {
+    for (uint32_t q = 0; q < qf; q++) {
+      for_partition_cold_q(w, b, q, qf, put);
+      __syncthreads();
+    }
+  } else {
+    for_partition_cold(w, b, put);
+  }
   const uint64_t w0 = w.w_off[b], w1 = w.w_off[b + 1];
   WRec* ow = w.split_w + wb;
   for (uint64_t i = w0 + tid; i < w1; i += blockDim.x) {
@@ -2202,6 +2361,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
     if (MOX_CHK(w, p < tw && wb + p < w.split_w_cap, CHK_SPLIT_W)) ow[p] = r;
   }
   __syncthreads();
+  if (sliced && MOX_SPLIT_STAGE) return;  // (no pair slots)
   // leftover singles (odd counts)
 #pragma unroll
   for (int j = 0; j < SUB_PER_T; j++) {
@@ -2239,7 +2399,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   if (threadIdx.x < 4) dbgc[threadIdx.x] = 0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NWV = RED_THREADS / 64;
-  const uint32_t G = w.map_grid;
+  const uint32_t G = reg_grid(w), RC = reg_cap(w);  // cold regions per partition (<= MAX_MAP_GRID), records per region
   uint32_t* tags = reinterpret_cast<uint32_t*>(s.tag4);
   // an overflowed map, directory or split means this attempt is rerun with
   // larger buffers: its records are incomplete (nothing downstream reads them)
@@ -2283,7 +2443,6 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
     // split unit: its contiguous cold range is cut into NWV wave chunks
     const uint64_t kin0 = split ? ud.in_off : 0;
     const uint32_t kin_n = split ? ud.in_n : 0;
-    [[maybe_unused]] const uint32_t kchunk = (kin_n + NWV - 1) / NWV;
     const bool stamp = MOX_ABL(w.dbg, DBG_STAMP) && tid == 0 && !split;
     if (stamp) w.stamps[b * 8 + 0] = __builtin_amdgcn_s_memrealtime();
     uint32_t kk = 0;
@@ -2295,19 +2454,16 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         s.cnt[i] = 0;
       }
       if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
-#if MOX_RED_FLAT
       // region prefix of a whole partition (the map workgroups' regions one after
       // another), in the sort index / bin space, which is free until the sort
       if (!split) {
         uint64_t tot;
-        const uint64_t ex = block_exscan(tid < (int)G ? cold_n_at(w, tid, b) : 0u, red_wsum, tot);
+        const uint64_t ex = block_exscan(tid < (int)G ? cold_n_at(w, G, tid, b) : 0u, red_wsum, tot);
         if (tid < (int)G) rpre[tid] = (uint32_t)ex;
         if (tid == 0) rpre[G] = (uint32_t)tot;
       }
-#endif
       __syncthreads();
       for (int rep = 0; rep < (MOX_ABL(w.dbg, DBG_RED_TWICE) ? 2 : 1); rep++)
-#if MOX_RED_FLAT
       // cold records: the unit's records as one flat index space (whole
       // partition: region g = map workgroup g, at rpre[g]; split unit: one
       // contiguous range), cut into NWV equal wave shares in 64-record steps so
@@ -2320,8 +2476,8 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         const uint32_t per = (((n + NWV - 1) / NWV) + 63) & ~63u;
         const uint32_t a0 = (uint32_t)wv * per < n ? (uint32_t)wv * per : n;
         const uint32_t a1 = n - a0 < per ? n : a0 + per;
-        const uint4* ubase = split ? w.split_k + kin0 : w.cold + b * w.cold_cap;  // region g at + g NB cold_cap
-        const uint64_t gstride = (uint64_t)NB * w.cold_cap;
+        const uint4* ubase = split ? w.split_k + kin0 : w.cold + b * RC;  // region g at + g NB RC
+        const uint64_t gstride = (uint64_t)NB * RC;
         // lane state: region r holds flat records [rs, re)
         uint32_t r = 0, rs = 0, re = split ? 0xFFFFFFFFu : 0u;
         if (!split && a0 < a1) {  // region of a0: last r with rpre[r] <= a0 (wave-uniform search)
@@ -2388,94 +2544,6 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           c += CH;
         }
       }
-#else
-      // cold records: wave wv streams its regions (whole partition: regions
-      // g = wv, wv + NWV, ...; split unit: one chunk) 64 x RED_UNROLL records at
-      // a time, the next chunk's loads in flight while the current one is
-      // inserted.  Lane k holds the size of the wave's k-th region.
-      {
-        uint32_t nreg, myn;
-        if (split) {
-          nreg = 1;
-          const uint64_t a = (uint64_t)wv * kchunk;
-          myn = lane == 0 && a < kin_n ? (uint32_t)(kin_n - a < kchunk ? kin_n - a : kchunk) : 0u;
-        } else {
-          nreg = G > (uint32_t)wv ? (G - wv + NWV - 1) / NWV : 0;  // <= 64 (G <= MAX_MAP_GRID)
-          myn = lane < (int)nreg ? cold_n_at(w, wv + lane * NWV, b) : 0u;
-        }
-        const uint64_t nonempty = __ballot(myn != 0);
-        auto next_region = [&](uint32_t k) -> uint32_t {  // first non-empty region index >= k
-          const uint64_t m = k >= 64 ? 0ull : (nonempty >> k) << k;
-          return m ? (uint32_t)__builtin_ctzll(m) : nreg;
-        };
-        // Loads are unconditional (an index past the region end, or a region
-        // past the last, reads a valid dummy record; process() masks by
-        // position), so every chunk issues exactly RED_UNROLL loads and the
-        // compiler can wait for one chunk while the next is still in flight.
-        auto load = [&](uint32_t kq, uint32_t iq, uint4 (&v)[RED_UNROLL]) {
-          const uint32_t kc = kq < nreg ? kq : 0u;  // nreg >= 1 inside the loop
-          const uint32_t n = __builtin_amdgcn_readlane(myn, kc);
-          const uint4* reg = split ? w.split_k + kin0 + (uint64_t)wv * kchunk
-                                   : w.cold + ((uint64_t)(wv + kc * NWV) * NB + b) * w.cold_cap;
-          typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
-            const uint32_t i = iq + u2 * 64 + lane;
-            const u32x4 x = *reinterpret_cast<const u32x4*>(reg + (i < n ? i : 0u));
-            v[u2] = make_uint4(x.x, x.y, x.z, x.w);
-          }
-        };
-        // ping-pong buffers A / B (no register copy between them): the chunk
-        // in one is inserted while the other's loads are in flight
-        auto process = [&](const uint4 (&cur)[RED_UNROLL], uint32_t kq, uint32_t iq) {
-          if (__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;  // redone anyway
-          const uint32_t n = __builtin_amdgcn_readlane(myn, kq);
-          uint32_t h[RED_UNROLL];
-          bool todo[RED_UNROLL];
-          RED_MARK(0);
-#pragma unroll
-          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
-            h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
-            todo[u2] = iq + u2 * 64 + lane < n && in_sub(h[u2], shift0, kk, sub);
-          }
-          RED_MARK(1);
-          if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
-#pragma unroll
-            for (int u2 = 0; u2 < RED_UNROLL; u2++)
-              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
-            RED_MARK(2);
-#pragma unroll
-            for (int u2 = 0; u2 < RED_UNROLL; u2++)
-              if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
-            RED_MARK(3);
-          } else {
-            asm volatile("" ::"v"(h[0]), "v"(h[1]));
-          }
-        };
-        auto advance = [&](uint32_t& kq, uint32_t& iq) {  // the chunk after (kq, iq)
-          iq += 64 * RED_UNROLL;
-          if (iq >= __builtin_amdgcn_readlane(myn, kq)) { kq = next_region(kq + 1); iq = 0; }
-        };
-        uint32_t k = next_region(0), i0 = 0;
-        uint4 A[RED_UNROLL], B[RED_UNROLL];
-        if (k < nreg) load(k, 0, A);
-        while (k < nreg) {
-          uint32_t kb = k, ib = i0;
-          advance(kb, ib);
-          load(kb, ib, B);
-          process(A, k, i0);
-          k = kb;
-          i0 = ib;
-          if (k >= nreg) break;
-          uint32_t ka = k, ia = i0;
-          advance(ka, ia);
-          load(ka, ia, A);
-          process(B, k, i0);
-          k = ka;
-          i0 = ia;
-        }
-      }
-#endif
       if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
       for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
         const WRec rr = wsrc[i];

@@ -3,6 +3,8 @@
 # (bench.py / tests load it with MOX_LIB=build/var_NAME/libmox.so, or
 # mox.Engine(lib_path=...)).
 # Usage: bash tools/build_variant.sh NAME "-DFLAG ..."
+# SRC=DIR builds DIR's sources instead of map-oxidize_amd/csrc (e.g. an older
+# commit's, exported with tools/export_src.sh).
 set -e
 NAME=$1; shift
 FLAGS="$*"
@@ -11,7 +13,7 @@ OUT=$ROOT/build/var_$NAME
 mkdir -p $OUT
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result"
 K="-mllvm -amdgpu-sched-strategy=max-memory-clause"
-C=$ROOT/map-oxidize_amd/csrc
+C=${SRC:-$ROOT/map-oxidize_amd/csrc}
 rm -f $OUT/*.o $OUT/libmox.so
 $H $K $FLAGS -c $C/mox_kernels.hip -o $OUT/k.o & P1=$!
 $H $FLAGS -c $C/mox_engine.hip -o $OUT/e.o & P2=$!
