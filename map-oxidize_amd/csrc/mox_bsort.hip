@@ -22,9 +22,13 @@
 // bytes every word shares).
 //
 // Ties after a level are words that share the window and both go on past it
-// (aux == 8 on both sides).  Their maximal runs are re-sorted on the next 7
-// bytes (level 1, 2, ...), with the run id as the most significant key so
-// runs stay where they are, until no run is left.
+// (aux == 8 on both sides).  A maximal run of at most 64 tied records (a long
+// word's punctuation variants, typically) is sorted in place by one thread
+// comparing the words' remaining bytes (k_bs_runs); longer runs are re-sorted
+// by the radix passes on the next 7 bytes (level 1, 2, ...), with the run id
+// as the most significant key so runs stay where they are, until no run is
+// left.  The sorted table's bytes leave through an LDS stage as aligned
+// 16-byte stores (k_bs_out2).
 #include <algorithm>
 #include <cstring>
 
@@ -40,8 +44,12 @@ static_assert(sizeof(BRec) == 16, "BRec is one 16-byte load");
 constexpr uint32_t WIN = 7;                      // window bytes per level
 constexpr uint32_t AUX_MORE = 8;                 // aux: the word continues past the window
 constexpr int OS_THREADS = 256;
-constexpr int OS_ITEMS = 16;                     // records per thread
-constexpr int OS_TILE = OS_THREADS * OS_ITEMS;   // 4,096 records per tile
+#ifndef MOX_OS_ITEMS
+#define MOX_OS_ITEMS 16
+#endif
+constexpr int OS_ITEMS = MOX_OS_ITEMS;           // records per thread
+constexpr int OS_TILE = OS_THREADS * OS_ITEMS;   // 4,096 records per tile (16 KiB stage per 1,024)
+constexpr int OS_WG_PER_CU = OS_ITEMS <= 8 ? 4 : 2;
 constexpr int OS_WAVES = OS_THREADS / 64;
 constexpr int OS_DIGITS = 12;                    // key bytes 0..7 (0 = aux), run bytes 0..3
 constexpr int SCAN_T = 1024, SCAN_PER = 8, SCAN_TILE = SCAN_T * SCAN_PER;
@@ -87,28 +95,37 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_init(const uint64_t* offs
   }
 }
 
-// Histograms of all OS_DIGITS digits over every record: gh[d * 256 + v].
-extern "C" __global__ __launch_bounds__(256) void k_bs_ghist(const BRec* in, uint64_t n, unsigned long long* gh) {
-  __shared__ uint32_t h[OS_DIGITS * 256];
-  for (int i = threadIdx.x; i < OS_DIGITS * 256; i += 256) h[i] = 0;
+// Histograms of digits 0 .. nd - 1 over every record: block b of the grid
+// (GH_BLOCKS blocks, one contiguous share of the records each) writes its row
+// ph[b][d * 256 + v]; k_bs_gscan sums the rows.  Per-wave LDS histograms (no
+// global atomics; a hot digit value contends within one wave only).
+constexpr int GH_BLOCKS = 256;
+extern "C" __global__ __launch_bounds__(256) void k_bs_ghist(const BRec* in, uint64_t n, int nd, uint32_t* ph) {
+  __shared__ uint32_t h[4][OS_DIGITS * 256];
+  const int t = threadIdx.x, wv = t >> 6;
+  for (int i = t; i < 4 * OS_DIGITS * 256; i += 256) (&h[0][0])[i] = 0;
   __syncthreads();
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x, lo = (uint64_t)blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  for (uint64_t i = lo + t; i < hi; i += 256) {
     const BRec r = in[i];
-#pragma unroll
-    for (int d = 0; d < OS_DIGITS; d++) atomicAdd(&h[d * 256 + digit_of(r, d)], 1u);
+    for (int d = 0; d < nd; d++) atomicAdd(&h[wv][d * 256 + digit_of(r, d)], 1u);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < OS_DIGITS * 256; i += 256)
-    if (h[i]) atomicAdd(&gh[i], (unsigned long long)h[i]);
+  for (int i = t; i < nd * 256; i += 256) ph[(uint64_t)blockIdx.x * OS_DIGITS * 256 + i] = h[0][i] + h[1][i] + h[2][i] + h[3][i];
 }
 
 // Exclusive scans of the global digit histograms: gs[d * 256 + v] = first
-// output position of digit value v in the pass over digit d.
-extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const unsigned long long* gh, uint64_t* gs) {
+// output position of digit value v in the pass over digit d; gh = the
+// histograms themselves (the host skips digits whose value is the same for
+// every record).
+extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const uint32_t* ph, int nd, unsigned long long* gh, uint64_t* gs) {
   __shared__ uint64_t ws[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   for (int d = 0; d < OS_DIGITS; d++) {
-    const uint64_t x = gh[d * 256 + t];
+    uint64_t x = 0;
+    if (d < nd)
+      for (int b = 0; b < GH_BLOCKS; b++) x += ph[(uint64_t)b * OS_DIGITS * 256 + d * 256 + t];
+    gh[d * 256 + t] = x;
     uint64_t inc = x;
     for (int o = 1; o < 64; o <<= 1) {
       const uint64_t y = __shfl_up(inc, o);
@@ -127,7 +144,7 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const unsigned long
 // blockIdx.x (tiles are dispatched in order, so every tile a look-back waits
 // on has been dispatched before it: the wait ends).  status[tile * 256 + v]
 // is zero at launch.
-extern "C" __global__ __launch_bounds__(OS_THREADS, 2) void k_os_pass(const BRec* __restrict__ in, BRec* __restrict__ out,
+extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass(const BRec* __restrict__ in, BRec* __restrict__ out,
                                                                        uint64_t n, int d, const uint64_t* __restrict__ gs,
                                                                        uint64_t* status, unsigned int* err) {
   __shared__ __attribute__((aligned(16))) BRec stage[OS_TILE];
@@ -296,6 +313,45 @@ extern "C" __global__ __launch_bounds__(SCAN_T) void k_scan_fin(uint64_t* a, uin
 __device__ __forceinline__ bool tied(const BRec& a, const BRec& b) {
   return (a.key & 0xFFu) == AUX_MORE && a.key == b.key && a.run == b.run;
 }
+// Is word ia < word ib (String Ord), given that their first `from` bytes are equal?
+__device__ bool word_less(const uint64_t* offs, const uint8_t* bytes, uint32_t ia, uint32_t ib, uint64_t from) {
+  const uint64_t oa = offs[ia], la = offs[ia + 1] - oa, ob = offs[ib], lb = offs[ib + 1] - ob, l = la < lb ? la : lb;
+  for (uint64_t k = from; k < l; k++) {
+    const uint8_t ca = bytes[oa + k], cb = bytes[ob + k];
+    if (ca != cb) return ca < cb;
+  }
+  return la < lb;
+}
+// After level `level`: every maximal run of tied records (k_bs_ties' flags
+// in / hd, taken before any record moves) of at most SMALL_RUN records is
+// sorted here, one thread per run, by the words' bytes after the compared
+// windows (insertion sort, in place), and marked resolved (aux AUX_DONE: no
+// longer tied).  Longer runs are counted (*big) and left tied for the next
+// level's radix pass.  Typical runs are a long word's punctuation variants: a
+// few records each.
+constexpr int SMALL_RUN = 64;
+constexpr uint32_t AUX_DONE = 9;
+extern "C" __global__ __launch_bounds__(256) void k_bs_runs(BRec* r, uint64_t n, const uint64_t* in, const uint64_t* hd,
+                                                            const uint64_t* offs, const uint8_t* bytes, uint32_t level,
+                                                            unsigned long long* big) {
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
+    if (!hd[j]) continue;  // not the head of a run
+    uint64_t e = j + 1;    // (a head has a tied successor)
+    while (e + 1 < n && e - j + 1 < (uint64_t)SMALL_RUN && in[e + 1] && !hd[e + 1]) e++;
+    if (e + 1 < n && in[e + 1] && !hd[e + 1]) {  // longer than SMALL_RUN: the next level
+      atomicAdd(big, 1ull);
+      continue;
+    }
+    const uint64_t from = (uint64_t)WIN * (level + 1);
+    for (uint64_t k = j + 1; k <= e; k++) {
+      const BRec x = r[k];
+      uint64_t q = k;
+      while (q > j && word_less(offs, bytes, x.idx, r[q - 1].idx, from)) { r[q] = r[q - 1]; q--; }
+      r[q] = x;
+    }
+    for (uint64_t k = j; k <= e; k++) r[k].key = (r[k].key & ~0xFFull) | AUX_DONE;
+  }
+}
 // in[j] = record j belongs to a run of >= 2 tied records; hd[j] = it starts one.
 extern "C" __global__ __launch_bounds__(256) void k_bs_ties(const BRec* r, uint64_t n, uint64_t* in, uint64_t* hd) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
@@ -337,12 +393,43 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_out1(const BRec* r, uint6
     olen[j] = offs[i + 1] - offs[i];
   }
 }
+// The words' bytes at their sorted offsets: block b writes the bytes of sorted
+// words [256 b, 256 b + 256), which are contiguous in the output.  They are
+// assembled in LDS (byte stores) from the 16-byte line below their first byte
+// and leave as aligned 16-byte stores; the partial first and last lines (shared
+// with the neighbouring blocks) byte by byte.  A block whose words exceed the
+// stage writes them byte by byte.
+constexpr int OUT_STAGE = 16384;
 extern "C" __global__ __launch_bounds__(256) void k_bs_out2(const BRec* r, uint64_t n, const uint64_t* offs, const uint8_t* bytes,
                                                              const uint64_t* ooffs, uint8_t* obytes) {
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t i = r[j].idx;
-    const uint64_t a = offs[i], len = offs[i + 1] - a, o = ooffs[j];
-    for (uint64_t k = 0; k < len; k++) obytes[o + k] = bytes[a + k];
+  __shared__ __attribute__((aligned(16))) uint8_t st[OUT_STAGE];
+  const int t = threadIdx.x;
+  for (uint64_t j0 = (uint64_t)blockIdx.x * 256; j0 < n; j0 += (uint64_t)gridDim.x * 256) {
+    const uint64_t j = j0 + t, jend = j0 + 256 < n ? j0 + 256 : n;
+    const uint64_t B0 = ooffs[j0], B1 = ooffs[jend], gbase = B0 & ~15ull;
+    uint64_t src = 0, len = 0, dst = 0;
+    if (j < n) {
+      const uint32_t i = r[j].idx;
+      src = offs[i];
+      len = offs[i + 1] - src;
+      dst = ooffs[j];
+    }
+    if (B1 - gbase <= (uint64_t)OUT_STAGE) {
+      for (uint64_t k = 0; k < len; k++) st[dst - gbase + k] = bytes[src + k];
+      __syncthreads();
+      const uint64_t a0 = (B0 + 15) & ~15ull, a1 = B1 & ~15ull;  // whole lines [a0, a1)
+      if (a0 < a1) {
+        for (uint64_t q = a0 + 16ull * t; q < a1; q += 16ull * 256)
+          *reinterpret_cast<uint4*>(obytes + q) = *reinterpret_cast<const uint4*>(st + (q - gbase));
+        if (t < 16 && B0 + t < a0) obytes[B0 + t] = st[B0 - gbase + t];
+        if (t >= 16 && t < 32 && a1 + (t - 16) < B1) obytes[a1 + (t - 16)] = st[a1 - gbase + (t - 16)];
+      } else if (t < 32 && B0 + t < B1) {
+        obytes[B0 + t] = st[B0 - gbase + t];
+      }
+      __syncthreads();  // the stage is rewritten by the next step
+    } else {
+      for (uint64_t k = 0; k < len; k++) obytes[dst + k] = bytes[src + k];
+    }
   }
 }
 
@@ -368,32 +455,34 @@ int scan_u64(mox_engine* e, uint64_t* a, uint64_t n, uint64_t* d_total, uint64_t
 
 struct BSort {
   BRec *a, *b;                // records, ping-pong
+  uint32_t* ph;               // GH_BLOCKS partial histogram rows
   unsigned long long* gh;     // OS_DIGITS x 256 global histograms (device)
   uint64_t* gs;               // ... their exclusive scans
-  uint64_t* status;           // look-back status words, 256 per tile
+  uint64_t* status;           // look-back status words: 256 per tile, one region per digit pass
   unsigned int* err;          // look-back timeout flag
   unsigned long long* h_gh;   // pinned host copy of gh
 };
 
-// LSD radix sort of s.a[0, n) by (run, key), one onesweep pass per digit that
-// is not the same for every record; the result ends in s.a.
-int radix_sort(mox_engine* e, BSort& s, uint64_t n) {
+// LSD radix sort of s.a[0, n) by its first nd digits (key bytes 0..7, then
+// run bytes), one onesweep pass per digit that is not the same for every
+// record; the result ends in s.a.  One host read (the histograms) per sort.
+int radix_sort(mox_engine* e, BSort& s, uint64_t n, int nd) {
   if (n < 2) return MOX_OK;
   hipStream_t st = e->stream;
-  HIPCHK(hipMemsetAsync(s.gh, 0, OS_DIGITS * 256 * 8, st));
-  hipLaunchKernelGGL(k_bs_ghist, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)s.a, n, s.gh);
-  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const unsigned long long*)s.gh, s.gs);
-  HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, OS_DIGITS * 256 * 8, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  hipLaunchKernelGGL(k_bs_ghist, dim3(GH_BLOCKS), dim3(256), 0, st, (const BRec*)s.a, n, nd, s.ph);
+  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const uint32_t*)s.ph, nd, s.gh, s.gs);
+  HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, (size_t)nd * 256 * 8, hipMemcpyDeviceToHost, st));
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   if (ntiles > 0x7FFFFFFFull) return fail(MOX_EINVAL, "bytewise sort: too many tiles");
-  for (int d = 0; d < OS_DIGITS; d++) {
+  // zero status words for every pass at once (a region per digit)
+  HIPCHK(hipMemsetAsync(s.status, 0, (size_t)nd * ntiles * 256 * 8, st));
+  HIPCHK(hipStreamSynchronize(st));
+  for (int d = 0; d < nd; d++) {
     bool uniform = false;
     for (int v = 0; v < 256; v++) uniform |= s.h_gh[d * 256 + v] == n;
     if (uniform) continue;  // every record has the same digit: the order stays
-    HIPCHK(hipMemsetAsync(s.status, 0, ntiles * 256 * 8, st));
     hipLaunchKernelGGL(k_os_pass, dim3((uint32_t)ntiles), dim3(OS_THREADS), 0, st, (const BRec*)s.a, s.b, n, d,
-                       (const uint64_t*)s.gs, s.status, s.err);
+                       (const uint64_t*)s.gs, s.status + (size_t)d * ntiles * 256, s.err);
     HIPCHK(hipGetLastError());
     std::swap(s.a, s.b);
   }
@@ -415,7 +504,7 @@ void bsort_free(mox_engine* e) {
 // The engine's result table (e->res) in bytewise order, on its GPU: the
 // sorted copy lives in s_counts / s_offs / s_bytes and becomes the result.
 // Scratch (s_tmp) is engine-owned and reused across calls: about 72 bytes per
-// word plus the look-back status (0.5 byte per word).
+// word plus the look-back status (6 bytes per word).
 int bsort_table(mox_engine* e) {
   HIPCHK(hipSetDevice(e->device));
   auto& r = e->res;
@@ -424,9 +513,10 @@ int bsort_table(mox_engine* e) {
   if (n >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: %llu words (at most 2^32 - 1)", (unsigned long long)n);
   hipStream_t st = e->stream;
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
-  // scratch: records A, B, subset S | flags, heads, positions | status | gh, gs | scan sums | totals, err
-  const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
-  const uint64_t need = 3 * rec + 3 * u64n + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
+  // scratch: records A, B, subset S | flags, heads, positions | status | partial rows, gh, gs | scan sums | totals, err
+  const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
+  const uint64_t phb = 4ull * GH_BLOCKS * OS_DIGITS * 256;
+  const uint64_t need = 3 * rec + 3 * u64n + stb + phb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
   int rc;
   if ((rc = grow_dev(e->s_tmp, need)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
       (rc = grow_dev(e->s_bytes, nb + 64)))
@@ -441,10 +531,11 @@ int bsort_table(mox_engine* e) {
   uint64_t* pos = (uint64_t*)q; q += u64n;
   BSort s;
   s.status = (uint64_t*)q; q += stb;
+  s.ph = (uint32_t*)q; q += phb;
   s.gh = (unsigned long long*)q; q += OS_DIGITS * 256 * 8;
   s.gs = (uint64_t*)q; q += OS_DIGITS * 256 * 8;
   uint64_t* ssum = (uint64_t*)q; q += sums;
-  uint64_t* total = (uint64_t*)q; q += 64;
+  uint64_t* total = (uint64_t*)q; q += 64;  // [0] subset size [1] runs [2] big runs
   s.err = (unsigned int*)q;
   s.h_gh = e->h_bsort;
   uint64_t* h_tot = (uint64_t*)(e->h_bsort + OS_DIGITS * 256);
@@ -453,26 +544,37 @@ int bsort_table(mox_engine* e) {
   hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, n, A);
   s.a = A;
   s.b = B;
-  if ((rc = radix_sort(e, s, n))) return rc;
+  if ((rc = radix_sort(e, s, n, 8))) return rc;
   BRec* R = s.a;                 // sorted (A or B)
   BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner
-  // levels 1, 2, ...: runs of words sharing all compared bytes
+  // after each level: short tie runs sorted in place by direct byte compares
+  // (k_bs_runs); runs longer than SMALL_RUN re-sorted on the next window
   uint32_t run_base = 1;
-  for (uint32_t level = 1;; level++) {
+  for (uint32_t level = 0;; level++) {
+    hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin, fhd);
+    HIPCHK(hipMemsetAsync(total + 2, 0, 8, st));
+    hipLaunchKernelGGL(k_bs_runs, dim3(grid_for(n)), dim3(256), 0, st, R, n, (const uint64_t*)fin, (const uint64_t*)fhd, r.offs,
+                       r.bytes, level, (unsigned long long*)(total + 2));
+    HIPCHK(hipMemcpyAsync(h_tot + 2, total + 2, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_tot + 3, s.err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    if ((uint32_t)h_tot[3]) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
+    if (h_tot[2] == 0) break;  // no run longer than SMALL_RUN is left
+    // the long runs (still tied) -> subset, re-sorted on window level + 1
     hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin, fhd);
     if ((rc = scan_u64(e, fin, n, total, ssum)) || (rc = scan_u64(e, fhd, n, total + 1, ssum))) return rc;
     HIPCHK(hipMemcpyAsync(h_tot, total, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if ((uint32_t)h_tot[2]) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
     const uint64_t m = h_tot[0], runs = h_tot[1];
     if (m == 0) break;
     if ((uint64_t)run_base + runs >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
     hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin,
-                       (const uint64_t*)fhd, m, run_base, r.offs, r.bytes, level, S, pos);
+                       (const uint64_t*)fhd, m, run_base, r.offs, r.bytes, level + 1, S, pos);
     s.a = S;
     s.b = S2;
-    if ((rc = radix_sort(e, s, m))) return rc;
+    const uint64_t top = (uint64_t)run_base + runs;  // run ids < top: bytes of run id to sort on
+    const int nrb = top < (1ull << 8) ? 1 : top < (1ull << 16) ? 2 : top < (1ull << 24) ? 3 : 4;
+    if ((rc = radix_sort(e, s, m, 8 + nrb))) return rc;
     hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)s.a, m, (const uint64_t*)pos, R);
     HIPCHK(hipGetLastError());
     run_base += (uint32_t)runs;

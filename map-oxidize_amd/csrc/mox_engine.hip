@@ -372,11 +372,21 @@ int pipeline_once(mox_engine* e, const Corpus& c) {
   return finish_pass(e, q);
 }
 
+// Region capacity that covers the largest region an attempt asked for
+// (cold_need), bounded by 4x the mean tokens per region: every region is sized
+// alike, so one skewed region (a hot word without a dictionary) would size all
+// 262 K of them; beyond the bound its records spill (spill_cap grows instead).
+uint64_t cold_cap_for(const mox_engine* e, const Ctl& h) {
+  const uint64_t want = h.cold_need + h.cold_need / 8 + 16;
+  const uint64_t bound = 4 * h.tokens / ((uint64_t)e->w.map_grid * NB) + 64;
+  return std::min(want, std::max<uint64_t>(bound, e->w.cold_cap));
+}
+
 // Capacities that cover what an overflowed attempt asked for.
 Caps grow_for(mox_engine* e, const Ctl& h) {
   Caps need = caps_of(e->w);
   if (h.overflow & OVF_POOL) {
-    need.cold_cap = std::max<uint64_t>(need.cold_cap, h.cold_need + h.cold_need / 8 + 16);
+    need.cold_cap = std::max<uint64_t>(need.cold_cap, cold_cap_for(e, h));
     need.spill_cap = std::max<uint64_t>(need.spill_cap, h.spill_need + h.spill_need / 4 + 1024);
   }
   if (h.overflow & OVF_W) {
@@ -550,7 +560,7 @@ void commit_result(mox_engine* e, const Corpus& c, const Ctl& h) {
   // spills are correct but slow (atomic scatter): size the regions for the
   // next run of this engine from what this one needed
   // (applied at the start of the next run: the buffers hold this run's table)
-  if (h.spill_need) e->next_cold_cap = std::max<uint64_t>(e->next_cold_cap, h.cold_need + h.cold_need / 8 + 16);
+  if (h.spill_need) e->next_cold_cap = std::max<uint64_t>(e->next_cold_cap, cold_cap_for(e, h));
   e->stats.bytes = c.own_hi - c.own_lo;
   e->stats.tokens = h.tokens;
   e->stats.uniques = h.n_total;

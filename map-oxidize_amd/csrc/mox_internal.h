@@ -67,7 +67,8 @@ constexpr int SUB_BITS_MAX = 12;
 constexpr int SUB_N = 1 << SUB_BITS_MAX;
 constexpr int U_MAX = NB * SUB_N;           // reduce units
 constexpr int SUB_PER_T = SUB_N / 1024;     // sub-buckets per thread in the 1024-thread unit kernels
-constexpr uint32_t SPLIT_MIN = 6144;        // records below which a partition is never split
+constexpr uint32_t SPLIT_MIN = 2048;        // records below which a partition is never split (= k_reduce's RED_CAP: at most
+                                            // that many distinct keys, one table pass)
 constexpr uint32_t SPLIT_TARGET = 320;      // records per sub-bucket aimed at
 constexpr uint32_t SMALL_CAP = 512;         // sub-buckets up to this many records: k_reduce_small
 #ifndef MOX_SPLIT_PER_REGION

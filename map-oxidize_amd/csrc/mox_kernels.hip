@@ -1773,11 +1773,14 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   uint32_t b = red_bucket(h);
   if (s.dbg) atomicAdd(&s.dbg[0], 1u);
   const uint32_t* tags = reinterpret_cast<const uint32_t*>(s.tag4);
-  uint32_t it = 0, eqtag = 0;
+  uint32_t it = 0, probes = 0, eqtag = 0;
   bool done = false;
   // wave-level loop (see long_insert): a lane that claims a slot stores the key
   // and publishes its count inside the iteration, never past the loop exit
   do {
+    // a table past RED_CAP keys is redone in sub-passes anyway: stop at once
+    // (a lane probing a full table would otherwise walk every bucket)
+    if (!done && __hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) done = true;
     if (!done) {
       const uint4 t = s.tag4[b];
       const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
@@ -1816,9 +1819,12 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
             }  // lost the slot: re-read this bucket
           } else {
             b = b + 1 == RED_BK ? 0 : b + 1;
+            ++probes;
           }
         }
-        if (!done && ++it >= 64u * RED_BK) {
+        // every bucket seen full, or (never expected) a publication that does
+        // not land: the table overflows, the unit is redone in sub-passes
+        if (!done && (probes >= (uint32_t)RED_BK || ++it >= 64u * RED_BK)) {
           s.misc[1] = 1;
           done = true;
         }
