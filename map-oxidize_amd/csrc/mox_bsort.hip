@@ -22,13 +22,12 @@
 // bytes every word shares).
 //
 // Ties after a level are words that share the window and both go on past it
-// (aux == 8 on both sides).  A maximal run of at most 64 tied records (a long
-// word's punctuation variants, typically) is sorted in place by one thread
-// comparing the words' remaining bytes (k_bs_runs); longer runs are re-sorted
-// by the radix passes on the next 7 bytes (level 1, 2, ...), with the run id
-// as the most significant key so runs stay where they are, until no run is
-// left.  The sorted table's bytes leave through an LDS stage as aligned
-// 16-byte stores (k_bs_out2).
+// (aux == 8 on both sides).  Their maximal runs are re-sorted by the radix
+// passes on the next 7 bytes (level 1, 2, ...), with the run id as the most
+// significant key so runs stay where they are, until no run is left.  (Sorting
+// short runs in place by one thread each was tried and lost: its dependent
+// byte loads made it the slowest kernel of the sort.)  The sorted table's
+// bytes leave through an LDS stage as aligned 16-byte stores (k_bs_out2).
 #include <algorithm>
 #include <cstring>
 
@@ -85,22 +84,32 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 }  // namespace
 
-extern "C" __global__ __launch_bounds__(256) void k_bs_init(const uint64_t* offs, const uint8_t* bytes, uint64_t n, BRec* out) {
+// Word i's count, byte offset and length, gathered once by the output kernels
+// through the sorted records' idx (one 16-byte read instead of three 8-byte
+// ones; table bytes < 4 GiB).
+struct BPay {
+  uint64_t count;
+  uint32_t off, len;
+};
+extern "C" __global__ __launch_bounds__(256) void k_bs_init(const uint64_t* offs, const uint8_t* bytes, const uint64_t* counts,
+                                                            uint64_t n, BRec* out, BPay* pay) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     BRec r;
     r.key = window(offs, bytes, i, 0);
     r.run = 0;
     r.idx = (uint32_t)i;
     out[i] = r;
+    const uint64_t o = offs[i];
+    pay[i] = BPay{counts[i], (uint32_t)o, (uint32_t)(offs[i + 1] - o)};
   }
 }
 
-// Histograms of digits 0 .. nd - 1 over every record: block b of the grid
-// (GH_BLOCKS blocks, one contiguous share of the records each) writes its row
-// ph[b][d * 256 + v]; k_bs_gscan sums the rows.  Per-wave LDS histograms (no
-// global atomics; a hot digit value contends within one wave only).
+// Histograms of digits 0 .. nd - 1 over every record: GH_BLOCKS blocks, one
+// contiguous share of the records each, per-wave LDS histograms (a hot digit
+// value contends within one wave only), then one global add per non-zero bin
+// and block into gh (zeroed before).
 constexpr int GH_BLOCKS = 256;
-extern "C" __global__ __launch_bounds__(256) void k_bs_ghist(const BRec* in, uint64_t n, int nd, uint32_t* ph) {
+extern "C" __global__ __launch_bounds__(256) void k_bs_ghist(const BRec* in, uint64_t n, int nd, unsigned long long* gh) {
   __shared__ uint32_t h[4][OS_DIGITS * 256];
   const int t = threadIdx.x, wv = t >> 6;
   for (int i = t; i < 4 * OS_DIGITS * 256; i += 256) (&h[0][0])[i] = 0;
@@ -111,21 +120,20 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_ghist(const BRec* in, uin
     for (int d = 0; d < nd; d++) atomicAdd(&h[wv][d * 256 + digit_of(r, d)], 1u);
   }
   __syncthreads();
-  for (int i = t; i < nd * 256; i += 256) ph[(uint64_t)blockIdx.x * OS_DIGITS * 256 + i] = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+  for (int i = t; i < nd * 256; i += 256) {
+    const uint32_t x = h[0][i] + h[1][i] + h[2][i] + h[3][i];
+    if (x) atomicAdd(&gh[i], (unsigned long long)x);
+  }
 }
 
 // Exclusive scans of the global digit histograms: gs[d * 256 + v] = first
-// output position of digit value v in the pass over digit d; gh = the
-// histograms themselves (the host skips digits whose value is the same for
-// every record).
-extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const uint32_t* ph, int nd, unsigned long long* gh, uint64_t* gs) {
+// output position of digit value v in the pass over digit d (the host skips
+// digits whose value is the same for every record).
+extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const unsigned long long* gh, int nd, uint64_t* gs) {
   __shared__ uint64_t ws[4];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  for (int d = 0; d < OS_DIGITS; d++) {
-    uint64_t x = 0;
-    if (d < nd)
-      for (int b = 0; b < GH_BLOCKS; b++) x += ph[(uint64_t)b * OS_DIGITS * 256 + d * 256 + t];
-    gh[d * 256 + t] = x;
+  for (int d = 0; d < nd; d++) {
+    const uint64_t x = gh[d * 256 + t];
     uint64_t inc = x;
     for (int o = 1; o < 64; o <<= 1) {
       const uint64_t y = __shfl_up(inc, o);
@@ -313,71 +321,69 @@ extern "C" __global__ __launch_bounds__(SCAN_T) void k_scan_fin(uint64_t* a, uin
 __device__ __forceinline__ bool tied(const BRec& a, const BRec& b) {
   return (a.key & 0xFFu) == AUX_MORE && a.key == b.key && a.run == b.run;
 }
-// Is word ia < word ib (String Ord), given that their first `from` bytes are equal?
-__device__ bool word_less(const uint64_t* offs, const uint8_t* bytes, uint32_t ia, uint32_t ib, uint64_t from) {
-  const uint64_t oa = offs[ia], la = offs[ia + 1] - oa, ob = offs[ib], lb = offs[ib + 1] - ob, l = la < lb ? la : lb;
-  for (uint64_t k = from; k < l; k++) {
-    const uint8_t ca = bytes[oa + k], cb = bytes[ob + k];
-    if (ca != cb) return ca < cb;
-  }
-  return la < lb;
-}
-// After level `level`: every maximal run of tied records (k_bs_ties' flags
-// in / hd, taken before any record moves) of at most SMALL_RUN records is
-// sorted here, one thread per run, by the words' bytes after the compared
-// windows (insertion sort, in place), and marked resolved (aux AUX_DONE: no
-// longer tied).  Longer runs are counted (*big) and left tied for the next
-// level's radix pass.  Typical runs are a long word's punctuation variants: a
-// few records each.
-constexpr int SMALL_RUN = 64;
-constexpr uint32_t AUX_DONE = 9;
-extern "C" __global__ __launch_bounds__(256) void k_bs_runs(BRec* r, uint64_t n, const uint64_t* in, const uint64_t* hd,
-                                                            const uint64_t* offs, const uint8_t* bytes, uint32_t level,
-                                                            unsigned long long* big) {
-  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    if (!hd[j]) continue;  // not the head of a run
-    uint64_t e = j + 1;    // (a head has a tied successor)
-    while (e + 1 < n && e - j + 1 < (uint64_t)SMALL_RUN && in[e + 1] && !hd[e + 1]) e++;
-    if (e + 1 < n && in[e + 1] && !hd[e + 1]) {  // longer than SMALL_RUN: the next level
-      atomicAdd(big, 1ull);
-      continue;
-    }
-    const uint64_t from = (uint64_t)WIN * (level + 1);
-    for (uint64_t k = j + 1; k <= e; k++) {
-      const BRec x = r[k];
-      uint64_t q = k;
-      while (q > j && word_less(offs, bytes, x.idx, r[q - 1].idx, from)) { r[q] = r[q - 1]; q--; }
-      r[q] = x;
-    }
-    for (uint64_t k = j; k <= e; k++) r[k].key = (r[k].key & ~0xFFull) | AUX_DONE;
-  }
-}
-// in[j] = record j belongs to a run of >= 2 tied records; hd[j] = it starts one.
-extern "C" __global__ __launch_bounds__(256) void k_bs_ties(const BRec* r, uint64_t n, uint64_t* in, uint64_t* hd) {
+// fl[j] = in | hd << 32: in = record j belongs to a run of >= 2 tied records,
+// hd = it starts one (one exclusive scan then gives both the subset index and
+// the heads before it: in <= 1 per record, so the low half never carries).
+extern "C" __global__ __launch_bounds__(256) void k_bs_ties(const BRec* r, uint64_t n, uint64_t* fl) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
     const BRec b = r[j];
     const bool tp = j > 0 && tied(r[j - 1], b), tn = j + 1 < n && tied(b, r[j + 1]);
-    in[j] = (tp || tn) ? 1 : 0;
-    hd[j] = (!tp && tn) ? 1 : 0;
+    fl[j] = ((tp || tn) ? 1ull : 0ull) | ((!tp && tn) ? (1ull << 32) : 0ull);
   }
 }
-// After the exclusive scans of in (cpos) and hd (hx): every record in a run
-// goes to the subset at its compact index with its next window and the run id
-// base + (heads up to and including its run's), and its sorted position.
-extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r, uint64_t n, const uint64_t* cpos, const uint64_t* hx,
-                                                                   uint64_t m, uint32_t run_base, const uint64_t* offs,
-                                                                   const uint8_t* bytes, uint32_t level, BRec* sub, uint64_t* pos) {
+// After the exclusive scan of fl: every record in a run goes to the subset at
+// its compact index with its next window and the run id base + (heads up to
+// and including its run's), and its sorted position.  The subset is in sorted
+// position order, so each run is a contiguous segment of it.
+extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r, uint64_t n, const uint64_t* fx, uint64_t m,
+                                                                   uint32_t run_base, const uint64_t* offs, const uint8_t* bytes,
+                                                                   uint32_t level, BRec* sub, uint64_t* pos) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t c = cpos[j], c1 = j + 1 < n ? cpos[j + 1] : m;
+    const uint64_t f = fx[j], c = f & 0xFFFFFFFFull, c1 = j + 1 < n ? (fx[j + 1] & 0xFFFFFFFFull) : m;
     if (c1 == c) continue;  // not in a run
     const BRec b = r[j];
     const bool head = !(j > 0 && tied(r[j - 1], b));
     BRec o;
     o.key = window(offs, bytes, b.idx, level);
     o.idx = b.idx;
-    o.run = run_base + (uint32_t)(hx[j] + (head ? 1 : 0));
+    o.run = run_base + (uint32_t)((f >> 32) + (head ? 1 : 0));
     sub[c] = o;
     pos[c] = j;
+  }
+}
+// The subset's runs sorted by key, each by one thread in LDS (insertion sort):
+// a workgroup loads SEG_CH subset records (plus SEG_MAX after them) and sorts
+// the runs whose head lies in its SEG_CH; a run longer than SEG_MAX sets
+// *longrun, and the host then radix-sorts the whole subset instead.  Typical
+// runs are a long word's punctuation variants: a few records each.
+constexpr int SEG_CH = 2048, SEG_MAX = 64;
+extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, uint64_t m, unsigned int* longrun) {
+  __shared__ BRec ls[SEG_CH + SEG_MAX];
+  const int t = threadIdx.x;
+  for (uint64_t c0 = (uint64_t)blockIdx.x * SEG_CH; c0 < m; c0 += (uint64_t)gridDim.x * SEG_CH) {
+    const uint32_t nl = (uint32_t)(m - c0 < (uint64_t)(SEG_CH + SEG_MAX) ? m - c0 : (uint64_t)(SEG_CH + SEG_MAX));
+    for (uint32_t i = t; i < nl; i += 256) ls[i] = S[c0 + i];
+    const uint32_t prev_run = c0 > 0 ? S[c0 - 1].run : 0xFFFFFFFFu;
+    __syncthreads();
+    const uint32_t nh = nl < (uint32_t)SEG_CH ? nl : (uint32_t)SEG_CH;
+    for (uint32_t p = t; p < nh; p += 256) {
+      const uint32_t run = ls[p].run;
+      if ((p == 0 ? prev_run : ls[p - 1].run) == run) continue;  // not a run head
+      uint32_t e = p;
+      while (e + 1 < nl && ls[e + 1].run == run) e++;
+      if (e - p + 1 > (uint32_t)SEG_MAX || (e + 1 == nl && c0 + nl < m && S[c0 + nl].run == run)) {
+        atomicOr(longrun, 1u);
+        continue;
+      }
+      for (uint32_t k = p + 1; k <= e; k++) {
+        const BRec x = ls[k];
+        uint32_t q = k;
+        while (q > p && ls[q - 1].key > x.key) { ls[q] = ls[q - 1]; q--; }
+        ls[q] = x;
+      }
+      for (uint32_t k = p; k <= e; k++) S[c0 + k] = ls[k];
+    }
+    __syncthreads();  // ls is reloaded for the next chunk
   }
 }
 extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub, uint64_t m, const uint64_t* pos, BRec* r) {
@@ -385,37 +391,66 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub,
 }
 // Output table in sorted order: counts and lengths, then (after the length
 // scan) the bytes.
-extern "C" __global__ __launch_bounds__(256) void k_bs_out1(const BRec* r, uint64_t n, const uint64_t* counts, const uint64_t* offs,
-                                                             uint64_t* ocounts, uint64_t* olen) {
+extern "C" __global__ __launch_bounds__(256) void k_bs_out1(const BRec* r, uint64_t n, const BPay* pay, uint64_t* ocounts,
+                                                             uint64_t* olen) {
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t i = r[j].idx;
-    ocounts[j] = counts[i];
-    olen[j] = offs[i + 1] - offs[i];
+    const BPay p = pay[r[j].idx];
+    ocounts[j] = p.count;
+    olen[j] = p.len;
   }
 }
 // The words' bytes at their sorted offsets: block b writes the bytes of sorted
 // words [256 b, 256 b + 256), which are contiguous in the output.  They are
-// assembled in LDS (byte stores) from the 16-byte line below their first byte
-// and leave as aligned 16-byte stores; the partial first and last lines (shared
-// with the neighbouring blocks) byte by byte.  A block whose words exceed the
-// stage writes them byte by byte.
+// assembled in LDS from the 16-byte line below their first byte and leave as
+// aligned 16-byte stores; the partial first and last lines (shared with the
+// neighbouring blocks) byte by byte.  A word of at most 7 bytes that never
+// entered a tie run (run 0) takes its bytes from its level-0 key; longer ones
+// from the table with dword loads.  A block whose words exceed the stage
+// writes them byte by byte.
 constexpr int OUT_STAGE = 16384;
-extern "C" __global__ __launch_bounds__(256) void k_bs_out2(const BRec* r, uint64_t n, const uint64_t* offs, const uint8_t* bytes,
+extern "C" __global__ __launch_bounds__(256) void k_bs_out2(const BRec* r, uint64_t n, const BPay* pay, const uint8_t* bytes,
                                                              const uint64_t* ooffs, uint8_t* obytes) {
   __shared__ __attribute__((aligned(16))) uint8_t st[OUT_STAGE];
   const int t = threadIdx.x;
   for (uint64_t j0 = (uint64_t)blockIdx.x * 256; j0 < n; j0 += (uint64_t)gridDim.x * 256) {
     const uint64_t j = j0 + t, jend = j0 + 256 < n ? j0 + 256 : n;
     const uint64_t B0 = ooffs[j0], B1 = ooffs[jend], gbase = B0 & ~15ull;
+    BRec rec{};
     uint64_t src = 0, len = 0, dst = 0;
+    bool inkey = false;
     if (j < n) {
-      const uint32_t i = r[j].idx;
-      src = offs[i];
-      len = offs[i + 1] - src;
+      rec = r[j];
       dst = ooffs[j];
+      const uint32_t aux = (uint32_t)(rec.key & 0xFFu);
+      inkey = rec.run == 0 && aux < AUX_MORE;  // the level-0 key holds the whole word
+      if (inkey) {
+        len = aux;
+      } else {
+        const BPay p = pay[rec.idx];
+        src = p.off;
+        len = p.len;
+      }
     }
     if (B1 - gbase <= (uint64_t)OUT_STAGE) {
-      for (uint64_t k = 0; k < len; k++) st[dst - gbase + k] = bytes[src + k];
+      uint8_t* o = st + (dst - gbase);
+      if (inkey) {
+        for (uint32_t k = 0; k < (uint32_t)len; k++) o[k] = (uint8_t)(rec.key >> (56 - 8 * k));
+      } else if (len) {
+        const uint32_t* w4 = reinterpret_cast<const uint32_t*>(bytes + (src & ~3ull));
+        const uint32_t sh = (uint32_t)(src & 3u), nd = (sh + (uint32_t)len + 3) >> 2;
+        for (uint32_t q = 0; q < nd; q += 4) {  // four dword loads in flight at a time
+          uint32_t v[4];
+#pragma unroll
+          for (int u = 0; u < 4; u++) v[u] = q + u < nd ? w4[q + u] : 0u;
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) {
+              const int64_t k = (int64_t)(4 * (q + u) + bb) - (int64_t)sh;
+              if (k >= 0 && (uint64_t)k < len) o[k] = (uint8_t)(v[u] >> (8 * bb));
+            }
+        }
+      }
       __syncthreads();
       const uint64_t a0 = (B0 + 15) & ~15ull, a1 = B1 & ~15ull;  // whole lines [a0, a1)
       if (a0 < a1) {
@@ -427,6 +462,8 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_out2(const BRec* r, uint6
         obytes[B0 + t] = st[B0 - gbase + t];
       }
       __syncthreads();  // the stage is rewritten by the next step
+    } else if (inkey) {
+      for (uint32_t k = 0; k < (uint32_t)len; k++) obytes[dst + k] = (uint8_t)(rec.key >> (56 - 8 * k));
     } else {
       for (uint64_t k = 0; k < len; k++) obytes[dst + k] = bytes[src + k];
     }
@@ -455,7 +492,6 @@ int scan_u64(mox_engine* e, uint64_t* a, uint64_t n, uint64_t* d_total, uint64_t
 
 struct BSort {
   BRec *a, *b;                // records, ping-pong
-  uint32_t* ph;               // GH_BLOCKS partial histogram rows
   unsigned long long* gh;     // OS_DIGITS x 256 global histograms (device)
   uint64_t* gs;               // ... their exclusive scans
   uint64_t* status;           // look-back status words: 256 per tile, one region per digit pass
@@ -469,8 +505,9 @@ struct BSort {
 int radix_sort(mox_engine* e, BSort& s, uint64_t n, int nd) {
   if (n < 2) return MOX_OK;
   hipStream_t st = e->stream;
-  hipLaunchKernelGGL(k_bs_ghist, dim3(GH_BLOCKS), dim3(256), 0, st, (const BRec*)s.a, n, nd, s.ph);
-  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const uint32_t*)s.ph, nd, s.gh, s.gs);
+  HIPCHK(hipMemsetAsync(s.gh, 0, (size_t)nd * 256 * 8, st));
+  hipLaunchKernelGGL(k_bs_ghist, dim3(GH_BLOCKS), dim3(256), 0, st, (const BRec*)s.a, n, nd, s.gh);
+  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const unsigned long long*)s.gh, nd, s.gs);
   HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, (size_t)nd * 256 * 8, hipMemcpyDeviceToHost, st));
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   if (ntiles > 0x7FFFFFFFull) return fail(MOX_EINVAL, "bytewise sort: too many tiles");
@@ -503,7 +540,7 @@ void bsort_free(mox_engine* e) {
 
 // The engine's result table (e->res) in bytewise order, on its GPU: the
 // sorted copy lives in s_counts / s_offs / s_bytes and becomes the result.
-// Scratch (s_tmp) is engine-owned and reused across calls: about 72 bytes per
+// Scratch (s_tmp) is engine-owned and reused across calls: about 88 bytes per
 // word plus the look-back status (6 bytes per word).
 int bsort_table(mox_engine* e) {
   HIPCHK(hipSetDevice(e->device));
@@ -511,12 +548,13 @@ int bsort_table(mox_engine* e) {
   const uint64_t n = r.n, nb = r.nb;
   if (n < 2) return MOX_OK;
   if (n >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: %llu words (at most 2^32 - 1)", (unsigned long long)n);
+  // (32-bit word offsets in the payload: a bigger table is sorted on the host, as on MOX_ENOMEM)
+  if (nb >= (1ull << 32)) return fail(MOX_ENOMEM, "bytewise sort: %llu table bytes (device sort: < 4 GiB)", (unsigned long long)nb);
   hipStream_t st = e->stream;
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
-  // scratch: records A, B, subset S | flags, heads, positions | status | partial rows, gh, gs | scan sums | totals, err
+  // scratch: records A, B, subset S, payload | run flags, positions | status | gh, gs | scan sums | totals, err
   const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
-  const uint64_t phb = 4ull * GH_BLOCKS * OS_DIGITS * 256;
-  const uint64_t need = 3 * rec + 3 * u64n + stb + phb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
+  const uint64_t need = 4 * rec + 2 * u64n + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
   int rc;
   if ((rc = grow_dev(e->s_tmp, need)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
       (rc = grow_dev(e->s_bytes, nb + 64)))
@@ -526,66 +564,68 @@ int bsort_table(mox_engine* e) {
   BRec* A = (BRec*)q; q += rec;
   BRec* B = (BRec*)q; q += rec;
   BRec* S = (BRec*)q; q += rec;
+  BPay* pay = (BPay*)q; q += rec;
   uint64_t* fin = (uint64_t*)q; q += u64n;
-  uint64_t* fhd = (uint64_t*)q; q += u64n;
   uint64_t* pos = (uint64_t*)q; q += u64n;
   BSort s;
   s.status = (uint64_t*)q; q += stb;
-  s.ph = (uint32_t*)q; q += phb;
   s.gh = (unsigned long long*)q; q += OS_DIGITS * 256 * 8;
   s.gs = (uint64_t*)q; q += OS_DIGITS * 256 * 8;
   uint64_t* ssum = (uint64_t*)q; q += sums;
-  uint64_t* total = (uint64_t*)q; q += 64;  // [0] subset size [1] runs [2] big runs
+  uint64_t* total = (uint64_t*)q; q += 64;  // [0] subset size [1] runs
   s.err = (unsigned int*)q;
   s.h_gh = e->h_bsort;
   uint64_t* h_tot = (uint64_t*)(e->h_bsort + OS_DIGITS * 256);
-  HIPCHK(hipMemsetAsync(s.err, 0, 4, st));
+  HIPCHK(hipMemsetAsync(s.err, 0, 8, st));  // [0] look-back timeout [1] long run (k_bs_segsort)
   // level 0: every word by its first 7 bytes and length class
-  hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, n, A);
+  hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, r.counts, n, A, pay);
   s.a = A;
   s.b = B;
   if ((rc = radix_sort(e, s, n, 8))) return rc;
   BRec* R = s.a;                 // sorted (A or B)
   BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner
-  // after each level: short tie runs sorted in place by direct byte compares
-  // (k_bs_runs); runs longer than SMALL_RUN re-sorted on the next window
+  // levels 1, 2, ...: runs of words sharing every compared byte, re-sorted on
+  // the next window (by run: short runs in LDS by k_bs_segsort; a subset with
+  // a longer run by the radix passes, run id as the most significant digits)
   uint32_t run_base = 1;
-  for (uint32_t level = 0;; level++) {
-    hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin, fhd);
-    HIPCHK(hipMemsetAsync(total + 2, 0, 8, st));
-    hipLaunchKernelGGL(k_bs_runs, dim3(grid_for(n)), dim3(256), 0, st, R, n, (const uint64_t*)fin, (const uint64_t*)fhd, r.offs,
-                       r.bytes, level, (unsigned long long*)(total + 2));
-    HIPCHK(hipMemcpyAsync(h_tot + 2, total + 2, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(h_tot + 3, s.err, 4, hipMemcpyDeviceToHost, st));
+  unsigned int* longrun = s.err + 1;
+  for (uint32_t level = 1;; level++) {
+    hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin);
+    if ((rc = scan_u64(e, fin, n, total, ssum))) return rc;
+    HIPCHK(hipMemcpyAsync(h_tot, total, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
-    if ((uint32_t)h_tot[3]) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
-    if (h_tot[2] == 0) break;  // no run longer than SMALL_RUN is left
-    // the long runs (still tied) -> subset, re-sorted on window level + 1
-    hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin, fhd);
-    if ((rc = scan_u64(e, fin, n, total, ssum)) || (rc = scan_u64(e, fhd, n, total + 1, ssum))) return rc;
-    HIPCHK(hipMemcpyAsync(h_tot, total, 16, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    const uint64_t m = h_tot[0], runs = h_tot[1];
+    if ((uint32_t)h_tot[2]) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
+    const uint64_t m = h_tot[0] & 0xFFFFFFFFull, runs = h_tot[0] >> 32;
     if (m == 0) break;
     if ((uint64_t)run_base + runs >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
-    hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin,
-                       (const uint64_t*)fhd, m, run_base, r.offs, r.bytes, level + 1, S, pos);
-    s.a = S;
-    s.b = S2;
-    const uint64_t top = (uint64_t)run_base + runs;  // run ids < top: bytes of run id to sort on
-    const int nrb = top < (1ull << 8) ? 1 : top < (1ull << 16) ? 2 : top < (1ull << 24) ? 3 : 4;
-    if ((rc = radix_sort(e, s, m, 8 + nrb))) return rc;
-    hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)s.a, m, (const uint64_t*)pos, R);
+    hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin, m,
+                       run_base, r.offs, r.bytes, level, S, pos);
+    HIPCHK(hipMemsetAsync(longrun, 0, 4, st));
+    hipLaunchKernelGGL(k_bs_segsort, dim3((uint32_t)std::min<uint64_t>(4096, (m + SEG_CH - 1) / SEG_CH)), dim3(256), 0, st, S, m,
+                       longrun);
+    HIPCHK(hipMemcpyAsync(h_tot + 3, longrun, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    BRec* sorted = S;
+    if ((uint32_t)h_tot[3]) {  // a run longer than SEG_MAX: the radix passes over the whole subset
+      s.a = S;
+      s.b = S2;
+      const uint64_t top = (uint64_t)run_base + runs;  // run ids < top: bytes of run id to sort on
+      const int nrb = top < (1ull << 8) ? 1 : top < (1ull << 16) ? 2 : top < (1ull << 24) ? 3 : 4;
+      if ((rc = radix_sort(e, s, m, 8 + nrb))) return rc;
+      sorted = s.a;
+    }
+    hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)sorted, m, (const uint64_t*)pos, R);
     HIPCHK(hipGetLastError());
     run_base += (uint32_t)runs;
   }
   // the sorted table: counts and lengths, offsets by a scan, bytes
   uint64_t* oc = (uint64_t*)e->s_counts.p;
   uint64_t* oo = (uint64_t*)e->s_offs.p;
-  hipLaunchKernelGGL(k_bs_out1, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, r.counts, r.offs, oc, oo);
+  hipLaunchKernelGGL(k_bs_out1, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, oc, oo);
   if ((rc = scan_u64(e, oo, n, oo + n, ssum))) return rc;
-  hipLaunchKernelGGL(k_bs_out2, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, r.offs, r.bytes, (const uint64_t*)oo,
-                     (uint8_t*)e->s_bytes.p);
+  hipLaunchKernelGGL(k_bs_out2, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, r.bytes,
+                     (const uint64_t*)oo, (uint8_t*)e->s_bytes.p);
   HIPCHK(hipGetLastError());
   r.counts = oc;
   r.offs = oo;

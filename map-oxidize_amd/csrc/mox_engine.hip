@@ -276,7 +276,7 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   hipLaunchKernelGGL(k_split_scatter, dim3(NB), dim3(1024), 0, s, w);
   q.step("k_split_scatter");
   // count-1 small units first: its hash-collision fallbacks join k_reduce's work list
-  hipLaunchKernelGGL(k_reduce_sort1, dim3(4 * e->n_cu), dim3(256), 0, s, w);  // 4 waves per workgroup, one unit per wave
+  hipLaunchKernelGGL(k_reduce_sort1, dim3(MOX_S1_WG * e->n_cu), dim3(256), 0, s, w);  // 4 waves per workgroup, one unit per wave
   q.step("k_reduce_sort1");
   hipLaunchKernelGGL(k_reduce_sort2, dim3(8 * e->n_cu), dim3(64), 0, s, w);  // one wave per unit of 513..1024 records
   q.step("k_reduce_sort2");

@@ -10,6 +10,12 @@ namespace mox {
 constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
 constexpr int MAP_WG_PER_CU = 1;
 constexpr int MAP_MIN_WAVES = 1;
+#ifndef MOX_LD_BATCH
+#define MOX_LD_BATCH 1  // k_map loader: poll, write and publish a row group at once (0: row by row)
+#endif
+#ifndef MOX_LD_FENCE
+#define MOX_LD_FENCE 1  // k_map loader: a scheduling fence after each row group's loads (mox_kernels.hip)
+#endif
 #ifndef MOX_MAP_LOADERS
 #define MOX_MAP_LOADERS 1
 #endif
@@ -71,6 +77,9 @@ constexpr uint32_t SPLIT_MIN = 2048;        // records below which a partition i
                                             // that many distinct keys, one table pass)
 constexpr uint32_t SPLIT_TARGET = 320;      // records per sub-bucket aimed at
 constexpr uint32_t SMALL_CAP = 512;         // sub-buckets up to this many records: k_reduce_small
+#ifndef MOX_S1_WG
+#define MOX_S1_WG 4  // k_reduce_sort1 workgroups per CU (its launch bound and persistent grid; 4 -> 128 VGPRs)
+#endif
 #ifndef MOX_SPLIT_PER_REGION
 #define MOX_SPLIT_PER_REGION 4
 #endif

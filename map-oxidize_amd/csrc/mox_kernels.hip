@@ -987,6 +987,30 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       }
     };
     auto retire = [&](const uint4 (&b)[LD_GROUP], uint32_t t0) {
+#if MOX_LD_BATCH
+      // the whole group at once: ONE poll of its slots' free words (lane i
+      // reads row t0 + i's), the rows' ds_writes back to back, then ONE store
+      // publishing every row (after the data: one wave, LDS executes in
+      // order).  Row by row, each row's poll waited for the previous row's
+      // ds_write (lgkmcnt counts both): ~370 serial cycles per row, and the
+      // loader alone took 661 us of k_map at C2 (tools/r04_ladder.sh, DBG_NO_ROW)
+      {
+        const uint32_t t = t0 + (uint32_t)lane;
+        const bool need = lane < LD_GROUP && t < n && t >= RING;
+        bool ok = !need || __hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == t - RING + 1;
+        while (!__all(ok)) {
+          __builtin_amdgcn_s_sleep(MOX_LD_SLEEP);
+          if (!ok) ok = __hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == t - RING + 1;
+        }
+      }
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#pragma unroll
+      for (int i = 0; i < LD_GROUP; i++)
+        if (t0 + i < n) reinterpret_cast<uint4*>(ring + ((t0 + i) % RING) * SLOT)[lane] = b[i];
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (lane < LD_GROUP && t0 + lane < n)
+        __hip_atomic_store(&sready[(t0 + lane) % RING], t0 + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
       // row by row: each row goes into its ring slot and is published as soon
       // as that slot is free (a whole-group wait held back the group's first
       // rows behind its slowest slot: k_map -0.9 % over three A/B pairs)
@@ -1002,17 +1026,29 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
         __atomic_signal_fence(__ATOMIC_SEQ_CST);
         if (lane == 0) __hip_atomic_store(&sready[t % RING], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
+#endif
     };
     __builtin_amdgcn_s_setprio(3);  // the loader feeds 15 consumers: never let it lose issue arbitration
     constexpr uint32_t STRIDE = MAP_LOADERS * LD_GROUP;  // rows between this loader's consecutive groups
     const uint32_t first = wv * LD_GROUP;
 #pragma unroll
-    for (int g = 0; g < LD_GROUPS - 1; g++) issue(buf[g], first + g * STRIDE);
+    // Groups are issued in order and each issue is fenced (MOX_LD_FENCE): the
+    // retire of the oldest group then waits for that group's loads only
+    // (s_waitcnt vmcnt counts loads in issue order).  Unfenced, the scheduler
+    // issued the first group's loads last, so retiring it waited for every
+    // load in flight: one group in flight, ~6.5 GB/s per CU, and the loader
+    // alone took 661 us of k_map's ~990 at C2 (tools/r04_ladder.sh).
+    for (int g = 0; g < LD_GROUPS - 1; g++) {
+      issue(buf[g], first + g * STRIDE);
+      if (MOX_LD_FENCE) SCHED_FENCE();
+    }
     for (uint32_t t0 = first; t0 < n; t0 += LD_GROUPS * STRIDE) {
 #pragma unroll
       for (int g = 0; g < LD_GROUPS; g++) {
         issue(buf[(g + LD_GROUPS - 1) % LD_GROUPS], t0 + (g + LD_GROUPS - 1) * STRIDE);
+        if (MOX_LD_FENCE) SCHED_FENCE();
         retire(buf[g], t0 + g * STRIDE);
+        if (MOX_LD_FENCE) SCHED_FENCE();
       }
     }
   } else {
@@ -1739,6 +1775,9 @@ constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort
 #define MOX_RED_UNROLL 2
 #endif
 constexpr int RED_UNROLL = MOX_RED_UNROLL;
+#ifndef MOX_RED_DYN
+#define MOX_RED_DYN 1  // k_reduce waves take chunk pairs from an LDS ticket (0: static equal shares)
+#endif
 constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
 
 struct RedLds {
@@ -1748,7 +1787,7 @@ struct RedLds {
   uint16_t* idx;           // RED_CAP: slots in output order
   uint16_t* bin;           // RED_SORTB + 1: bin counts, then bin starts (exclusive scan)
   uint16_t* fill;          // RED_SORTB: bin fill cursors
-  uint32_t* misc;          // [0] uniques [1] overflow [2] compaction cursor
+  uint32_t* misc;          // [0] uniques [1] overflow [2] chunk ticket (MOX_RED_DYN) [3] key bytes
   uint32_t* dbg;           // DBG_COUNT: [0] slow inserts [1] slow iterations [2] publication retries
   Ctl* ctl;                // path counters (MOX_PATHS builds)
   bool plain;
@@ -1803,9 +1842,15 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
         if (retry) {
           if (s.dbg) atomicAdd(&s.dbg[2], 1u);
         } else {
+          // the first free slot from the key's home slot (h & 3) on, wrapping
+          // inside the bucket: a key that finds its home free takes it, so
+          // red_home (MOX_RED_HOME) finds it in one LDS round trip
           int e = -1;
 #pragma unroll
-          for (int i = 3; i >= 0; i--) if (tv[i] == 0) e = i;
+          for (int j = 3; j >= 0; j--) {
+            const int i = (int)((h + (uint32_t)j) & 3u);
+            if (tv[i] == 0) e = i;
+          }
           if (e >= 0) {
             const uint32_t sl = 4 * b + e;
             if (atomicCAS(const_cast<uint32_t*>(&tags[sl]), 0u, h) == 0u) {
@@ -1857,6 +1902,21 @@ __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, ui
   if (cv == 0 || !key_eq16(kk, k)) return false;
   if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
   else atomicAdd(&s.cnt[sl], (unsigned long long)c);
+  return true;
+}
+
+// Fast path for a key sitting in its home slot (the slot red_insert tries
+// first): tag, key and count read in one LDS round trip, 28 bytes.
+#ifndef MOX_RED_HOME
+#define MOX_RED_HOME 0
+#endif
+__device__ __forceinline__ bool red_home(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
+  const uint32_t sl = 4 * red_bucket(h) + (h & 3u);
+  const uint32_t t = reinterpret_cast<const uint32_t*>(s.tag4)[sl];
+  const uint4 kk = s.key[sl];
+  const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (t != h || cv == 0 || !key_eq16(kk, k)) return false;
+  atomicAdd(&s.cnt[sl], (unsigned long long)c);
   return true;
 }
 
@@ -2403,8 +2463,9 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   s.plain = MOX_ABL(w.dbg, DBG_RED_PLAINADD) != 0;
   s.ctl = w.ctl;
   if (threadIdx.x < 4) dbgc[threadIdx.x] = 0;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  constexpr int NWV = RED_THREADS / 64;
+  const int tid = threadIdx.x, lane = tid & 63;
+  [[maybe_unused]] const int wv = tid >> 6;
+  [[maybe_unused]] constexpr int NWV = RED_THREADS / 64;
   const uint32_t G = reg_grid(w), RC = reg_cap(w);  // cold regions per partition (<= MAX_MAP_GRID), records per region
   uint32_t* tags = reinterpret_cast<uint32_t*>(s.tag4);
   // an overflowed map, directory or split means this attempt is rerun with
@@ -2479,23 +2540,41 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       // inserted.
       {
         const uint32_t n = split ? kin_n : rpre[G];
+        constexpr uint32_t CH = 64 * RED_UNROLL;
+#if MOX_RED_DYN
+        // dynamic shares: waves take the next 2 chunks from an LDS ticket, so
+        // they finish within ~2 chunks of each other (static equal shares left
+        // the slowest wave ~25 us behind per partition at C2,
+        // profiles/r03_k_reduce_stamps.txt: insert_tail)
+        constexpr uint32_t SCH = 2 * CH;
+        const uint32_t a1 = n;
+        auto grab = [&]() -> uint32_t {
+          uint32_t v = 0;
+          if (lane == 0) v = atomicAdd(&s.misc[2], SCH);
+          return __builtin_amdgcn_readfirstlane(v);
+        };
+        const uint32_t a0 = grab();
+#else
         const uint32_t per = (((n + NWV - 1) / NWV) + 63) & ~63u;
         const uint32_t a0 = (uint32_t)wv * per < n ? (uint32_t)wv * per : n;
         const uint32_t a1 = n - a0 < per ? n : a0 + per;
+#endif
         const uint4* ubase = split ? w.split_k + kin0 : w.cold + b * RC;  // region g at + g NB RC
         const uint64_t gstride = (uint64_t)NB * RC;
         // lane state: region r holds flat records [rs, re)
         uint32_t r = 0, rs = 0, re = split ? 0xFFFFFFFFu : 0u;
-        if (!split && a0 < a1) {  // region of a0: last r with rpre[r] <= a0 (wave-uniform search)
+        auto seek = [&](uint32_t c) {  // region of record c: last r with rpre[r] <= c (wave-uniform search)
+          if (split || c >= a1) return;
           uint32_t lo = 0, hi = G - 1;
           while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) >> 1;
-            if (rpre[mid] <= a0) lo = mid; else hi = mid - 1;
+            if (rpre[mid] <= c) lo = mid; else hi = mid - 1;
           }
           r = lo;
           rs = rpre[r];
           re = rpre[r + 1];
-        }
+        };
+        seek(a0);
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         auto load = [&](uint32_t c, uint4 (&v)[RED_UNROLL]) {  // unconditional: uniform vmcnt
 #pragma unroll
@@ -2524,6 +2603,11 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
+            if (MOX_RED_HOME) {
+#pragma unroll
+              for (int u2 = 0; u2 < RED_UNROLL; u2++)
+                if (todo[u2]) todo[u2] = !red_home(s, h[u2], cur[u2], 1);
+            }
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
               if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
@@ -2536,9 +2620,22 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
             asm volatile("" ::"v"(h[0]), "v"(h[1]));
           }
         };
-        constexpr uint32_t CH = 64 * RED_UNROLL;
         uint32_t c = a0;
         uint4 A[RED_UNROLL], B[RED_UNROLL];
+#if MOX_RED_DYN
+        // chunk pairs [c, c + CH), [c + CH, c + SCH) of one ticket, the next
+        // ticket's first chunk in flight while the second is inserted
+        if (c < a1) load(c, A);
+        while (c < a1) {
+          load(c + CH, B);
+          process(A, c);
+          const uint32_t cn = grab();
+          seek(cn);
+          load(cn, A);
+          process(B, c + CH);
+          c = cn;
+        }
+#else
         if (c < a1) load(c, A);
         while (c < a1) {
           load(c + CH, B);
@@ -2549,6 +2646,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           process(B, c);
           c += CH;
         }
+#endif
       }
       if (stamp) w.stamps[b * 8 + 1] = __builtin_amdgcn_s_memrealtime();  // wave 0 done streaming
       for (uint64_t i = ws0 + tid; i < ws1; i += RED_THREADS) {
@@ -3161,7 +3259,7 @@ __device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, cons
   wave_lds_fence();  // this unit's LDS reads before the next unit's writes
 }
 
-extern "C" __global__ __launch_bounds__(64 * S1_WAVES, 4) void k_reduce_sort1(Work w) {
+extern "C" __global__ __launch_bounds__(64 * S1_WAVES, MOX_S1_WG) void k_reduce_sort1(Work w) {
   __shared__ uint4 skey[S1_WAVES][SMALL_CAP];
   __shared__ uint16_t shp[S1_WAVES][SMALL_CAP + 2];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round 4, GPU call E: k_map loader fence A/B at C2 (var_noldf: round-3
+# loader issue order, var_ldf: each row group's loads fenced), interleaved
+# twice; the k_map time ladder with the fenced loader; the C2 bench line.
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-x5}; mkdir -p $O
+step() { echo "== $1 rc=$2"; [ "$2" -eq 0 ] || exit "$2"; }
+bash tools/ab_kernel.sh "noldf ldf noldf ldf" "0" "k_map k_reduce" > $O/ldf_ab.txt 2>&1; rc=$?; cat $O/ldf_ab.txt; step "ldf ab" $rc
+for v in noldf ldf; do echo "$v $(grep -o '"value": [0-9.]*' gpurun_out/abk/${v}_0.log | head -1)"; done
+bash tools/r04_ladder.sh > $O/ladder.txt 2>&1; rc=$?; cat $O/ladder.txt; step "ladder" $rc
+timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err; step "bench C2" $?
+python3 -c "import json;d=json.loads(open('$O/bench_c2.json').read().strip().splitlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']['avg_launch_ms'],d['phases_ms'])"
