@@ -353,11 +353,14 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r
 }
 // The subset's runs sorted by key, each by one thread in LDS (insertion sort):
 // a workgroup loads SEG_CH subset records (plus SEG_MAX after them) and sorts
-// the runs whose head lies in its SEG_CH; a run longer than SEG_MAX sets
-// *longrun, and the host then radix-sorts the whole subset instead.  Typical
-// runs are a long word's punctuation variants: a few records each.
-constexpr int SEG_CH = 2048, SEG_MAX = 64;
-extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, uint64_t m, unsigned int* longrun) {
+// the runs whose head lies in its SEG_CH.  A run longer than SEG_MAX is listed
+// (lrun: its first record and length) for k_bs_longsort; one longer than
+// RUN_LMAX, or one running past the loaded window, sets *longrun, and the host
+// then radix-sorts the whole subset instead.  Typical runs are a long word's
+// punctuation variants: a few records each.
+constexpr int SEG_CH = 2048, SEG_MAX = 64, RUN_LMAX = 4096;
+extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, uint64_t m, unsigned int* longrun, uint2* lrun,
+                                                               unsigned int* nlrun, unsigned int lrun_cap) {
   __shared__ BRec ls[SEG_CH + SEG_MAX];
   const int t = threadIdx.x;
   for (uint64_t c0 = (uint64_t)blockIdx.x * SEG_CH; c0 < m; c0 += (uint64_t)gridDim.x * SEG_CH) {
@@ -371,8 +374,18 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, uint64_t
       if ((p == 0 ? prev_run : ls[p - 1].run) == run) continue;  // not a run head
       uint32_t e = p;
       while (e + 1 < nl && ls[e + 1].run == run) e++;
-      if (e - p + 1 > (uint32_t)SEG_MAX || (e + 1 == nl && c0 + nl < m && S[c0 + nl].run == run)) {
-        atomicOr(longrun, 1u);
+      if (e + 1 == nl && c0 + nl < m && S[c0 + nl].run == run) {  // runs on past the window: count it out
+        uint64_t f = c0 + nl;
+        while (f < m && f - (c0 + p) <= (uint64_t)RUN_LMAX && S[f].run == run) f++;
+        const uint64_t len = f - (c0 + p);
+        if (len > (uint64_t)RUN_LMAX) { atomicOr(longrun, 1u); continue; }
+        const unsigned int q = atomicAdd(nlrun, 1u);
+        if (q < lrun_cap) lrun[q] = make_uint2((uint32_t)(c0 + p), (uint32_t)len); else atomicOr(longrun, 1u);
+        continue;
+      }
+      if (e - p + 1 > (uint32_t)SEG_MAX) {  // k_bs_longsort
+        const unsigned int q = atomicAdd(nlrun, 1u);
+        if (q < lrun_cap) lrun[q] = make_uint2((uint32_t)(c0 + p), e - p + 1); else atomicOr(longrun, 1u);
         continue;
       }
       for (uint32_t k = p + 1; k <= e; k++) {
@@ -384,6 +397,41 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, uint64_t
       for (uint32_t k = p; k <= e; k++) S[c0 + k] = ls[k];
     }
     __syncthreads();  // ls is reloaded for the next chunk
+  }
+}
+// The listed long runs (SEG_MAX < length <= RUN_LMAX), one workgroup each:
+// loaded into LDS, padded to a power of two with ~0 keys, bitonic-sorted by
+// key, written back.  (Equal keys are words tied on this window too: their
+// order is settled by the next level.)
+extern "C" __global__ __launch_bounds__(256) void k_bs_longsort(BRec* S, const uint2* lrun, const unsigned int* nlrun,
+                                                                unsigned int lrun_cap) {
+  __shared__ BRec ls[RUN_LMAX];
+  const unsigned int nr = *nlrun < lrun_cap ? *nlrun : lrun_cap;
+  const int t = threadIdx.x;
+  for (unsigned int q = blockIdx.x; q < nr; q += gridDim.x) {
+    const uint2 lr = lrun[q];
+    const uint32_t L = lr.y;
+    uint32_t P = 1;
+    while (P < L) P <<= 1;
+    for (uint32_t i = t; i < P; i += 256) {
+      if (i < L) ls[i] = S[lr.x + i];
+      else { ls[i].key = ~0ull; ls[i].run = ~0u; ls[i].idx = ~0u; }
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1)
+      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+        for (uint32_t i = t; i < P; i += 256) {
+          const uint32_t l = i ^ j;
+          if (l > i) {
+            const bool asc = (i & k) == 0;
+            const BRec a = ls[i], b = ls[l];
+            if ((a.key > b.key) == asc) { ls[i] = b; ls[l] = a; }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t i = t; i < L; i += 256) S[lr.x + i] = ls[i];
+    __syncthreads();
   }
 }
 extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub, uint64_t m, const uint64_t* pos, BRec* r) {
@@ -554,7 +602,8 @@ int bsort_table(mox_engine* e) {
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   // scratch: records A, B, subset S, payload | run flags, positions | status | gh, gs | scan sums | totals, err
   const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
-  const uint64_t need = 4 * rec + 2 * u64n + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
+  const unsigned int lrun_cap = (unsigned int)std::min<uint64_t>(1u << 20, n / 4 + 16);  // k_bs_longsort's run list
+  const uint64_t need = 4 * rec + 2 * u64n + 8ull * lrun_cap + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
   int rc;
   if ((rc = grow_dev(e->s_tmp, need)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
       (rc = grow_dev(e->s_bytes, nb + 64)))
@@ -567,6 +616,7 @@ int bsort_table(mox_engine* e) {
   BPay* pay = (BPay*)q; q += rec;
   uint64_t* fin = (uint64_t*)q; q += u64n;
   uint64_t* pos = (uint64_t*)q; q += u64n;
+  uint2* lrun = (uint2*)q; q += 8ull * lrun_cap;
   BSort s;
   s.status = (uint64_t*)q; q += stb;
   s.gh = (unsigned long long*)q; q += OS_DIGITS * 256 * 8;
@@ -576,7 +626,7 @@ int bsort_table(mox_engine* e) {
   s.err = (unsigned int*)q;
   s.h_gh = e->h_bsort;
   uint64_t* h_tot = (uint64_t*)(e->h_bsort + OS_DIGITS * 256);
-  HIPCHK(hipMemsetAsync(s.err, 0, 8, st));  // [0] look-back timeout [1] long run (k_bs_segsort)
+  HIPCHK(hipMemsetAsync(s.err, 0, 12, st));  // [0] look-back timeout [1] radix fallback [2] long runs (k_bs_segsort)
   // level 0: every word by its first 7 bytes and length class
   hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, r.counts, n, A, pay);
   s.a = A;
@@ -588,7 +638,7 @@ int bsort_table(mox_engine* e) {
   // the next window (by run: short runs in LDS by k_bs_segsort; a subset with
   // a longer run by the radix passes, run id as the most significant digits)
   uint32_t run_base = 1;
-  unsigned int* longrun = s.err + 1;
+  unsigned int* longrun = s.err + 1;  // [0] fall back [1] listed long runs
   for (uint32_t level = 1;; level++) {
     hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin);
     if ((rc = scan_u64(e, fin, n, total, ssum))) return rc;
@@ -601,9 +651,11 @@ int bsort_table(mox_engine* e) {
     if ((uint64_t)run_base + runs >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
     hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin, m,
                        run_base, r.offs, r.bytes, level, S, pos);
-    HIPCHK(hipMemsetAsync(longrun, 0, 4, st));
+    HIPCHK(hipMemsetAsync(longrun, 0, 8, st));  // [0] fall back to the radix [1] listed long runs
     hipLaunchKernelGGL(k_bs_segsort, dim3((uint32_t)std::min<uint64_t>(4096, (m + SEG_CH - 1) / SEG_CH)), dim3(256), 0, st, S, m,
-                       longrun);
+                       longrun, lrun, longrun + 1, lrun_cap);
+    hipLaunchKernelGGL(k_bs_longsort, dim3(1024), dim3(256), 0, st, S, (const uint2*)lrun, (const unsigned int*)(longrun + 1),
+                       lrun_cap);
     HIPCHK(hipMemcpyAsync(h_tot + 3, longrun, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     BRec* sorted = S;

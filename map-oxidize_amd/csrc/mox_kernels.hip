@@ -506,6 +506,9 @@ __device__ void generic_token(const MapCtx& m, uint64_t p) {
 // Clamped aligned 16-byte load: the block always overlaps [lo, hi), so it never
 // leaves the allocation; bytes out of range are fixed up by fix16.
 __device__ __forceinline__ uint4 raw16(const Corpus& c, uint64_t p) {
+  // an empty buffer has no block to clamp to (c.hi - 1 < c.lo: the clamp would
+  // land 16 bytes below the buffer): read nothing
+  if (c.hi <= c.lo) return make_uint4(0x20202020u, 0x20202020u, 0x20202020u, 0x20202020u);
   const uint64_t first = c.lo & ~15ull, last = (c.hi - 1) & ~15ull;
   p = p < first ? first : (p > last ? last : p);
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
