@@ -101,7 +101,10 @@ constexpr uint64_t ARENA_BIT = 1ull << 63;              // long-word ref points 
 enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO_COLDSTORE = 8u, DBG_NO_DICTADD = 16u,
                   DBG_RED_NOSORT = 32u, DBG_RED_NOINSERT = 64u, DBG_RED_NOSLOW = 128u, DBG_COUNT = 256u, DBG_RED_PLAINADD = 512u, DBG_STAMP = 1024u,
                   DBG_RED_TWICE = 2048u,    // TWICE: k_reduce streams the cold records twice (timing only: counts double)
-                  DBG_NO_ROW = 4096u };     // NO_ROW: k_map consumers release each row untouched (loader + ring only)
+                  DBG_NO_ROW = 4096u,       // NO_ROW: k_map consumers release each row untouched (loader + ring only)
+                  DBG_PAIR_NOSTORE = 8192u, // no dictionary: pairs formed, their global stores skipped (timing only)
+                  DBG_NOPAIR = 16384u,      // no dictionary: every record stored alone, no pair slots (timing A/B)
+                  DBG_PAIR_SEQ = 32768u };  // no dictionary: pairs stored at consecutive addresses (timing only: wrong regions)
 // Bounds checks of derived indices (UnitDesc ranges, scatter cursors, table
 // offsets), compiled in only with -DMOX_CHECK (libmox_check.so, `make check`):
 // a failed check counts into ctl->dbg_cnt[0], records the largest site id in

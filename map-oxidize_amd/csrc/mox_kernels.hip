@@ -426,17 +426,27 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
       const int r = pair_try(m.s.pst, m.s.pend, B, key, &q);
       if (r == 2) {
         const uint32_t pos = atomicAdd(&m.s.bcnt[B], 2u);
-        if (pos < SPLIT_PER_REGION) {
-          note_sample(m, b, qr, pos, hash32(q.x, q.y, q.z, q.w));
-          note_sample(m, b, qr, pos + 1, h);
-        }
-        if (pos + 1 < m.rc) {
-          uint4* o = region_of(m, b, qr) + pos;
+        if (MOX_ABL(m.w.dbg, DBG_PAIR_NOSTORE)) {
+          asm volatile("" ::"v"(pos), "v"(q.x));
+        } else if (MOX_ABL(m.w.dbg, DBG_PAIR_SEQ)) {
+          const uint64_t slab = (uint64_t)NB * m.qf * m.rc;
+          const uint32_t sp = atomicAdd(&m.s.misc[2], 2u) % (uint32_t)(slab > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : slab - 1);
+          uint4* o = m.w.cold + blockIdx.x * slab + (sp & ~1u);
           o[0] = q;
           o[1] = key;
         } else {
-          cold_spill(m, q);
-          cold_spill(m, key);
+          if (pos < SPLIT_PER_REGION) {
+            note_sample(m, b, qr, pos, hash32(q.x, q.y, q.z, q.w));
+            note_sample(m, b, qr, pos + 1, h);
+          }
+          if (pos + 1 < m.rc) {
+            uint4* o = region_of(m, b, qr) + pos;
+            o[0] = q;
+            o[1] = key;
+          } else {
+            cold_spill(m, q);
+            cold_spill(m, key);
+          }
         }
       }
       done = r != 0;
@@ -448,7 +458,15 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-  if (m.dict_n == 0) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key); return; }
+  if (m.dict_n == 0) {
+    if (!MOX_ABL(m.w.dbg, DBG_NOPAIR)) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key); return; }
+    const uint32_t B = h >> (32 - NB_LOG2 - m.qb), qr = B & (m.qf - 1);
+    const uint32_t pos = atomicAdd(&m.s.bcnt[B], 1u);
+    if (pos < SPLIT_PER_REGION) note_sample(m, b, qr, pos, h);
+    if (pos < m.rc) region_of(m, b, qr)[pos] = key;
+    else cold_spill(m, key);
+    return;
+  }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < SPLIT_PER_REGION) note_sample(m, b, 0, pos, h);
   if (pos < m.rc) {
@@ -1782,6 +1800,11 @@ constexpr int RED_UNROLL = MOX_RED_UNROLL;
 #define MOX_RED_DYN 1  // k_reduce waves take chunk pairs from an LDS ticket (0: static equal shares)
 #endif
 constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
+#ifndef MOX_RED_TAB
+#define MOX_RED_TAB 1  // k_reduce: ticket -> region table (0: binary search per ticket)
+#endif
+constexpr uint32_t RED_TICKET = 128 * MOX_RED_UNROLL;  // records per k_reduce ticket (two chunks)
+constexpr int RED_TAB_MAX = RED_SORTB;                  // ticket table entries (u16, in the fill space)
 
 struct RedLds {
   uint4* tag4;             // RED_BK x 4 key hashes (0 = free)
@@ -2461,6 +2484,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   __shared__ uint32_t s_unit;
   __shared__ uint64_t red_wsum[RED_THREADS / 64];
   uint32_t* rpre = reinterpret_cast<uint32_t*>(s.idx);  // region prefix (G + 1 words in the idx + bin space)
+  uint16_t* rtab = s.fill;                              // ticket -> region (fill space: free until the sort)
   static_assert(RED_CAP * 2 + (RED_SORTB + 8) * 2 >= (MAX_MAP_GRID + 1) * 4, "region prefix space");
   s.dbg = MOX_ABL(w.dbg, DBG_COUNT) ? dbgc : nullptr;
   s.plain = MOX_ABL(w.dbg, DBG_RED_PLAINADD) != 0;
@@ -2526,11 +2550,24 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       if (tid == 0) { s.misc[0] = 0; s.misc[1] = 0; s.misc[2] = 0; s.misc[3] = 0; }
       // region prefix of a whole partition (the map workgroups' regions one after
       // another), in the sort index / bin space, which is free until the sort
+      bool tab = false;  // ticket -> region table built (MOX_RED_TAB)
       if (!split) {
         uint64_t tot;
-        const uint64_t ex = block_exscan(tid < (int)G ? cold_n_at(w, G, tid, b) : 0u, red_wsum, tot);
+        const uint32_t cn = tid < (int)G ? cold_n_at(w, G, tid, b) : 0u;
+        const uint64_t ex = block_exscan(cn, red_wsum, tot);
         if (tid < (int)G) rpre[tid] = (uint32_t)ex;
         if (tid == 0) rpre[G] = (uint32_t)tot;
+#if MOX_RED_DYN && MOX_RED_TAB
+        // region of every ticket start (record j RED_TICKET): the region holding
+        // it, written by that region's thread from its own prefix and count, so
+        // a wave finds a ticket's region in one LDS read instead of a binary
+        // search over the prefix (8 dependent reads at 256 regions)
+        tab = (tot + RED_TICKET - 1) / RED_TICKET <= (uint64_t)RED_TAB_MAX;
+        if (tab && cn) {
+          for (uint32_t j = (uint32_t)((ex + RED_TICKET - 1) / RED_TICKET); (uint64_t)j * RED_TICKET < ex + cn; j++)
+            rtab[j] = (uint16_t)tid;
+        }
+#endif
       }
       __syncthreads();
       for (int rep = 0; rep < (MOX_ABL(w.dbg, DBG_RED_TWICE) ? 2 : 1); rep++)
@@ -2549,7 +2586,8 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         // they finish within ~2 chunks of each other (static equal shares left
         // the slowest wave ~25 us behind per partition at C2,
         // profiles/r03_k_reduce_stamps.txt: insert_tail)
-        constexpr uint32_t SCH = 2 * CH;
+        constexpr uint32_t SCH = RED_TICKET;
+        static_assert(RED_TICKET == 2 * CH, "a ticket is two chunks");
         const uint32_t a1 = n;
         auto grab = [&]() -> uint32_t {
           uint32_t v = 0;
@@ -2568,6 +2606,12 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         uint32_t r = 0, rs = 0, re = split ? 0xFFFFFFFFu : 0u;
         auto seek = [&](uint32_t c) {  // region of record c: last r with rpre[r] <= c (wave-uniform search)
           if (split || c >= a1) return;
+          if (tab) {  // c is a ticket start
+            r = rtab[c / SCH];
+            rs = rpre[r];
+            re = rpre[r + 1];
+            return;
+          }
           uint32_t lo = 0, hi = G - 1;
           while (lo < hi) {
             const uint32_t mid = (lo + hi + 1) >> 1;
@@ -2631,8 +2675,11 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         if (c < a1) load(c, A);
         while (c < a1) {
           load(c + CH, B);
+          // the next ticket's LDS atomic goes out before this chunk's probes
+          uint32_t tv = 0;
+          if (lane == 0) tv = atomicAdd(&s.misc[2], SCH);
           process(A, c);
-          const uint32_t cn = grab();
+          const uint32_t cn = __builtin_amdgcn_readfirstlane(tv);
           seek(cn);
           load(cn, A);
           process(B, c + CH);
