@@ -13,10 +13,15 @@ for v in $VARS; do
     MOX_LIB=build/var_$v/libmox.so MOX_DBG=$d timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- \
       python3 bench.py $ARGS > $D.log 2>&1
     rc=$?; [ $rc -eq 0 ] || { echo "$v dbg $d rc=$rc"; tail -3 $D.log; exit $rc; }
-    python3 - "$D/run_kernel_stats.csv" "$v dbg=$d" $KS <<'PY'
-import csv, sys
+    python3 - "$D/run_kernel_stats.csv" "$v dbg=$d" "$D.log" $KS <<'PY'
+import csv, json, sys
 rows = {r["Name"].split("(")[0]: r for r in csv.DictReader(open(sys.argv[1]))}
-print(sys.argv[2], " ".join("%s %.1fus" % (k, float(rows[k]["AverageNs"]) / 1e3) for k in sys.argv[3:] if k in rows))
+gbs = ""
+try:
+    gbs = "%.1f GB/s " % json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])["value"]
+except Exception:
+    pass
+print(sys.argv[2], gbs + " ".join("%s %.1fus" % (k, float(rows[k]["AverageNs"]) / 1e3) for k in sys.argv[4:] if k in rows))
 PY
   done
 done
