@@ -269,8 +269,10 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_hist");
   hipLaunchKernelGGL(k_scatter, dim3(w.map_grid), dim3(1024), 0, s, w);
   q.step("k_scatter");
-  hipLaunchKernelGGL(k_split_count, dim3(NB), dim3(256), 0, s, w);  // SC_THREADS; the last workgroup: unit scan
+  hipLaunchKernelGGL(k_split_count, dim3(NB), dim3(256), 0, s, w);  // SC_THREADS
   q.step("k_split_count");
+  hipLaunchKernelGGL(k_unit_scan, dim3(1), dim3(256), 0, s, w);  // SC_THREADS
+  q.step("k_unit_scan");
   hipLaunchKernelGGL(k_split_scatter, dim3(NB), dim3(1024), 0, s, w);
   q.step("k_split_scatter");
   // count-1 small units first: its hash-collision fallbacks join k_reduce's work list
@@ -283,8 +285,10 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   hipLaunchKernelGGL(k_reduce_small, dim3(8 * e->n_cu), dim3(128), 0, s, w);  // persistent, 8 per CU (SR_THREADS)
   q.step("k_reduce_small");
   q.rec(4);
-  hipLaunchKernelGGL(k_unit_uniq_scan, dim3(NB), dim3(1024), 0, s, w);  // the last workgroup: final scan
+  hipLaunchKernelGGL(k_unit_uniq_scan, dim3(NB), dim3(1024), 0, s, w);
   q.step("k_unit_uniq_scan");
+  hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(NB), 0, s, w);
+  q.step("k_final_scan");
   hipLaunchKernelGGL(k_mat, dim3(1024), dim3(256), 0, s, w, c);  // grid >= NB long-table slices
   q.step("k_mat");
   q.rec(5);

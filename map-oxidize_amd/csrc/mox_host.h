@@ -43,8 +43,10 @@ __global__ void k_hist(Work w);
 __global__ void k_scatter(Work w);
 __global__ void k_reduce(Work w);
 __global__ void k_split_count(Work w);
+__global__ void k_unit_scan(Work w);
 __global__ void k_split_scatter(Work w);
 __global__ void k_unit_uniq_scan(Work w);
+__global__ void k_final_scan(Work w);
 __global__ void k_reduce_small(Work w);
 __global__ void k_reduce_sort1(Work w);
 __global__ void k_reduce_sort2(Work w);

@@ -368,7 +368,7 @@ struct Work {  // device buffers of one engine
   // reduce units (partition b = units u_base[b] .. u_base[b+1]-1; one unit
   // unless b was split into 2^b_kk[b] sub-buckets)
   uint32_t* b_kk;                 // NB
-  uint32_t* red_order;            // NB: partitions by descending record count (unit_scan), k_reduce workgroup i takes red_order[i]
+  uint32_t* red_order;            // NB: partitions by descending record count (k_unit_scan), k_reduce workgroup i takes red_order[i]
   uint32_t* u_base;               // NB + 1
   uint32_t* sub_hist;             // NB x 2 x SUB_N: cold, weighted records per sub-bucket
   uint64_t* sp_off;               // NB + 1: first split_k record of partition b
@@ -380,7 +380,7 @@ struct Work {  // device buffers of one engine
   uint64_t* u_uniq;               // U_MAX: distinct keys of unit u
   uint64_t* u_bytes;              // U_MAX: key bytes of unit u's distinct keys
   uint64_t* u_bytes_off;          // U_MAX: byte offset of unit u inside its partition
-  // table directory (k_unit_uniq_scan with its final scan -> k_mat)
+  // table directory (k_unit_uniq_scan -> k_final_scan -> k_mat)
   uint64_t* b_bytes;              // NB: key bytes of partition b
   uint64_t* bytes_off;            // NB + 1: byte offset of partition b's first key
   uint64_t* ls_n;                 // NB: occupied long-table slots of slice b

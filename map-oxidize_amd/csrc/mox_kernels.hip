@@ -16,12 +16,12 @@
 //   k_unicode                 full Unicode lowercase + Final_Sigma for non-ASCII tokens,
 //                             and the dictionary totals as weighted records
 //   k_hist (+ bucket scan in its last workgroup), k_scatter   shuffle directory
-//   k_split_count (+ unit scan), k_split_scatter
+//   k_split_count, k_unit_scan, k_split_scatter
 //                             high-cardinality split of partitions into sub-bucket units
 //   k_reduce, k_reduce_small  per-unit LDS hash group-by / sort-based reduce (= reduce_phase merge,
 //                             main.rs:132-134), deterministic (hash, key) order
 //   long table                words > 16 bytes: hashed keys, byte-compare resolution
-//   k_unit_uniq_scan (+ final scan), k_mat
+//   k_unit_uniq_scan, k_final_scan, k_mat
 //                             dense (word, count) table in HBM, one pass
 #include "mox_internal.h"
 
@@ -2080,9 +2080,9 @@ __device__ __forceinline__ void split_count(const Work& w) {
   __shared__ uint32_t s_ones, s_kk;
   const uint32_t b = blockIdx.x;
   const int tid = threadIdx.x;
-  if (w.ctl->overflow & OVF_RERUN) { if (tid == 0) st_agent(&w.b_kk[b], 0u); return; }
+  if (w.ctl->overflow & OVF_RERUN) { if (tid == 0) w.b_kk[b] = 0; return; }
   const uint64_t nc = w.b_recs[b], nw = w.b_w[b];
-  if (nc + nw <= SPLIT_MIN) { if (tid == 0) st_agent(&w.b_kk[b], 0u); return; }
+  if (nc + nw <= SPLIT_MIN) { if (tid == 0) w.b_kk[b] = 0; return; }
   for (int i = tid; i < LC_BITS / 32; i += blockDim.x) bm[i] = 0;
   if (tid == 0) s_ones = 0;
   __syncthreads();
@@ -2129,7 +2129,7 @@ __device__ __forceinline__ void split_count(const Work& w) {
       while (kk < SUB_BITS_MAX && est > (float)SPLIT_TARGET * (float)(1u << kk)) kk++;
     }
     s_kk = kk;
-    st_agent(&w.b_kk[b], kk);  // read by k_split_count's last workgroup (unit_scan)
+    w.b_kk[b] = kk;
   }
   __syncthreads();
   const uint32_t kk = s_kk;
@@ -2157,7 +2157,7 @@ __device__ __forceinline__ uint64_t split_span(uint64_t n, uint32_t kk) { return
 // the output region of every whole partition.
 constexpr int SC_PER = NB / SC_THREADS;
 constexpr int SC_BINS = 256;  // size classes of the k_reduce order (one per thread)
-static_assert(SC_BINS == SC_THREADS && SC_PER * SC_THREADS == NB, "unit_scan geometry");
+static_assert(SC_BINS == SC_THREADS && SC_PER * SC_THREADS == NB, "k_unit_scan geometry");
 __device__ void unit_scan(const Work& w) {
   __shared__ uint64_t wsum[16];
   __shared__ uint32_t smax, smin, bins[SC_BINS], fill[SC_BINS];
@@ -2171,7 +2171,7 @@ __device__ void unit_scan(const Work& w) {
 #pragma unroll
   for (int j = 0; j < SC_PER; j++) {
     const uint32_t b = SC_PER * t + j;
-    kk[j] = ld_agent(&w.b_kk[b]);  // k_split_count's other workgroups (agent-scope stores)
+    kk[j] = w.b_kk[b];
     const uint64_t nr = w.b_recs[b], nwb = w.b_w[b];
     sz[j] = kk[j] ? 0u : (uint32_t)min(nr + nwb, 0x7FFFFFFFull);  // split partitions: their units go to the queues
     nu += 1ull << kk[j];
@@ -2246,12 +2246,8 @@ __device__ void unit_scan(const Work& w) {
     if (tk > w.split_k_cap || tw > w.split_w_cap) atomicOr(&w.ctl->overflow, OVF_SPLIT);
   }
 }
-// The last workgroup to finish its partition's split decision runs the unit
-// scan (one launch less than a separate one-workgroup kernel).
-extern "C" __global__ __launch_bounds__(SC_THREADS) void k_split_count(Work w) {
-  split_count(w);
-  if (last_block(&w.ctl->done[2])) unit_scan(w);
-}
+extern "C" __global__ __launch_bounds__(SC_THREADS) void k_split_count(Work w) { split_count(w); }
+extern "C" __global__ __launch_bounds__(SC_THREADS) void k_unit_scan(Work w) { unit_scan(w); }  // one workgroup
 
 // k_split_scatter (one workgroup per split partition): unit directory from the
 // histogram, then every record of the partition to its unit's contiguous range
@@ -2512,7 +2508,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 #else
 #define RED_MARK(k) do { } while (0)
 #endif
-  const uint32_t ob = blockIdx.x < NB ? w.red_order[blockIdx.x] : 0u;  // unit_scan: biggest partitions first
+  const uint32_t ob = blockIdx.x < NB ? w.red_order[blockIdx.x] : 0u;  // k_unit_scan: biggest partitions first
   bool own = blockIdx.x < NB && w.b_kk[ob] == 0;
   for (;;) {
     uint32_t u;
@@ -2626,24 +2622,51 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           re = rpre[r + 1];
         };
         seek(a0);
+        // the walk state is settled before the first record load: a value of it
+        // still arriving from a register reload (scratch is vector memory) made
+        // the compiler wait for every load in flight at each chunk (vmcnt(0))
+        asm volatile("" ::"v"(r), "v"(rs), "v"(re));
         typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
         auto load = [&](uint32_t c, uint4 (&v)[RED_UNROLL]) {  // unconditional: uniform vmcnt
+          // every address first, then the loads back to back: a region walk
+          // between two loads of one chunk made the compiler wait for the first
+          // (its temporaries reused the in-flight load's registers)
+          const uint4* p[RED_UNROLL];
 #pragma unroll
           for (int u2 = 0; u2 < RED_UNROLL; u2++) {
             const uint32_t i = c + u2 * 64 + lane;
             const bool ok = i < a1;
             bool adv = ok && i >= re;
-            while (__any(adv)) {  // no cross-lane dependence: a plain per-lane walk
-              if (adv) { r++; rs = re; re = rpre[r + 1]; }
-              adv = ok && i >= re;
+            // per-lane walk to the region holding record i: one step covers a
+            // chunk that crosses one region end (regions average ~150 records);
+            // the loop only runs for regions of fewer than 64 records (the
+            // compiler put a wait for every load in flight at the head of a
+            // loop here, so the common step stays outside it)
+            if (adv) { r++; rs = re; re = rpre[r + 1]; }
+            adv = ok && i >= re;
+            if (__any(adv)) {
+              do {
+                if (adv) { r++; rs = re; re = rpre[r + 1]; }
+                adv = ok && i >= re;
+              } while (__any(adv));
             }
-            const uint4* p = ok ? ubase + (uint64_t)r * gstride + (i - rs) : ubase;
-            const u32x4 x = *reinterpret_cast<const u32x4*>(p);
+            p[u2] = ok ? ubase + (uint64_t)r * gstride + (i - rs) : ubase;
+          }
+#pragma unroll
+          for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+            const u32x4 x = *reinterpret_cast<const u32x4*>(p[u2]);
             v[u2] = make_uint4(x.x, x.y, x.z, x.w);
           }
         };
         auto process = [&](const uint4 (&cur)[RED_UNROLL], uint32_t c) {
-          if (__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;  // redone anyway
+          if (__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {  // redone anyway
+            // the chunk's loads are waited for on this path too: left pending
+            // into the next iteration, they made the compiler wait for every
+            // load in flight (vmcnt(0)) before the region walk, each chunk
+#pragma unroll
+            for (int u2 = 0; u2 < RED_UNROLL; u2++) asm volatile("" ::"v"(cur[u2].x), "v"(cur[u2].y), "v"(cur[u2].z), "v"(cur[u2].w));
+            return;
+          }
           uint32_t h[RED_UNROLL];
           bool todo[RED_UNROLL];
           RED_MARK(0);
@@ -3400,7 +3423,7 @@ __device__ __forceinline__ void unit_uniq_scan(const Work& w) {
   if (w.ctl->overflow & OVF_RERUN) return;
   const uint32_t kk = w.b_kk[b], u0 = w.u_base[b];
   if (!kk) {
-    if (tid == 0) { w.u_uniq_off[u0] = 0; w.u_bytes_off[u0] = 0; st_agent(&w.b_bytes[b], w.u_bytes[u0]); }
+    if (tid == 0) { w.u_uniq_off[u0] = 0; w.u_bytes_off[u0] = 0; w.b_bytes[b] = w.u_bytes[u0]; }
   } else {
     const uint32_t nsub = 1u << kk;
     uint64_t v[SUB_PER_T], y[SUB_PER_T], sv = 0, sy = 0;
@@ -3422,7 +3445,7 @@ __device__ __forceinline__ void unit_uniq_scan(const Work& w) {
       ex += v[j];
       ey += y[j];
     }
-    if (tid == 0) { st_agent(&w.b_uniq[b], tot); st_agent(&w.b_bytes[b], btot); }
+    if (tid == 0) { w.b_uniq[b] = tot; w.b_bytes[b] = btot; }
   }
   // long-table slice b
   const uint64_t L = w.long_cap / NB, s0 = (uint64_t)b * L;
@@ -3435,7 +3458,7 @@ __device__ __forceinline__ void unit_uniq_scan(const Work& w) {
   }
   if (n) { atomicAdd(&lsn, n); atomicAdd(&lsb, by); }
   __syncthreads();
-  if (tid == 0) { st_agent(&w.ls_n[b], (uint64_t)lsn); st_agent(&w.ls_b[b], (uint64_t)lsb); }  // read by the last workgroup (final_scan)
+  if (tid == 0) { w.ls_n[b] = lsn; w.ls_b[b] = lsb; }
 }
 
 // One workgroup of NB threads: partition / slice offsets, table sizes and the
@@ -3446,11 +3469,10 @@ __device__ void final_scan(const Work& w) {
   const bool rerun = (w.ctl->overflow & OVF_RERUN) != 0;  // nothing was reduced
   const uint32_t b = threadIdx.x;
   uint64_t ns, sb, nl, lb;
-  // written by the other k_unit_uniq_scan workgroups with agent-scope stores
-  w.uniq_off[b] = block_exscan(rerun ? 0 : ld_agent(&w.b_uniq[b]), wsum, ns);
-  w.bytes_off[b] = block_exscan(rerun ? 0 : ld_agent(&w.b_bytes[b]), wsum, sb);
-  w.ls_off[b] = block_exscan(rerun ? 0 : ld_agent(&w.ls_n[b]), wsum, nl);
-  w.ls_boff[b] = block_exscan(rerun ? 0 : ld_agent(&w.ls_b[b]), wsum, lb);
+  w.uniq_off[b] = block_exscan(rerun ? 0 : w.b_uniq[b], wsum, ns);
+  w.bytes_off[b] = block_exscan(rerun ? 0 : w.b_bytes[b], wsum, sb);
+  w.ls_off[b] = block_exscan(rerun ? 0 : w.ls_n[b], wsum, nl);
+  w.ls_boff[b] = block_exscan(rerun ? 0 : w.ls_b[b], wsum, lb);
   if (b == 0) {
     w.uniq_off[NB] = ns;
     w.bytes_off[NB] = sb;
@@ -3465,13 +3487,8 @@ __device__ void final_scan(const Work& w) {
     if (sb + lb > w.bytes_cap) atomicOr(&w.ctl->overflow, OVF_BYTES);
   }
 }
-// The last workgroup runs the final scan (one launch less than a separate
-// one-workgroup kernel).
-extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) {
-  static_assert(NB == 1024, "final_scan: one partition per thread of a k_unit_uniq_scan workgroup");
-  unit_uniq_scan(w);
-  if (last_block(&w.ctl->done[1])) final_scan(w);
-}
+extern "C" __global__ __launch_bounds__(1024) void k_unit_uniq_scan(Work w) { unit_uniq_scan(w); }
+extern "C" __global__ __launch_bounds__(NB) void k_final_scan(Work w) { final_scan(w); }  // one workgroup
 
 // True when this attempt produced a complete table that fits its buffers.
 __device__ __forceinline__ bool table_ok(const Work& w) {
