@@ -662,6 +662,22 @@ __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&
   K[2] = __builtin_amdgcn_alignbyte(E3, E2, sh) & M.z;
   K[3] = __builtin_amdgcn_alignbyte(E4, E3, sh) & M.w;
 }
+// The rare paths of a row (byte-wise walks, Unicode checks) load from global
+// memory.  Left pending where they rejoin the common path, their destination
+// registers made the compiler wait for every vector memory operation in flight
+// (s_waitcnt vmcnt(0)) at the next use of those registers on EVERY row, which
+// in a consumer means waiting for its own cold-record stores.  Waiting at the
+// end of the rare path instead keeps the common path free of that wait.
+// (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15)
+__device__ __forceinline__ void vm_settle() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
+// s_waitcnt immediate (gfx9 encoding) for vmcnt(v), expcnt and lgkmcnt not waited on
+constexpr int vmcnt_wait(int v) { return (v & 15) | ((v >> 4) << 14) | (7 << 4) | (15 << 8); }
+// the k_map loader retires its oldest row group while the LD_GROUPS - 1 younger
+// groups' loads stay in flight
+constexpr int LD_RETIRE_WAIT = vmcnt_wait((LD_GROUPS - 1) * LD_GROUP);
+static_assert((LD_GROUPS - 1) * LD_GROUP < 64, "vmcnt is 6 bits");
+
 // compiler scheduling barrier: no instruction moves across it
 #define SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 // A sched_barrier orders only what the selection DAG left on each side of it,
@@ -845,6 +861,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     chk = anyz || near_end;
   } else {
     start = ctx ? 0u : slow_starts(m, p0);
+    vm_settle();
   }
   if MOX_ABL(m.w.dbg, DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
   const uint32_t cnt = __popc(start);
@@ -899,6 +916,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       const uint32_t e = list[j];
       if (e & 0x8000u) generic_token(m, sbase + (e & 1023u));
     }
+    vm_settle();
   }
   if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
   uint64_t t1 = 0;
@@ -1015,13 +1033,20 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       // order).  Row by row, each row's poll waited for the previous row's
       // ds_write (lgkmcnt counts both): ~370 serial cycles per row, and the
       // loader alone took 661 us of k_map at C2 (tools/r04_ladder.sh, DBG_NO_ROW)
+      // this group's loads are done once at most the younger groups' loads are
+      // in flight (loads return in order).  Said explicitly, ahead of the slot
+      // poll: after the poll loop the compiler's own wait was vmcnt(0), which
+      // drained the loader's whole pipeline once per round of LD_GROUPS groups
+      __builtin_amdgcn_s_waitcnt(LD_RETIRE_WAIT);
       {
         const uint32_t t = t0 + (uint32_t)lane;
         const bool need = lane < LD_GROUP && t < n && t >= RING;
         bool ok = !need || __hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == t - RING + 1;
-        while (!__all(ok)) {
-          __builtin_amdgcn_s_sleep(MOX_LD_SLEEP);
-          if (!ok) ok = __hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == t - RING + 1;
+        if (!__all(ok)) {  // (the loop only when a slot is still taken: see the wait above)
+          do {
+            __builtin_amdgcn_s_sleep(MOX_LD_SLEEP);
+            if (!ok) ok = __hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == t - RING + 1;
+          } while (!__all(ok));
         }
       }
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -2294,10 +2319,13 @@ __device__ void split_stage_slice(const Work& w, uint32_t b, uint32_t q, uint32_
   __syncthreads();
   const uint32_t n = S.rpre[M];
   uint32_t r = 0, rs = 0, re = S.rpre[1];  // this thread's region walk (its indices only grow)
-  for (uint32_t c0 = 0; c0 < n; c0 += SST_CH) {
-    uint4 k[SST_PER];
-    uint32_t sub[SST_PER], rk[SST_PER];
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  // the chunk's records; the next chunk's loads are issued as soon as these
+  // are in the stage, so they are in flight during this chunk's stores (the
+  // stores are a fixed count of predicated instructions: waiting for the
+  // loads then needs vmcnt(SST_PER), not vmcnt(0) behind the stores)
+  uint4 k[SST_PER];
+  auto load_chunk = [&](uint32_t c0) {
 #pragma unroll
     for (int j = 0; j < SST_PER; j++) {
       const uint32_t i = c0 + j * 1024 + tid;
@@ -2307,6 +2335,10 @@ __device__ void split_stage_slice(const Work& w, uint32_t b, uint32_t q, uint32_
       const u32x4 x = *reinterpret_cast<const u32x4*>(ok_i ? p : w.cold);
       k[j] = make_uint4(x.x, x.y, x.z, x.w);
     }
+  };
+  if (n) load_chunk(0);
+  for (uint32_t c0 = 0; c0 < n; c0 += SST_CH) {
+    uint32_t sub[SST_PER], rk[SST_PER];
 #pragma unroll
     for (int j = 0; j < SST_PER; j++) {
       const uint32_t i = c0 + j * 1024 + tid;
@@ -2333,14 +2365,19 @@ __device__ void split_stage_slice(const Work& w, uint32_t b, uint32_t q, uint32_
         S.stage[pos] = k[j];
         S.sidx[pos] = (uint16_t)sub[j];
       }
+    if (c0 + SST_CH < n) load_chunk(c0 + SST_CH);
     __syncthreads();
     const uint32_t nc = n - c0 < (uint32_t)SST_CH ? n - c0 : (uint32_t)SST_CH;
-    for (uint32_t j = tid; j < nc; j += 1024) {
-      const uint32_t sb = S.sidx[j];
-      const uint32_t d = S.gb[sb] + (j - S.lst[sb]);
-      if (MOX_CHK(w, d < tc && kb + d < w.split_k_cap, CHK_SPLIT_K)) ok[d] = S.stage[j];
+#pragma unroll
+    for (int jj = 0; jj < SST_PER; jj++) {
+      const uint32_t j = tid + jj * 1024;
+      if (j < nc) {
+        const uint32_t sb = S.sidx[j];
+        const uint32_t d = S.gb[sb] + (j - S.lst[sb]);
+        if (MOX_CHK(w, d < tc && kb + d < w.split_k_cap, CHK_SPLIT_K)) ok[d] = S.stage[j];
+      }
     }
-    __syncthreads();  // the stage is rewritten by the next chunk
+    lds_barrier();  // the stage is rewritten by the next chunk (LDS only: the stores need not land first)
   }
 }
 
@@ -3273,11 +3310,15 @@ __device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, cons
     // sort again on 64-bit keys -- the h32 bits below the unit, all of
     // hash32b, the index -- which is key_less order whenever (h32, hash32b)
     // differ
+    // (keys from the wave's LDS copy: the registers k[] are dead after the
+    // first pass, which keeps this rare path from setting the kernel's
+    // register peak)
     uint64_t v2[PER];
 #pragma unroll
     for (int s = 0; s < PER; s++) {
       const uint32_t i = (uint32_t)(s * 64 + lane);
-      const uint32_t h = hash32(k[s].x, k[s].y, k[s].z, k[s].w), hb = hash32b(k[s].x, k[s].y, k[s].z, k[s].w);
+      const uint4 ks = key[i < n ? i : 0u];
+      const uint32_t h = hash32(ks.x, ks.y, ks.z, ks.w), hb = hash32b(ks.x, ks.y, ks.z, ks.w);
       const uint64_t pre = ((uint64_t)(shift >= 32 ? 0u : (h << shift) >> shift) << (32 + IB)) | ((uint64_t)hb << IB);
       v2[s] = i < n ? (pre | i) : ~0ull;
     }
@@ -3362,14 +3403,22 @@ extern "C" __global__ __launch_bounds__(64 * S1_WAVES, MOX_S1_WG) void k_reduce_
       kk[s] = make_uint4(x.x, x.y, x.z, x.w);
     }
   };
+  // descriptors carry only the fields this kernel reads (7 of 10 dwords):
+  // three of them are live across the sort, and at 128 VGPRs the full ones
+  // spilled to scratch, whose reloads (vector memory) waited for every load
+  // and store in flight once per unit
+  auto slim = [&](uint32_t uu) {
+    const UnitDesc& x = w.udesc[uu < U ? uu : U - 1];
+    return UnitDesc{x.in_off, 0, x.rec_off, x.in_n, x.win_n, 0, x.kk};
+  };
   uint32_t u = blockIdx.x * S1_WAVES + wv;
   if (u >= U) return;
-  UnitDesc d = w.udesc[u];
-  UnitDesc dn = w.udesc[u + GW < U ? u + GW : U - 1];
+  UnitDesc d = slim(u);
+  UnitDesc dn = slim(u + GW);
   uint4 k[S1_PER];
   load_keys(d, ok_unit(d), k);
   for (; u < U; u += GW) {
-    const UnitDesc dnn = w.udesc[u + 2 * GW < U ? u + 2 * GW : U - 1];
+    const UnitDesc dnn = slim(u + 2 * GW);
     uint4 kn[S1_PER];
     load_keys(dn, u + GW < U && ok_unit(dn), kn);
     if (ok_unit(d)) sort_reduce_unit<S1_PER>(w, u, d, k, key, hp, lane);
