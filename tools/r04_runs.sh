@@ -25,6 +25,7 @@
 #            (tools/ab_kernel.sh; variants from tools/build_variant.sh)
 #   pmc      k_map FETCH/WRITE traffic at C2 (tools/pmc_traffic_wl.sh) and SQ
 #            counters of k_map and k_reduce (tools/pmc_sq.sh)
+#   lines    C4 and C5 bench lines, a C4 kernel trace + one pass's timeline
 #
 # Variants used by the round-4 A/Bs (tools/build_variant.sh NAME FLAGS; SRC= an
 # exported older commit for the "head"/"base" arms): ldr -DMOX_LD_BATCH=0,
@@ -88,6 +89,17 @@ pmc)
   bash tools/pmc_traffic_wl.sh C2 1073741824 ${2:-pmc}_traffic > $O/traffic.txt 2>&1; rc=$?; tail -5 $O/traffic.txt; step traffic $rc
   bash tools/pmc_sq.sh k_map ${2:-pmc}_sqmap > $O/sq_k_map.txt 2>&1; rc=$?; cat $O/sq_k_map.txt; step "sq k_map" $rc
   bash tools/pmc_sq.sh 'k_reduce$' ${2:-pmc}_sqred > $O/sq_k_reduce.txt 2>&1; rc=$?; cat $O/sq_k_reduce.txt; step "sq k_reduce" $rc
+  ;;
+lines)
+  # C4 / C5 bench lines (production build) and a C4 kernel trace + timeline
+  for wl in C4 C5; do
+    timeout -k 10 500 python -u bench.py --workload $wl --steps 5 --warmup 2 > $O/bench_$wl.json 2> $O/bench_$wl.err; step "bench $wl" $?
+    python3 -c "import json;d=json.loads(open('$O/bench_$wl.json').read().strip().splitlines()[-1]);print('$wl',d['value'],d['ms_per_step'],d['phases_ms'])"
+  done
+  timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4 -o run -- \
+    python3 bench.py --workload C4 --steps 3 --warmup 1 --no-cpu-baseline > $O/c4_under_rocprof.log 2>&1; step "rocprof C4" $?
+  python3 tools/trace_timeline.py $O/c4 > $O/c4_timeline.txt; step "timeline C4" $?
+  tail -1 $O/c4_timeline.txt
   ;;
 *)
   echo "unknown section $SEC"; exit 2
