@@ -81,6 +81,11 @@ def parse():
     return ap.parse_args()
 
 
+def progress(msg):
+    """A progress line on stderr (long runs keep writing, so a watchdog sees them alive)."""
+    print("[bench %s] %s" % (time.strftime("%H:%M:%S"), msg), file=sys.stderr, flush=True)
+
+
 def cpu_model():
     try:
         out = subprocess.run(["lscpu"], capture_output=True, timeout=20).stdout.decode()
@@ -106,7 +111,8 @@ def cpu_baseline(kind, seed, sample_bytes, runs=3):
         path = os.path.join(d, "shakes.txt")
         data.tofile(path)
         del data
-        for _ in range(max(1, runs)):
+        for i in range(max(1, runs)):
+            progress("cpu baseline run %d of %d (%d MiB)" % (i + 1, max(1, runs), sample_bytes >> 20))
             r = subprocess.run([exe, path, "--workdir", d, "--quiet", "--time"], capture_output=True, timeout=600)
             if r.returncode != 0:
                 return None
@@ -203,6 +209,7 @@ def main_group(a):
     shards, bufs = [], []
     for r in range(n):
         lo, hi, ob, oe, end = mdist.shard_range(total, n, r, per_rank=per_rank, halo=HALO)
+        progress("%s: generating shard %d of %d (%d MiB)" % (a.workload, r + 1, n, (hi - lo) >> 20))
         host = corpus.fill(kind, seed, lo, hi - lo)
         m = g.member(r)
         d = m.alloc(hi - lo)
@@ -222,7 +229,9 @@ def main_group(a):
             rows.append(g.stats())
         return time.perf_counter() - t0, rows
 
+    progress("shards in HBM; hash-order steps")
     el_hash, rows_hash = timed(base_flags)
+    progress("sorted-result steps")
     elapsed, rows = timed(base_flags | mox.MOX_F_SORT_BYTES)  # the value: sorted result inside the step
     last = rows[-1]
     t = g.fetch()  # bytewise order (sorted on GPU 0 by the last timed step)
@@ -318,10 +327,12 @@ def main():
     # stream ~5.6 us); one diagnostic step after the timed region has them all
     eng = mox.Engine(device=local if a.device < 0 else a.device, flags=base_flags | mox.MOX_F_TIMING_MAP,
                      sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
+    progress("%s: generating %d MiB of corpus" % (a.workload, (hi - lo) >> 20))
     host = corpus.fill(kind, seed, lo, hi - lo)
     d_buf = eng.alloc(hi - lo)
     eng.h2d(d_buf, host)
     del host
+    progress("corpus in HBM; %d warmup + %d timed steps" % (a.warmup, a.steps))
     if world > 1 and a.xport == "rccl":
         uid = mox.comm_unique_id() if rank == 0 else b""
         obj = [uid]
@@ -359,6 +370,7 @@ def main():
     for _ in range(a.warmup):
         step()
     eng.synchronize()  # completes (and checks) every queued pass
+    progress("warmup done")
     if dist:
         dist.barrier()
     map_ms, xms, gms = [], [], []
