@@ -29,6 +29,7 @@
 // byte loads made it the slowest kernel of the sort.)  The sorted table's
 // bytes leave through an LDS stage as aligned 16-byte stores (k_bs_out2).
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "mox_host.h"
@@ -596,6 +597,11 @@ int bsort_table(mox_engine* e) {
   const uint64_t n = r.n, nb = r.nb;
   if (n < 2) return MOX_OK;
   if (n >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: %llu words (at most 2^32 - 1)", (unsigned long long)n);
+  // MOX_BSORT_MAX_WORDS: the most words the device sort takes (a bigger table
+  // is sorted on the host, as when the sort's scratch does not fit)
+  if (const char* cap = getenv("MOX_BSORT_MAX_WORDS"))
+    if (n > strtoull(cap, nullptr, 10))
+      return fail(MOX_ENOMEM, "bytewise sort: %llu words, MOX_BSORT_MAX_WORDS=%s", (unsigned long long)n, cap);
   // (32-bit word offsets in the payload: a bigger table is sorted on the host, as on MOX_ENOMEM)
   if (nb >= (1ull << 32)) return fail(MOX_ENOMEM, "bytewise sort: %llu table bytes (device sort: < 4 GiB)", (unsigned long long)nb);
   hipStream_t st = e->stream;

@@ -225,3 +225,33 @@ def test_bench_multi_gpu_without_torchrun():
     assert line["n_gpus"] == 2 and line["value"] > 0 and line["check_sum_counts_eq_tokens"]
     mg = line["multi_gpu"]
     assert mg["mode"] == "engine group (one process)" and mg["all_to_all_bytes"] > 0 and mg["gathered_table"]["n"] > 0
+
+
+def test_group_sort_falls_back_to_the_host(monkeypatch):
+    """a gathered table the device sort cannot take (its scratch, or
+    MOX_BSORT_MAX_WORDS) is sorted on the host by mox_fetch_table, not lost."""
+    data = mixed(2 << 20, 91)
+    monkeypatch.setenv("MOX_BSORT_MAX_WORDS", "10")
+    g = group(2, flags=mox.MOX_F_SORT_BYTES)
+    try:
+        t = g.count(data)
+        got = list(t.items())
+        t.close()
+    finally:
+        g.close()
+    assert got == coracle.count(data)[0]
+
+
+def test_group_set_flags_reaches_every_member():
+    """mox_set_flags on a group applies to every member: with
+    MOX_F_TIMING_MAP set after creation, every member times its map kernel."""
+    data = mixed(2 << 20, 92)
+    g = group(2)
+    try:
+        g.set_flags(mox.MOX_F_TIMING_MAP)
+        t = g.count(data)
+        t.close()
+        assert all(g.member(i).stats()["ms_map"] > 0 for i in range(2))
+        assert g.stats()["ms_map"] > 0
+    finally:
+        g.close()
