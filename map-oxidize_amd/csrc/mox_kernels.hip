@@ -1818,7 +1818,7 @@ constexpr int RED_BK = 608;    // 2 workgroups per CU: table + sort scratch <= 8
 constexpr int RED_SLOTS = 4 * RED_BK;
 constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort width
 #ifndef MOX_RED_UNROLL
-#define MOX_RED_UNROLL 2
+#define MOX_RED_UNROLL 1  // 64-record chunks (round-4 A/B, profiles/r04/c2_k_reduce_depth_ab.txt)
 #endif
 constexpr int RED_UNROLL = MOX_RED_UNROLL;
 #ifndef MOX_RED_DYN
@@ -1828,7 +1828,10 @@ constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partit
 #ifndef MOX_RED_TAB
 #define MOX_RED_TAB 1  // k_reduce: ticket -> region table (0: binary search per ticket)
 #endif
-constexpr uint32_t RED_TICKET = 128 * MOX_RED_UNROLL;  // records per k_reduce ticket (two chunks)
+#ifndef MOX_RED_DEPTH
+#define MOX_RED_DEPTH 3  // k_reduce chunks per ticket: two chunks' loads in flight while one is inserted
+#endif
+constexpr uint32_t RED_TICKET = 64 * MOX_RED_UNROLL * MOX_RED_DEPTH;  // records per k_reduce ticket
 constexpr int RED_TAB_MAX = RED_SORTB;                  // ticket table entries (u16, in the fill space)
 
 struct RedLds {
@@ -2624,7 +2627,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         // the slowest wave ~25 us behind per partition at C2,
         // profiles/r03_k_reduce_stamps.txt: insert_tail)
         constexpr uint32_t SCH = RED_TICKET;
-        static_assert(RED_TICKET == 2 * CH, "a ticket is two chunks");
+        static_assert(RED_TICKET == MOX_RED_DEPTH * CH, "a ticket is MOX_RED_DEPTH chunks");
         const uint32_t a1 = n;
         auto grab = [&]() -> uint32_t {
           uint32_t v = 0;
@@ -2728,12 +2731,35 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
               if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
             RED_MARK(3);
           } else {
-            asm volatile("" ::"v"(h[0]), "v"(h[1]));
+#pragma unroll
+            for (int u2 = 0; u2 < RED_UNROLL; u2++) asm volatile("" ::"v"(h[u2]));
           }
         };
         uint32_t c = a0;
         uint4 A[RED_UNROLL], B[RED_UNROLL];
-#if MOX_RED_DYN
+#if MOX_RED_DYN && MOX_RED_DEPTH == 3
+        // tickets of three chunks [c, c + CH), [c + CH, c + 2 CH), [c + 2 CH,
+        // c + 3 CH): two chunks' loads in flight while one is inserted (the
+        // stream is bound by the bytes each wave keeps in flight)
+        uint4 C[RED_UNROLL];
+        if (c < a1) {
+          load(c, A);
+          load(c + CH, B);
+        }
+        while (c < a1) {
+          load(c + 2 * CH, C);
+          uint32_t tv = 0;
+          if (lane == 0) tv = atomicAdd(&s.misc[2], SCH);
+          process(A, c);
+          const uint32_t cn = __builtin_amdgcn_readfirstlane(tv);
+          seek(cn);
+          load(cn, A);
+          process(B, c + CH);
+          load(cn + CH, B);
+          process(C, c + 2 * CH);
+          c = cn;
+        }
+#elif MOX_RED_DYN
         // chunk pairs [c, c + CH), [c + CH, c + SCH) of one ticket, the next
         // ticket's first chunk in flight while the second is inserted
         if (c < a1) load(c, A);
