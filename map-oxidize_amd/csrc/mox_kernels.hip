@@ -3313,6 +3313,7 @@ __device__ __forceinline__ void sort_reduce_unit(const Work& w, uint32_t u, cons
     if (i < n) key[i] = k[s];
   }
   s1_sort<PER, uint32_t>(v, lane);
+  if (MOX_ABL(w.dbg, DBG_S1_SORT2)) s1_sort<PER, uint32_t>(v, lane);
   // run heads: hash bits differ from the previous position's
   uint32_t idx[PER];
   uint32_t hm = 0, bad = 0;

@@ -26,6 +26,10 @@
 #   pmc      k_map FETCH/WRITE traffic at C2 (tools/pmc_traffic_wl.sh) and SQ
 #            counters of k_map and k_reduce (tools/pmc_sq.sh)
 #   lines    C4 and C5 bench lines, a C4 kernel trace + one pass's timeline
+#   csort    a k_reduce_sort1 variant (AB_VAR, default cs = -DMOX_S1_CSORT=1 in the
+#            commit that had it) against the default build: tables identical
+#            (tools/cmp_order.py), parity tests with it, C4 per-kernel A/B, and the
+#            sort-twice ablation (DBG_S1_SORT2, builds abl / csabl)
 #
 # Variants used by the round-4 A/Bs (tools/build_variant.sh NAME FLAGS; SRC= an
 # exported older commit for the "head"/"base" arms): ldr -DMOX_LD_BATCH=0,
@@ -100,6 +104,17 @@ lines)
     python3 bench.py --workload C4 --steps 3 --warmup 1 --no-cpu-baseline > $O/c4_under_rocprof.log 2>&1; step "rocprof C4" $?
   python3 tools/trace_timeline.py $O/c4 > $O/c4_timeline.txt; step "timeline C4" $?
   tail -1 $O/c4_timeline.txt
+  ;;
+csort)
+  V=${AB_VAR:-cs}
+  timeout -k 10 300 python3 -u tools/cmp_order.py build/var_$V/libmox.so > $O/cmp_order.txt 2>&1; rc=$?; cat $O/cmp_order.txt; step "cmp order" $rc
+  MOX_LIB=build/var_$V/libmox.so timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 200 \
+    --timeout-method thread -m "gpu and not slow" -k "split or high_card or corpora or deterministic or fuzz or kats" > $O/par.log 2>&1
+  step "parity $(tail -1 $O/par.log)" $?
+  bash tools/ab_kernel.sh "def $V def $V" "0" "k_reduce_sort1 k_reduce_sort2" --workload C4 --steps 3 --warmup 1 --no-cpu-baseline \
+    > $O/ab.txt 2>&1; rc=$?; cat $O/ab.txt; step ab $rc
+  bash tools/ab_kernel.sh "abl ${V}abl" "0 65536" "k_reduce_sort1" --workload C4 --steps 3 --warmup 1 --no-cpu-baseline \
+    > $O/abl.txt 2>&1; rc=$?; cat $O/abl.txt; step abl $rc
   ;;
 *)
   echo "unknown section $SEC"; exit 2
