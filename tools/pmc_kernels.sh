@@ -5,9 +5,11 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 K=$1; TAG=${2:-pmck}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 i=0
-for grp in "SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY" \
-           "SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_BUSY_CYCLES,SQ_WAIT_INST_LDS,SQ_INST_CYCLES_VMEM" \
-           "FETCH_SIZE" "WRITE_SIZE,GRBM_GUI_ACTIVE"; do
+# PMC_GROUPS: space-separated counter groups instead of the four below
+CGROUPS=${PMC_GROUPS:-"SQ_WAVES,SQ_INSTS_VALU,SQ_INSTS_SALU,SQ_INSTS_LDS,SQ_WAVE_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY \
+SQ_INSTS_VMEM_RD,SQ_INSTS_VMEM_WR,SQ_LDS_BANK_CONFLICT,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_BUSY_CYCLES,SQ_WAIT_INST_LDS,SQ_INST_CYCLES_VMEM \
+FETCH_SIZE WRITE_SIZE,GRBM_GUI_ACTIVE"}
+for grp in $CGROUPS; do
   i=$((i+1))
   timeout -s KILL 150 rocprofv3 --pmc $grp --kernel-include-regex "$K" --output-format csv -d $OUT/p$i -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit $rc; }

@@ -26,6 +26,7 @@
 #   pmc      k_map FETCH/WRITE traffic at C2 (tools/pmc_traffic_wl.sh) and SQ
 #            counters of k_map and k_reduce (tools/pmc_sq.sh)
 #   lines    C4 and C5 bench lines, a C4 kernel trace + one pass's timeline
+#   c4pmc    C4 FETCH_SIZE / WRITE_SIZE per kernel: k_map and the post-map kernels
 #   csort    a k_reduce_sort1 variant (AB_VAR, default cs = -DMOX_S1_CSORT=1 in the
 #            commit that had it) against the default build: tables identical
 #            (tools/cmp_order.py), parity tests with it, C4 per-kernel A/B, and the
@@ -104,6 +105,12 @@ lines)
     python3 bench.py --workload C4 --steps 3 --warmup 1 --no-cpu-baseline > $O/c4_under_rocprof.log 2>&1; step "rocprof C4" $?
   python3 tools/trace_timeline.py $O/c4 > $O/c4_timeline.txt; step "timeline C4" $?
   tail -1 $O/c4_timeline.txt
+  ;;
+c4pmc)
+  # C4 per-kernel HBM traffic (FETCH_SIZE, WRITE_SIZE passes) of k_map and the post-map kernels
+  BENCH_ARGS="--workload C4" PMC_GROUPS="FETCH_SIZE WRITE_SIZE,GRBM_GUI_ACTIVE" \
+    bash tools/pmc_kernels.sh 'k_map|k_split_count|k_split_scatter|k_reduce_sort1|k_reduce_sort2|k_mat' ${2:-c4pmc}_k \
+    > $O/pmc.txt 2>&1; rc=$?; cat $O/pmc.txt; step "c4 pmc" $rc
   ;;
 csort)
   V=${AB_VAR:-cs}
