@@ -232,7 +232,7 @@ int alloc_fixed(mox_engine* e) {
   return MOX_OK;
 }
 
-constexpr size_t map_lds_bytes() { return DICT_SLOTS * (16 + 4) + NB * 4 + 16 + 17 * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
+constexpr size_t map_lds_bytes() { return DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
 static_assert(map_lds_bytes() <= 160 * 1024, "k_map LDS over 160 KiB");
 size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
 

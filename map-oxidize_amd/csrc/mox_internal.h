@@ -47,6 +47,7 @@ constexpr int TOKMAX = ROW / 2;             // token starts per row (at most eve
 // them.  Slot = 64 lanes x 16 B = [16 B before | PAY payload bytes | 16 B after].
 constexpr int SLOT = ROW;
 constexpr int PAY = ROW - 32;               // 992 payload bytes per row
+constexpr int KSEL_N = 17 * 4;              // k_map key selectors: key length 0..16 x byte offset 0..3
 #ifndef MOX_LD_GROUPS
 #define MOX_LD_GROUPS 4  // 3: k_map +2.5-4 % on C2 (interleaved A/B)
 #endif

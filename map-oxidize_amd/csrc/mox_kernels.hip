@@ -309,7 +309,7 @@ struct MapLds {
   uint32_t* dcnt;   // DICT_SLOTS
   uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's space)
   uint32_t* misc;   // [0] spills [1] row ticket
-  uint4* masktab;   // [17]: byte masks keeping the first len bytes of a 16-byte key
+  uint4* seltab;    // [KSEL_N]: v_perm selectors of a len-byte key at byte offset sh (entry 4 len + sh)
   // no dictionary (dict_n == 0): pair slots per region, inside dkey's space
   uint4* pend;      // NB x qf parked records
   uint32_t* pst;    // NB x qf slot states (PS_*)
@@ -633,7 +633,7 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
 }
 
 // Key of list entry e from the lowered slot: 20 bytes read at the 4-aligned
-// start, byte-aligned with v_alignbyte, masked to len bytes.  Split in two so
+// start, aligned and masked to len bytes by v_perm_b32 (seltab).  Split in two so
 // that a token pass can issue the LDS reads of all its batches before it uses
 // any of them (key_load for every batch, a scheduling barrier, then key_make):
 // left alone, the scheduler waited for each batch's reads before issuing the
@@ -643,24 +643,23 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
 // is needed (k_map -2.4 % against 24 bytes at the 8-aligned start).
 struct KeyLd {
   uint32_t E[5];
-  uint4 M;
+  uint4 S;  // v_perm selectors: alignment and length mask in one (seltab)
 };
 __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf, uint32_t e, KeyLd& r) {
   const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
   const uint32_t* q = reinterpret_cast<const uint32_t*>(rowbuf + (pos & ~3u));
 #pragma unroll
   for (int i = 0; i < 5; i++) r.E[i] = q[i];
-  r.M = s.masktab[len];
+  r.S = s.seltab[4 * len + (pos & 3u)];
 }
 __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
-  const uint32_t pos = e & 1023u;
-  const uint4 M = r.M;
-  const uint32_t E0 = r.E[0], E1 = r.E[1], E2 = r.E[2], E3 = r.E[3], E4 = r.E[4];
-  const uint32_t sh = pos & 3u;
-  K[0] = __builtin_amdgcn_alignbyte(E1, E0, sh) & M.x;
-  K[1] = __builtin_amdgcn_alignbyte(E2, E1, sh) & M.y;
-  K[2] = __builtin_amdgcn_alignbyte(E3, E2, sh) & M.z;
-  K[3] = __builtin_amdgcn_alignbyte(E4, E3, sh) & M.w;
+  (void)e;
+  // byte 4 d + j of the key = byte S.d[j] of (E[d + 1]:E[d]) (0x0C: zero): one
+  // v_perm_b32 per dword aligns and masks at once
+  K[0] = __builtin_amdgcn_perm(r.E[1], r.E[0], r.S.x);
+  K[1] = __builtin_amdgcn_perm(r.E[2], r.E[1], r.S.y);
+  K[2] = __builtin_amdgcn_perm(r.E[3], r.E[2], r.S.z);
+  K[3] = __builtin_amdgcn_perm(r.E[4], r.E[3], r.S.w);
 }
 // The rare paths of a row (byte-wise walks, Unicode checks) load from global
 // memory.  Left pending where they rejoin the common path, their destination
@@ -967,7 +966,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
   m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
-  m.s.masktab = (uint4*)sp; sp += 17 * 16;
+  m.s.seltab = (uint4*)sp; sp += KSEL_N * 16;
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
@@ -997,14 +996,16 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   }
   if (tid < 4) m.s.misc[tid] = (resume && tid == 0) ? w.spill_n[blockIdx.x] : 0u;
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
-  if (tid < 17) {
-    uint32_t mk[4];
+  if (tid < KSEL_N) {  // key byte 4 d + j = window byte sh + 4 d + j, or 0 past len (v_perm selector 0x0C)
+    const uint32_t len = (uint32_t)tid >> 2, sh = (uint32_t)tid & 3u;
+    uint32_t sel[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-      const int c = tid - 4 * i;  // bytes kept in dword i
-      mk[i] = c <= 0 ? 0u : (c >= 4 ? ~0u : ((1u << (8 * c)) - 1u));
+    for (int d = 0; d < 4; d++) {
+      sel[d] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) sel[d] |= ((uint32_t)(4 * d + j) < len ? sh + (uint32_t)j : 0x0Cu) << (8 * j);
     }
-    m.s.masktab[tid] = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+    m.s.seltab[tid] = make_uint4(sel[0], sel[1], sel[2], sel[3]);
   }
   __syncthreads();
   unsigned long long ntok = 0;
