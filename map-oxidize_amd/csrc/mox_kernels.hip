@@ -246,10 +246,8 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 // dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
 // bits.  Final table order is (h32, hash32b, key) (key_less), so it is deterministic.
 __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t a;  // 3-input xor in one v_bitop3_b32 (0x96)
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96"
-      : "=v"(a)
-      : "v"(k0), "v"(__builtin_rotateleft32(k1, 11)), "v"(__builtin_rotateleft32(k2, 21)));
+  // 3-input xor in one v_bitop3_b32 (0x96)
+  uint32_t a = __builtin_amdgcn_bitop3_b32(k0, __builtin_rotateleft32(k1, 11), __builtin_rotateleft32(k2, 21), 0x96);
   a ^= __builtin_rotateleft32(k3, 6);
   a *= 0x9E3779B1u;
   a ^= a >> 15;
@@ -692,14 +690,15 @@ __device__ __forceinline__ void after_fence(uint32_t (&v)[TU]) {
 #define AFTER_FENCE(v) after_fence(v)
 
 // 16-byte key equality as one OR of XORs, each (a ^ b) | c step one
-// v_bitop3_b32 (truth table 0xBE: src0 0xF0, src1 0xCC, src2 0xAA); kept opaque:
-// the combiner would otherwise split it into four compares and a boolean tree
+// v_bitop3_b32 (truth table 0xBE: src0 0xF0, src1 0xCC, src2 0xAA).  The
+// builtin keeps the combiner from splitting it into four compares and a
+// boolean tree, and (unlike inline asm, which it replaces) lets the scheduler
+// interleave the chains without a wait state after every step.
 __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
-  uint32_t d;
-  asm("v_xor_b32 %0, %1, %2" : "=v"(d) : "v"(k.x), "v"(K[0]));
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xbe" : "=v"(d) : "v"(k.y), "v"(K[1]), "v"(d));
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xbe" : "=v"(d) : "v"(k.z), "v"(K[2]), "v"(d));
-  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xbe" : "=v"(d) : "v"(k.w), "v"(K[3]), "v"(d));
+  uint32_t d = k.x ^ K[0];
+  d = __builtin_amdgcn_bitop3_b32(k.y, K[1], d, 0xBE);
+  d = __builtin_amdgcn_bitop3_b32(k.z, K[2], d, 0xBE);
+  d = __builtin_amdgcn_bitop3_b32(k.w, K[3], d, 0xBE);
   return d == 0;
 }
 
