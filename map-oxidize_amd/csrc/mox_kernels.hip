@@ -828,17 +828,24 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   if (!slow) {
     // per dword (ASCII bytes, no carries between bytes): whitespace = byte < 33
     // and (byte == 32 or 9 <= byte <= 13); ctl = other bytes < 33 (NUL included)
-    uint32_t ws16 = 0, ctl = 0;
+    uint32_t ws16, ctl = 0;
     {
       const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
+      uint32_t wsd[4];
 #pragma unroll
       for (int d = 0; d < 4; d++) {
         const uint32_t x = ad[d];
         const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
-        const uint32_t wsd = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
-        ctl |= lt33 & ~wsd;
-        ws16 |= (((wsd >> 7) | (wsd >> 14) | (wsd >> 21) | (wsd >> 28)) & 0xFu) << (4 * d);
+        wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
+        ctl |= lt33 & ~wsd[d];
       }
+      // the 16 byte flags (bit 7 of every byte) into bits 0..15: two dwords'
+      // flags interleave at bits 8 k and 8 k + 4, three shifted copies move
+      // bytes 1..3's into bits 1..3 / 5..7, and v_perm joins the two low bytes
+      uint32_t lo = (wsd[0] >> 7) | (wsd[1] >> 3), hi = (wsd[2] >> 7) | (wsd[3] >> 3);
+      lo |= (lo >> 7) | (lo >> 14) | (lo >> 21);
+      hi |= (hi >> 7) | (hi >> 14) | (hi >> 21);
+      ws16 = __builtin_amdgcn_perm(hi, lo, 0x0C0C0400u);
     }
     const uint32_t wsn = from_next_lane(ws16);
     const uint32_t wsp = from_prev_lane(ws16);
