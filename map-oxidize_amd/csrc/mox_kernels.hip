@@ -817,7 +817,7 @@ struct Cyc {
 //  2. token phase (lane = token): pass_a over all tokens (both dictionary slots
 //     read at once: an LDS count on a hit, the cold store on a miss).
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
-                                       uint16_t* list, struct Cyc* cyc) {
+                                       uint16_t* list, struct Cyc* cyc, bool edge) {
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
   const bool ctx = lane == 0 || lane == 63;
@@ -852,7 +852,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     ws32 = ws16 | (wsn << 16);
     start = (~ws32) & ((ws32 << 1) | ((wsp >> 15) & 1u)) & 0xFFFFu;
     if (ctx) start = 0;
-    if (sbase + 16 < m.c.own_lo || sbase + ROW - 16 > m.c.own_hi) {
+    if (edge && (sbase + 16 < m.c.own_lo || sbase + ROW - 16 > m.c.own_hi)) {  // edge: k_map's edge rows
       if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
       if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
     }
@@ -861,8 +861,11 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       const uint32_t z16 = zero_mask16(a);
       z32 = z16 | (from_next_lane(z16) << 16);
     }
-    const bool near_end = !m.c.at_end && sbase + ROW + 32 >= m.c.hi;
-    if (near_end) lim = m.c.hi > p0 ? (uint32_t)(m.c.hi - p0 < 64 ? m.c.hi - p0 : 64) : 0u;
+    bool near_end = false;
+    if (__builtin_expect(edge, 0)) {  // (a uniform branch: the look-ahead limit only in edge rows)
+      near_end = !m.c.at_end && sbase + ROW + 32 >= m.c.hi;
+      if (near_end) lim = m.c.hi > p0 ? (uint32_t)(m.c.hi - p0 < 64 ? m.c.hi - p0 : 64) : 0u;
+    }
     chk = anyz || near_end;
   } else {
     start = ctx ? 0u : slow_starts(m, p0);
@@ -1107,6 +1110,16 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   } else {
     // ---------------- consumers
     uint16_t* list = lists + (wv - MAP_LOADERS) * TOKMAX;
+    // Edge rows: only they can reach a buffer or ownership bound.  Row r's slot
+    // starts at base0 + r PAY - 16 and nrows PAY covers own_hi - base0, so every
+    // row r >= 1 starts past lo and own_lo, and every row r <= nrows - 3 ends
+    // ~2 rows before own_hi <= hi.  With a row of margin on each side, the other
+    // rows skip the 64-bit range checks (two uniform 32-bit compares instead of
+    // ~20 VALU instructions per row); a launch whose nrows does not cover its
+    // range makes every row an edge row.
+    uint32_t e_lo = rb < 2 ? (uint32_t)(2 - rb) : 0u;
+    const uint32_t e_hi = nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u;
+    if (c.own_hi > base0 && nrows * PAY < c.own_hi - base0) e_lo = n;
 #ifdef MOX_STAMP
     Cyc cyc{0, 0, 0, 0, 0, 0};
     Cyc* cp = &cyc;
@@ -1126,9 +1139,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       uint8_t* sl = ring + slot * SLOT;
       const uint64_t sbase = base0 + (rb + u) * PAY - 16;
       uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
-      if (sbase < c.lo || sbase + SLOT > c.hi) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
+      const bool edge = u < e_lo || u >= e_hi;
+      if (edge && (sbase < c.lo || sbase + SLOT > c.hi)) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
       if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
-      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp);
+      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge);
       else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
