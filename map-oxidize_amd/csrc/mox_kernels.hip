@@ -630,6 +630,11 @@ __device__ uint32_t slow_starts(const MapCtx& m, uint64_t p0) {
   return st;
 }
 
+// Token list entry (u16): slot offset (bits 0..9) + 1024 x length, or bit 15
+// set.  An entry is odd -- a token the generic walk takes -- when it is at or
+// above LIST_ODD: its length field is over 16 (the common-row list builder
+// stores any length there and lets this test flag it), or bit 15 is set.
+constexpr uint32_t LIST_ODD = 17u << 10;
 // Key of list entry e from the lowered slot: 20 bytes read at the 4-aligned
 // start, aligned and masked to len bytes by v_perm_b32 (seltab).  Split in two so
 // that a token pass can issue the LDS reads of all its batches before it uses
@@ -744,7 +749,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
   uint32_t pos[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    const bool valid = !(e[u] & 0x8000u);
+    const bool valid = e[u] < LIST_ODD;
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
     miss[u] = valid & !(hit1 | hit2);
     if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[hit1 ? s1[u] : s2[u]], 1u);
@@ -795,7 +800,7 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
   for (int u = 0; u < TU; u++) key_make(e[u], ld[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    if (e[u] & 0x8000u) continue;
+    if (e[u] >= LIST_ODD) continue;
     const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
     cold_word(m, hash32(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1);
   }
@@ -879,7 +884,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   const uint32_t pre = incl - cnt, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return;
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
-  // list entry (u16): slot offset (10 bits) | length (5 bits, <= 16) | odd (bit 15)
+  // list entries: see LIST_ODD
   uint32_t k = pre;
   bool any_odd = false;
   if (!chk && !slow) {
@@ -904,7 +909,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       const uint32_t p = ffbl(st);  // ~0 once the lane has run out of starts
       st &= st - 1;
       const uint32_t len = ffbl(ws32 >> (p & 31u));
-      *(it < cnt ? mine + it : sink) = (uint16_t)(lbase + p + (len > 16 ? 0x8000u : (len << 10)));
+      // len > 16 (or no whitespace in the window: ffbl ~0) lands at or above LIST_ODD by itself
+      *(it < cnt ? mine + it : sink) = (uint16_t)(lbase + p + (len << 10));
     }
   } else {
     while (start) {
@@ -922,7 +928,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
     for (uint32_t j = lane; j < total; j += 64) {
       const uint32_t e = list[j];
-      if (e & 0x8000u) generic_token(m, sbase + (e & 1023u));
+      if (e >= LIST_ODD) generic_token(m, sbase + (e & 1023u));
     }
     vm_settle();
   }
