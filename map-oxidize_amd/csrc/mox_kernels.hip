@@ -653,7 +653,8 @@ __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf,
   const uint32_t* q = reinterpret_cast<const uint32_t*>(rowbuf + (pos & ~3u));
 #pragma unroll
   for (int i = 0; i < 5; i++) r.E[i] = q[i];
-  r.S = s.seltab[4 * len + (pos & 3u)];
+  r.S = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s.seltab) + (((e >> 4) & 0x7C0u) | ((pos & 3u) << 4)));
+  (void)len;  // (entry 4 len + (pos & 3), as a byte offset straight from the list entry)
 }
 __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
   (void)e;
@@ -977,11 +978,13 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.wk = (KWork)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
                  ((sizeof(Corpus) + alignof(Work) - 1) & ~(alignof(Work) - 1)));
   uint8_t* sp = smem;
-  m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
+  // the arrays the token pass indexes per token first: their offsets fit the
+  // LDS instructions' 16-bit offset field, so no address add per access
   m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
   m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
   m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
   m.s.seltab = (uint4*)sp; sp += KSEL_N * 16;
+  m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
@@ -1124,7 +1127,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     // ~20 VALU instructions per row); a launch whose nrows does not cover its
     // range makes every row an edge row.
     uint32_t e_lo = rb < 2 ? (uint32_t)(2 - rb) : 0u;
-    const uint32_t e_hi = nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u;
+    const uint32_t e_hi = __builtin_amdgcn_readfirstlane(nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u);
     if (c.own_hi > base0 && nrows * PAY < c.own_hi - base0) e_lo = n;
 #ifdef MOX_STAMP
     Cyc cyc{0, 0, 0, 0, 0, 0};
