@@ -554,10 +554,13 @@ __device__ __forceinline__ uint32_t zero_mask16(uint4 v) {
   const uint64_t l = ((uint64_t)v.y << 32) | v.x, h = ((uint64_t)v.w << 32) | v.z;
   return movemask8(zero_bytes80(l)) | (movemask8(zero_bytes80(h)) << 8);
 }
-__device__ __forceinline__ uint4 lower16(uint4 v) {
-  const uint64_t l = lower_ascii(((uint64_t)v.y << 32) | v.x), h = lower_ascii(((uint64_t)v.w << 32) | v.z);
-  return make_uint4((uint32_t)l, (uint32_t)(l >> 32), (uint32_t)h, (uint32_t)(h >> 32));
+// ASCII lowercase of 4 bytes < 0x80 (no carries between bytes), in 32-bit
+// operations: the 64-bit form's constant pairs were held in SGPRs across the
+// k_map row loop and spilled (a VGPR-lane reload and write-back per row)
+__device__ __forceinline__ uint32_t lower4(uint32_t x) {
+  return x | ((((x + 0x3F3F3F3Fu) & ~(x + 0x25252525u)) & 0x80808080u) >> 2);
 }
+__device__ __forceinline__ uint4 lower16(uint4 v) { return make_uint4(lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w)); }
 // Whole-wave lane shifts by one on the VALU (DPP wave_shl:1 / wave_shr:1; gfx9
 // family), instead of ds_bpermute through the LDS crossbar.  Lane 63 (next) and
 // lane 0 (prev) get 0.
@@ -826,7 +829,10 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
                                        uint16_t* list, struct Cyc* cyc, bool edge) {
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
-  const bool ctx = lane == 0 || lane == 63;
+  // lanes 0 and 63 are context only: their starts are cleared with a per-lane
+  // mask (a loop-invariant VGPR; as a lane-mask bool it took an SGPR pair)
+  const uint32_t keep = (uint32_t)(lane - 1) < 62u ? 0xFFFFFFFFu : 0u;
+  const bool ctx = keep == 0;
   const bool slow = __any(nonascii16(a) != 0);
   uint32_t ws32 = 0, z32 = 0, start;
   bool chk = false;  // rows with NUL bytes or near a non-final buffer end need the odd checks
@@ -857,7 +863,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     const uint32_t wsp = from_prev_lane(ws16);
     ws32 = ws16 | (wsn << 16);
     start = (~ws32) & ((ws32 << 1) | ((wsp >> 15) & 1u)) & 0xFFFFu;
-    if (ctx) start = 0;
+    start &= keep;
     if (edge && (sbase + 16 < m.c.own_lo || sbase + ROW - 16 > m.c.own_hi)) {  // edge: k_map's edge rows
       if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
       if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
