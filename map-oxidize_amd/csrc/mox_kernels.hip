@@ -322,10 +322,13 @@ struct MapCtx {
   uint32_t dict_n;
   uint32_t qf, qb;   // regions per partition (QF, 1 with a dictionary) and log2(qf)
   uint32_t rg, rc;   // regions per partition over the grid (qf map_grid), records per region (cold_cap / qf)
+  uint4* wcold;      // this workgroup's first region (q = 0, b = 0): cold + blockIdx qf NB rc
 };
-// This workgroup's region q of partition b.
-__device__ __forceinline__ uint4* region_of(const MapCtx& m, uint32_t b, uint32_t q) {
-  return m.w.cold + ((uint64_t)(blockIdx.x * m.qf + q) * NB + b) * m.rc;
+// Record pos of this workgroup's region q of partition b: one 64-bit
+// multiply-add and one address add from the workgroup's region base (the
+// full region index needed four more instructions per cold store)
+__device__ __forceinline__ uint4* cold_at(const MapCtx& m, uint32_t b, uint32_t q, uint32_t pos) {
+  return m.wcold + ((uint64_t)(q * NB + b) * m.rc + pos);
 }
 // Work fields of the rare paths (spills, Unicode lane, long words, error
 // flags), loaded where they are used: the opaque pointer keeps the compiler from
@@ -438,7 +441,7 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
             note_sample(m, b, qr, pos + 1, h);
           }
           if (pos + 1 < m.rc) {
-            uint4* o = region_of(m, b, qr) + pos;
+            uint4* o = cold_at(m, b, qr, pos);
             o[0] = q;
             o[1] = key;
           } else {
@@ -461,14 +464,14 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
     const uint32_t B = h >> (32 - NB_LOG2 - m.qb), qr = B & (m.qf - 1);
     const uint32_t pos = atomicAdd(&m.s.bcnt[B], 1u);
     if (pos < SPLIT_PER_REGION) note_sample(m, b, qr, pos, h);
-    if (pos < m.rc) region_of(m, b, qr)[pos] = key;
+    if (pos < m.rc) *cold_at(m, b, qr, pos) = key;
     else cold_spill(m, key);
     return;
   }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
   if (pos < SPLIT_PER_REGION) note_sample(m, b, 0, pos, h);
   if (pos < m.rc) {
-    region_of(m, b, 0)[pos] = key;
+    *cold_at(m, b, 0, pos) = key;
     return;
   }
   cold_spill(m, key);
@@ -774,7 +777,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     const uint32_t b = bucket_of(h[u]);
     const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
     if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, 0, pos[u], h[u]);
-    if (pos[u] < m.rc) region_of(m, b, 0)[pos[u]] = key;
+    if (pos[u] < m.rc) *cold_at(m, b, 0, pos[u]) = key;
     else cold_spill(m, key);
   }
 }
@@ -1006,6 +1009,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.qb = m.qf == 4u ? 2u : (m.qf == 2u ? 1u : 0u);
   m.rg = w.map_grid * m.qf;
   m.rc = w.cold_cap / m.qf;
+  m.wcold = w.cold + (uint64_t)blockIdx.x * m.qf * NB * m.rc;
   if (!m.dict_n) m.s.bcnt = m.s.dcnt;  // NB x qf region counters
   // without a dictionary the key array is zero (no real key is zero, so nothing
   // would hit; that case takes pass_c, and the pair slots live there)
@@ -1178,7 +1182,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       const uint32_t pos = atomicAdd(&m.s.bcnt[i], 1u);
       const uint4 q = m.s.pend[i];
       note_sample(m, b, qr, pos, hash32(q.x, q.y, q.z, q.w));
-      if (pos < m.rc) region_of(m, b, qr)[pos] = q;
+      if (pos < m.rc) *cold_at(m, b, qr, pos) = q;
       else cold_spill(m, q);
     }
     __syncthreads();
