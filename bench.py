@@ -222,11 +222,13 @@ def main_group(a):
         g.set_flags(flags)
         for _ in range(a.warmup):
             g.run_shards(shards)
+        g.synchronize()
         rows = []
         t0 = time.perf_counter()
         for _ in range(a.steps):
             g.run_shards(shards)  # synchronous: returns with the gathered table on GPU 0
             rows.append(g.stats())
+        g.synchronize()  # member 0's stream drained: the last step's sort / gather tail is inside the clock
         return time.perf_counter() - t0, rows
 
     progress("shards in HBM; hash-order steps")
@@ -401,6 +403,26 @@ def main():
         if dist:
             dist.barrier()
         el_hash = time.perf_counter() - t1
+    sorted_result = None
+    if world == 1:
+        # like-for-like with the N > 1 line (whose step ends in the bytewise
+        # sort of the gathered table): the same K steps, each a synchronous pass
+        # followed by the device bytewise sort of its table (mox_sort_result)
+        eng.synchronize()
+        sort_ms = []
+        t1 = time.perf_counter()
+        for i in range(a.steps):
+            step(sync=True)
+            eng.sort_result()
+            sort_ms.append(eng.stats()["ms_sort"])
+        eng.synchronize()
+        el_sorted = time.perf_counter() - t1
+        sorted_result = {"value": round(total / (el_sorted / a.steps) / 1e9, 3),
+                         "ms_per_step": round(el_sorted / a.steps * 1e3, 4),
+                         "sort_bytes_ms": round(statistics.mean(sort_ms), 4),
+                         "note": "the same K steps as synchronous passes, each followed by the device bytewise "
+                                 "sort of its table (mox_sort_result): the work of the N > 1 step's sorted "
+                                 "result on one GPU"}
     eng.set_flags(base_flags | mox.MOX_F_TIMING)  # untimed diagnostic step: per-phase events
     step(sync=True)
     eng.synchronize()
@@ -493,6 +515,7 @@ def main():
                                            "unicode_tokens", "long_tokens", "chunks", "max_subpasses", "retries",
                                            "reduce_units", "split_partitions")},
             "multi_gpu": xinfo,
+            "sorted_result": sorted_result,
             "check_sum_counts_eq_tokens": ok,
             "cpu_baseline": None,
         }

@@ -56,6 +56,8 @@ constexpr int SCAN_T = 1024, SCAN_PER = 8, SCAN_TILE = SCAN_T * SCAN_PER;
 // look-back status word of (tile, digit): flag in bits 63..62, count below
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_VAL = (1ull << 62) - 1;
 constexpr uint32_t OS_SPIN_MAX = 1u << 22;       // a look-back that waits longer reports a failure (never expected)
+constexpr uint64_t TICK_BYTES = 64;              // k_os_pass tile tickets (OS_DIGITS words), zeroed with the status words
+static_assert(OS_DIGITS * 4 <= (int)TICK_BYTES, "one ticket per digit pass");
 
 __device__ __forceinline__ uint32_t digit_of(const BRec& r, int d) {
   if (d < 8) return (uint32_t)(r.key >> (8 * d)) & 0xFFu;
@@ -149,20 +151,27 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const unsigned long
   }
 }
 
-// One onesweep pass: records in -> out, stably ordered by digit d.  Tile =
-// blockIdx.x (tiles are dispatched in order, so every tile a look-back waits
-// on has been dispatched before it: the wait ends).  status[tile * 256 + v]
-// is zero at launch.
+// One onesweep pass: records in -> out, stably ordered by digit d.  The tile
+// index comes from a ticket (*tick, zero at launch) taken when the workgroup
+// starts, not from blockIdx.x: every tile a look-back waits on has then
+// already started and publishes without waiting on later tiles, whatever
+// order the hardware dispatches workgroups in.  status[tile * 256 + v] is
+// zero at launch.
 extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass(const BRec* __restrict__ in, BRec* __restrict__ out,
                                                                        uint64_t n, int d, const uint64_t* __restrict__ gs,
-                                                                       uint64_t* status, unsigned int* err) {
+                                                                       uint64_t* status, unsigned int* err,
+                                                                       unsigned int* tick) {
   __shared__ __attribute__((aligned(16))) BRec stage[OS_TILE];
   __shared__ uint32_t wcnt[OS_WAVES][256];  // per-wave digit counters, then per-wave offsets inside the digit
   __shared__ uint32_t lstart[256];          // first tile position of each digit
   __shared__ uint64_t gbase[256];           // first output position of this tile's records of each digit
   __shared__ uint32_t ws[OS_WAVES];
+  __shared__ uint32_t s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const uint64_t t0 = (uint64_t)blockIdx.x * OS_TILE;
+  if (tid == 0) s_tile = atomicAdd(tick, 1u);
+  __syncthreads();
+  const uint32_t tile = s_tile;
+  const uint64_t t0 = (uint64_t)tile * OS_TILE;
   const uint32_t tn = (uint32_t)(n - t0 < (uint64_t)OS_TILE ? n - t0 : (uint64_t)OS_TILE);
   for (int w = 0; w < OS_WAVES; w++) wcnt[w][tid] = 0;
   // records of wave wv: tile positions wv * 64 ITEMS + i * 64 + lane (input order = (wv, i, lane))
@@ -221,9 +230,9 @@ extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass
   }
   // decoupled look-back: publish the tile's count, sum the counts of the
   // tiles before it back to the first inclusive prefix, publish that
-  uint64_t* st = status + (uint64_t)blockIdx.x * 256 + tid;
+  uint64_t* st = status + (uint64_t)tile * 256 + tid;
   uint64_t sum = 0;
-  if (blockIdx.x == 0) {
+  if (tile == 0) {
     st_agent(st, ST_INC | cnt);
   } else {
     st_agent(st, ST_AGG | cnt);
@@ -545,6 +554,7 @@ struct BSort {
   uint64_t* gs;               // ... their exclusive scans
   uint64_t* status;           // look-back status words: 256 per tile, one region per digit pass
   unsigned int* err;          // look-back timeout flag
+  unsigned int* tick;         // OS_DIGITS tile tickets (one per digit pass), just below status
   unsigned long long* h_gh;   // pinned host copy of gh
 };
 
@@ -560,15 +570,15 @@ int radix_sort(mox_engine* e, BSort& s, uint64_t n, int nd) {
   HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, (size_t)nd * 256 * 8, hipMemcpyDeviceToHost, st));
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   if (ntiles > 0x7FFFFFFFull) return fail(MOX_EINVAL, "bytewise sort: too many tiles");
-  // zero status words for every pass at once (a region per digit)
-  HIPCHK(hipMemsetAsync(s.status, 0, (size_t)nd * ntiles * 256 * 8, st));
+  // zero the tile tickets and the status words of every pass at once (a region per digit)
+  HIPCHK(hipMemsetAsync(s.tick, 0, TICK_BYTES + (size_t)nd * ntiles * 256 * 8, st));
   HIPCHK(hipStreamSynchronize(st));
   for (int d = 0; d < nd; d++) {
     bool uniform = false;
     for (int v = 0; v < 256; v++) uniform |= s.h_gh[d * 256 + v] == n;
     if (uniform) continue;  // every record has the same digit: the order stays
     hipLaunchKernelGGL(k_os_pass, dim3((uint32_t)ntiles), dim3(OS_THREADS), 0, st, (const BRec*)s.a, s.b, n, d,
-                       (const uint64_t*)s.gs, s.status + (size_t)d * ntiles * 256, s.err);
+                       (const uint64_t*)s.gs, s.status + (size_t)d * ntiles * 256, s.err, s.tick + d);
     HIPCHK(hipGetLastError());
     std::swap(s.a, s.b);
   }
@@ -609,7 +619,7 @@ int bsort_table(mox_engine* e) {
   // scratch: records A, B, subset S, payload | run flags, positions | status | gh, gs | scan sums | totals, err
   const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
   const unsigned int lrun_cap = (unsigned int)std::min<uint64_t>(1u << 20, n / 4 + 16);  // k_bs_longsort's run list
-  const uint64_t need = 4 * rec + 2 * u64n + 8ull * lrun_cap + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
+  const uint64_t need = 4 * rec + 2 * u64n + 8ull * lrun_cap + TICK_BYTES + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
   int rc;
   if ((rc = grow_dev(e->s_tmp, need)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
       (rc = grow_dev(e->s_bytes, nb + 64)))
@@ -624,6 +634,7 @@ int bsort_table(mox_engine* e) {
   uint64_t* pos = (uint64_t*)q; q += u64n;
   uint2* lrun = (uint2*)q; q += 8ull * lrun_cap;
   BSort s;
+  s.tick = (unsigned int*)q; q += TICK_BYTES;
   s.status = (uint64_t*)q; q += stb;
   s.gh = (unsigned long long*)q; q += OS_DIGITS * 256 * 8;
   s.gs = (uint64_t*)q; q += OS_DIGITS * 256 * 8;
@@ -689,6 +700,9 @@ int bsort_table(mox_engine* e) {
   r.offs = oo;
   r.bytes = (const uint8_t*)e->s_bytes.p;
   r.sorted = true;
+  // complete: the callers time the sort on the host clock (ms_sort), so the
+  // output kernels above must be inside it
+  HIPCHK(hipStreamSynchronize(st));
   return MOX_OK;
 }
 

@@ -2157,9 +2157,12 @@ __device__ __forceinline__ void split_count(const Work& w) {
   // sample = the first SPLIT_PER_REGION cold records of every map workgroup's
   // region (spread over the whole corpus; their key hashes, noted by k_map),
   // topped up with weighted records
-  const uint32_t G = reg_grid(w);
-  // sample slots spread over all regions (QF regions per map workgroup: every QF-th region's first records)
-  const uint32_t sstride = G * SPLIT_PER_REGION > SPLIT_SAMPLE ? G * SPLIT_PER_REGION / SPLIT_SAMPLE : 1u;  // QF when RG = 4 x 256
+  const uint32_t G = reg_grid(w), QF = reg_qf(w), MG = G / QF;
+  // sample slot rj (of NS = 256) reads region QF g + q of map workgroup g =
+  // rj MG / NS (spread evenly over all map workgroups, so over the whole
+  // corpus) with q = rj mod QF rotating through the slices; a grid of at most
+  // NS regions is sampled whole
+  constexpr uint32_t NS = SPLIT_SAMPLE / SPLIT_PER_REGION;
   auto mark = [&](uint32_t h) {
     const uint32_t bit = hbits(h, NB_LOG2, 12);  // LC_BITS = 2^12
     atomicOr(&bm[bit >> 5], 1u << (bit & 31));
@@ -2171,7 +2174,8 @@ __device__ __forceinline__ void split_count(const Work& w) {
 #pragma unroll
     for (int j = 0; j < PER; j++) {  // k_map's note_sample: contiguous per partition, 0 = no record
       const uint32_t idx = tid + j * SC_THREADS;
-      const uint32_t rj = idx / SPLIT_PER_REGION, reg = rj * sstride + rj % sstride;  // every map workgroup, every q
+      const uint32_t rj = idx / SPLIT_PER_REGION;
+      const uint32_t reg = G <= NS ? rj : (uint32_t)((uint64_t)rj * MG / NS) * QF + rj % QF;
       v[j] = idx < SPLIT_SAMPLE && reg < G ? w.samp[((uint64_t)b * G + reg) * SPLIT_PER_REGION + idx % SPLIT_PER_REGION] : 0u;
     }
 #pragma unroll
@@ -2508,7 +2512,11 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   // open at once
   const uint32_t qf = reg_qf(w);
   const bool sliced = qf > 1 && kk >= (qf == 4u ? 2u : 1u);
-  if (sliced && MOX_SPLIT_STAGE) {
+  // the stage's per-sub-bucket arrays (lcnt, lst, gb) hold 1,024 entries: a
+  // slice opens (2^kk) / qf sub-buckets, which exceeds that only for qf = 2 and
+  // kk = 12 (a 257..512-workgroup map grid); such a slice takes the pair path
+  const bool stage_fits = ((1u << kk) >> (qf == 4u ? 2u : 1u)) <= 1024u;
+  if (sliced && stage_fits && MOX_SPLIT_STAGE) {
     SplitStage S;
     S.stage = reinterpret_cast<uint4*>(xs);
     S.sidx = reinterpret_cast<uint16_t*>(xs + SST_CH * 16);
@@ -2659,6 +2667,13 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       // per step), the next chunk's loads in flight while the current one is
       // inserted.
       {
+#if MOX_RED_DYN
+        if (rep) {  // DBG_RED_TWICE: the chunk tickets restart for the second stream
+          __syncthreads();
+          if (tid == 0) s.misc[2] = 0;
+          __syncthreads();
+        }
+#endif
         const uint32_t n = split ? kin_n : rpre[G];
         constexpr uint32_t CH = 64 * RED_UNROLL;
 #if MOX_RED_DYN

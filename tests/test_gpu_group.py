@@ -255,3 +255,73 @@ def test_group_set_flags_reaches_every_member():
         assert g.stats()["ms_map"] > 0
     finally:
         g.close()
+
+
+def test_group_eight_members_c3_exact():
+    """The driver's N = 8 configuration on one GPU: an engine group of 8
+    members (copy transport, all on device 0) over 8 byte-range shards of the
+    C3 stream (128 MiB each, the bench's left context and 64 KiB look-ahead),
+    local passes, exchange, per-owner reduce, gather and the device bytewise
+    sort.  The gathered table is the oracle's sorted table, array for array."""
+    n, per = 8, 128 << 20
+    cfg = corpus.CONFIGS["C3"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, n * per)
+    g = group(n, flags=mox.MOX_F_SORT_BYTES, reserve_bytes=per)
+    bufs = []
+    try:
+        shards = []
+        for r in range(n):
+            lo, hi, ob, oe, end = mdist.shard_range(n * per, n, r, per_rank=per, halo=1 << 16)
+            m = g.member(r)
+            d = m.alloc(hi - lo)
+            bufs.append((m, d))
+            m.h2d(d, data[lo:hi])
+            shards.append((d, hi - lo, ob, oe, end))
+        for _ in range(2):  # twice: the second call reuses every member's buffers
+            g.run_shards(shards)
+            st = g.stats()
+            t = g.fetch()
+            counts, offs, raw = t.arrays()
+            tokens = t.tokens
+            t.close()
+            wc, wo, wraw, wtok = coracle.count_arrays(data, nthreads=16)
+            assert st["n_gpus"] == n and st["x_bytes_sent"] > 0 and st["ms_sort"] > 0
+            assert tokens == wtok == st["tokens"]
+            assert np.array_equal(counts, wc) and np.array_equal(offs, wo) and raw == wraw
+    finally:
+        for m, d in bufs:
+            m.free(d)
+        g.close()
+
+
+def test_bench_eight_members_without_torchrun():
+    """`bench.py --gpus 8 --xport host --device 0`: the bench's multi-GPU step
+    with 8 members (engine group, copy transport on one GPU) exits 0 with the
+    multi_gpu fields, so that the driver's 8-GPU run can only fail in RCCL."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--xport", "host", "--device", "0",
+           "--steps", "2", "--warmup", "1", "--bytes-per-gpu", str(128 << 20), "--no-cpu-baseline"]
+    r = subprocess.run(cmd, capture_output=True, timeout=600, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    line = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert line["n_gpus"] == 8 and line["value"] > 0 and line["check_sum_counts_eq_tokens"]
+    mg = line["multi_gpu"]
+    assert mg["all_to_all_bytes"] > 0 and mg["gathered_table"]["n"] > 0
+    assert line["phases_ms"]["sort_bytes"] > 0 and line["hash_order"]["value"] > 0
+
+
+def test_bench_torchrun_processes_host_transport():
+    """The driver's multi-GPU launch shape (torch.distributed.run, one process
+    per rank, bench.py main()) with 2 ranks sharing device 0 over the host
+    transport: exchange, gather and the sort at rank 0 inside the timed step;
+    rank 0 prints one JSON line with the multi_gpu fields."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29571", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--xport", "host", "--device", "0", "--steps", "2", "--warmup", "1",
+           "--bytes-per-gpu", str(64 << 20)]
+    r = subprocess.run(cmd, capture_output=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    line = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0 and line["check_sum_counts_eq_tokens"]
+    mg = line["multi_gpu"]
+    assert mg["all_to_all_bytes"] > 0 and mg["gathered_table"]["n"] > 0 and len(mg["per_rank_tokens"]) == 2

@@ -133,3 +133,39 @@ def test_c3_group_two_8gib_shards_exact():
     del data
     assert counts.size == wc.size
     assert np.array_equal(counts, wc) and np.array_equal(offs, wo) and raw == wraw
+
+
+def test_c2_async_bench_mode_exact():
+    """The mode the headline bench times, at its full size (bench.py, N = 1):
+    K back-to-back asynchronous passes (mox_run_range_async) over the 1 GiB C2
+    corpus with MOX_F_TIMING_MAP, each pass's dictionary built on the side
+    stream into the dictionary set the previous pass did not use.  Every
+    completed pass's tokens and distinct words equal the oracle's, and the last
+    pass's table equals the oracle's table."""
+    cfg = corpus.CONFIGS["C2"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
+    wc, wo, wraw, wtok = coracle.count_arrays(data, nthreads=16)
+    e = mox.Engine(device=0, flags=mox.MOX_F_TIMING_MAP, reserve_bytes=data.nbytes)
+    d = e.alloc(data.nbytes)
+    try:
+        e.h2d(d, data)
+        completed = []
+        for i in range(6):
+            e.run_range_async(d, data.nbytes, 0, data.nbytes, True)
+            if i > 0:  # this call completed the previous pass
+                st = e.stats()
+                completed.append((st["tokens"], st["uniques"], st["ms_map"] > 0))
+        e.run_wait()
+        st = e.stats()
+        completed.append((st["tokens"], st["uniques"], st["ms_map"] > 0))
+        assert st["async_reruns"] == 0 and st["async_dropped"] == 0, st
+        t = e.fetch()
+        counts, offs, raw = t.arrays()
+        tokens = t.tokens
+        t.close()
+    finally:
+        e.free(d)
+        e.close()
+    assert completed == [(wtok, wc.size, True)] * 6
+    assert tokens == wtok
+    assert_tables_equal((counts, offs, raw), (wc, wo, wraw))

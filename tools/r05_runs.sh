@@ -1,0 +1,57 @@
+#!/bin/bash
+# Round-5 GPU runs, one section per call; every file under profiles/r05/ names
+# the section that produced it.  Usage on a GPU box (through gpurun):
+#   bash tools/r05_runs.sh SECTION [TAG]      (outputs under gpurun_out/TAG)
+#
+# Sections:
+#   newtests the round-5 tests: full-size async bench-mode C2 parity, the
+#            8-member engine group, bench.py --gpus 8 (engine group) and the
+#            torchrun launch shape on one GPU, the device sort tests
+#   evid     default C2 bench line (with the CPU baseline) and a rocprofv3
+#            kernel trace + stats of the C2 bench with one pass's timeline
+#   fast     the fast GPU suite (gpu and not slow)
+#   slow     the slow GPU tests
+#   ab       interleaved per-kernel A/B of build variants: AB_VARS="v1 v2 v1 v2"
+#            AB_KERNELS="k_map" [AB_DBG="0"] [AB_ARGS="--workload C4 ..."]
+#   pmc      k_map FETCH/WRITE traffic at C2 and SQ counters of k_map
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+SEC=$1
+O=gpurun_out/${2:-$SEC}; mkdir -p $O
+step() { echo "== $1 rc=$2"; [ "$2" -eq 0 ] || exit "$2"; }
+pyt() {  # pyt LOG TIMEOUT pytest-args...
+  local log=$1 to=$2; shift 2
+  timeout -k 10 $to python -u -m pytest -x -v --timeout 600 --timeout-method thread "$@" > $O/$log 2>&1
+  local rc=$?; step "$log $(tail -1 $O/$log)" $rc
+}
+case $SEC in
+newtests)
+  pyt sort.log 300 tests/test_table_sort.py tests/test_gpu_group.py -m gpu -k "sort"
+  pyt group8.log 600 tests/test_gpu_group.py -m gpu -k "eight or torchrun"
+  pyt async_c2.log 400 tests/test_gpu_scale.py -m gpu -k "async_bench_mode"
+  ;;
+evid)
+  timeout -k 10 400 python -u bench.py > $O/bench_c2.json 2> $O/bench_c2.err; step "bench C2" $?
+  cut -c1-300 $O/bench_c2.json
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o run -- \
+    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/c2_under_rocprof.log 2>&1; step "rocprof C2" $?
+  python3 tools/trace_timeline.py $O/c2 > $O/c2_timeline.txt; step "timeline C2" $?
+  tail -1 $O/c2_timeline.txt
+  ;;
+fast)
+  pyt gpu_fast.log 900 tests -m "gpu and not slow"
+  ;;
+slow)
+  pyt gpu_slow.log 1100 tests -m "gpu and slow"
+  ;;
+ab)
+  bash tools/ab_kernel.sh "$AB_VARS" "${AB_DBG:-0}" "$AB_KERNELS" ${AB_ARGS:-} > $O/ab.txt 2>&1; rc=$?; cat $O/ab.txt; step ab $rc
+  ;;
+pmc)
+  bash tools/pmc_traffic_wl.sh C2 1073741824 ${2:-pmc}_traffic > $O/traffic.txt 2>&1; rc=$?; tail -5 $O/traffic.txt; step traffic $rc
+  bash tools/pmc_sq.sh k_map ${2:-pmc}_sqmap > $O/sq_k_map.txt 2>&1; rc=$?; cat $O/sq_k_map.txt; step "sq k_map" $rc
+  ;;
+*)
+  echo "unknown section $SEC"; exit 2
+  ;;
+esac
