@@ -232,8 +232,7 @@ int alloc_fixed(mox_engine* e) {
   return MOX_OK;
 }
 
-constexpr size_t map_lds_bytes() { return DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 + RING * 8 + RING * SLOT + MAP_CONSUMERS * 2 * TOKMAX; }
-static_assert(map_lds_bytes() <= 160 * 1024, "k_map LDS over 160 KiB");
+constexpr size_t map_lds_bytes() { return MAP_LDS_BYTES; }  // (mox_internal.h)
 size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
 
 float ev_ms(mox_engine* e, int a, int b) {

@@ -57,10 +57,25 @@ constexpr int KSEL_N = 17 * 4;              // k_map key selectors: key length 0
 constexpr int LD_GROUP = MOX_LD_GROUP;      // loader: rows per register group
 constexpr int LD_GROUPS = MOX_LD_GROUPS;    // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
+// k_map row supply.  MOX_MAP_SELF=1: every wave loads its own rows, one row
+// ahead, by LDS-DMA into two row buffers of its own (no loader wave, no ring);
+// the wait for a row's DMA counts the wave's cold-record stores issued since
+// (mox_kernels.hip, k_map).  0: one loader wave + the LDS ring (round 4).
+#ifndef MOX_MAP_SELF
+#define MOX_MAP_SELF 1
+#endif
+constexpr int MAP_ROW_WAVES = MOX_MAP_SELF ? MAP_WAVES : MAP_CONSUMERS;  // waves that process rows
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
 constexpr uint32_t QF_MAX = 4;              // most cold regions per (map workgroup, partition) (k_map without a dictionary)
+// k_map dynamic LDS (carved in this order by k_map): dictionary counts, region
+// counters, misc, key selectors, dictionary keys, then the row supply (per-wave
+// row buffers, or the ring with its ready / free words) and the token lists
+constexpr size_t MAP_LDS_BYTES = (size_t)DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 +
+                                 (MOX_MAP_SELF ? (size_t)MAP_WAVES * 2 * SLOT : (size_t)RING * 8 + (size_t)RING * SLOT) +
+                                 (size_t)MAP_ROW_WAVES * 2 * TOKMAX;
+static_assert(MAP_LDS_BYTES <= 160 * 1024, "k_map LDS over 160 KiB");
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;
 constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B

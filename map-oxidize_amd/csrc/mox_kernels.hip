@@ -352,7 +352,7 @@ __device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w
   return -1;
 }
 
-__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1);
+__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1, uint32_t* nst = nullptr);
 
 // A short word (lowered length <= 16, no NUL byte) as an exact 16-byte key.
 // Hot words: LDS dictionary count.  Others: appended to this workgroup's
@@ -417,11 +417,14 @@ __device__ __forceinline__ void note_sample(const MapCtx& m, uint32_t b, uint32_
     rare(m).samp[((uint64_t)b * m.rg + blockIdx.x * m.qf + q) * SPLIT_PER_REGION + pos] = h;
 }
 // No dictionary: slot B = the partition bits and the qb bits below them
-// (partition b = B >> qb, region q = B & (qf - 1)).
-__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t h, uint4 key) {
+// (partition b = B >> qb, region q = B & (qf - 1)).  *nst (when given) counts
+// the pair stores the wave issued (2 per round in which any lane stored a pair;
+// a lower bound: spills and samples are not counted), for k_map's row-DMA wait.
+__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t h, uint4 key, uint32_t* nst) {
   const uint32_t b = B >> m.qb, qr = B & (m.qf - 1);
   bool done = false;
   do {
+    bool st2 = false;
     if (!done) {
       uint4 q;
       const int r = pair_try(m.s.pst, m.s.pend, B, key, &q);
@@ -444,6 +447,7 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
             uint4* o = cold_at(m, b, qr, pos);
             o[0] = q;
             o[1] = key;
+            st2 = true;
           } else {
             cold_spill(m, q);
             cold_spill(m, key);
@@ -452,15 +456,16 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
       }
       done = r != 0;
     }
+    if (nst && __any(st2)) *nst += 2u;
     __builtin_amdgcn_wave_barrier();
   } while (__any(!done));
 }
-__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
+__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1, uint32_t* nst) {
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   if (m.dict_n == 0) {
-    if (!MOX_ABL(m.w.dbg, DBG_NOPAIR)) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key); return; }
+    if (!MOX_ABL(m.w.dbg, DBG_NOPAIR)) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key, nst); return; }
     const uint32_t B = h >> (32 - NB_LOG2 - m.qb), qr = B & (m.qf - 1);
     const uint32_t pos = atomicAdd(&m.s.bcnt[B], 1u);
     if (pos < SPLIT_PER_REGION) note_sample(m, b, qr, pos, h);
@@ -720,9 +725,12 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
 // of a phase are issued before the first is used (SCHED_FENCE).  The
 // dictionary arrays are zero when there is no dictionary (a real key is never
 // zero, so nothing hits), but that case takes pass_c.
+// nst counts the cold-store instructions the wave issues (one per batch in
+// which any lane stores a record; spills and samples are extra), for the
+// counted wait on the next row's DMA (k_map, MOX_MAP_SELF).
 template <int TU>
 __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t total) {
+                                       uint32_t total, uint32_t& nst) {
   const int lane = threadIdx.x & 63;
   uint32_t e[TU];
 #pragma unroll
@@ -773,6 +781,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
   SCHED_FENCE();
 #pragma unroll
   for (int u = 0; u < TU; u++) {
+    nst += __any(miss[u] && pos[u] < m.rc) ? 1u : 0u;
     if (!miss[u]) continue;
     const uint32_t b = bucket_of(h[u]);
     const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
@@ -786,7 +795,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 // straight to the cold path.
 template <int TU>
 __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t total) {
+                                       uint32_t total, uint32_t& nst) {
   const int lane = threadIdx.x & 63;
   uint32_t e[TU];
 #pragma unroll
@@ -809,7 +818,53 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
   for (int u = 0; u < TU; u++) {
     if (e[u] >= LIST_ODD) continue;
     const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
-    cold_word(m, hash32(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1);
+    cold_word(m, hash32(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1, &nst);
+  }
+}
+
+// ---- k_map row supply by the row's own wave (MOX_MAP_SELF)
+// LDS-DMA of one row slot: lane i's 16 bytes at gsrc land at LDS byte address
+// lds + 16 i (global_load_lds_dwordx4, nt: read once).  Written as asm so that
+// the compiler neither waits for it nor counts it: its LDS target is read only
+// after the counted wait below.  M0 is restored in the same statement.
+__device__ __forceinline__ void row_dma(const uint8_t* gsrc, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+// Source byte of lane block p of a row slot, clamped like raw16 to a 16-byte
+// block that overlaps [lo, hi) (bytes outside are fixed up by fix16 after the
+// read); an empty buffer reads its first block (c.base + first is the buffer
+// start rounded down to 16 B, a valid address: make_corpus)
+__device__ __forceinline__ uint64_t dma_src(const Corpus& c, uint64_t p) {
+  const uint64_t first = c.lo & ~15ull, last = (c.hi - 1) & ~15ull;
+  p = p > last ? last : p;
+  p = p < first ? first : p;
+  return c.hi <= c.lo ? first : p;
+}
+template <int N>
+__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
+// Wait until at most n (wave-uniform) of the wave's vector-memory operations
+// are outstanding, rounded down to a step of this ladder (waiting for a few
+// more than needed is safe: they are older)
+__device__ __forceinline__ void vm_wait_le(uint32_t n) {
+  if (n >= 8) {
+    if (n >= 32) vm_wait_n<32>();
+    else if (n >= 16) vm_wait_n<16>();
+    else if (n >= 12) vm_wait_n<12>();
+    else vm_wait_n<8>();
+  } else if (n >= 4) {
+    if (n >= 6) { if (n == 7) vm_wait_n<7>(); else vm_wait_n<6>(); }
+    else if (n == 5) vm_wait_n<5>();
+    else vm_wait_n<4>();
+  } else if (n >= 2) {
+    if (n == 3) vm_wait_n<3>(); else vm_wait_n<2>();
+  } else if (n == 1) {
+    vm_wait_n<1>();
+  } else {
+    vm_wait_n<0>();
   }
 }
 
@@ -828,8 +883,11 @@ struct Cyc {
 //     prefix sum of per-lane start counts from 5 bit-sliced ballots);
 //  2. token phase (lane = token): pass_a over all tokens (both dictionary slots
 //     read at once: an LDS count on a hit, the cold store on a miss).
+// nst: vector-memory stores the row issued (a lower bound, pass_a); vclear:
+// the row waited for every vector-memory operation of the wave (vm_settle on a
+// rare path), so the next row's DMA has landed.
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
-                                       uint16_t* list, struct Cyc* cyc, bool edge) {
+                                       uint16_t* list, struct Cyc* cyc, bool edge, uint32_t& nst, bool& vclear) {
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
   // lanes 0 and 63 are context only: their starts are cleared with a per-lane
@@ -885,6 +943,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   } else {
     start = ctx ? 0u : slow_starts(m, p0);
     vm_settle();
+    vclear = true;
   }
   if MOX_ABL(m.w.dbg, DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
   const uint32_t cnt = __popc(start);
@@ -941,23 +1000,24 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       if (e >= LIST_ODD) generic_token(m, sbase + (e & 1023u));
     }
     vm_settle();
+    vclear = true;
   }
   if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
   uint64_t t1 = 0;
   if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
   if (m.dict_n == 0) {  // no dictionary: no probes (uniform branch)
     for (uint32_t j0 = 0; j0 < total;) {
-      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, total); j0 += 128; }
-      else { pass_c<1>(m, rowbuf, list, j0, total); j0 += 64; }
+      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, total, nst); j0 += 128; }
+      else { pass_c<1>(m, rowbuf, list, j0, total, nst); j0 += 64; }
     }
     wave_lds_fence();
     return;
   }
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
-    if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, total); j0 += 192; }
-    else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, total); j0 += 128; }
-    else { pass_a<1>(m, rowbuf, list, j0, total); j0 += 64; }
+    if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, total, nst); j0 += 192; }
+    else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, total, nst); j0 += 128; }
+    else { pass_a<1>(m, rowbuf, list, j0, total, nst); j0 += 64; }
   }
   if (cyc) cyc->pa += __builtin_amdgcn_s_memtime() - t1;
   wave_lds_fence();
@@ -994,10 +1054,14 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
   m.s.seltab = (uint4*)sp; sp += KSEL_N * 16;
   m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
+#if MOX_MAP_SELF
+  uint8_t* rowbufs = sp; sp += MAP_WAVES * 2 * SLOT;  // two row buffers per wave
+#else
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
   uint8_t* ring = sp; sp += RING * SLOT;
-  uint16_t* lists = (uint16_t*)sp; sp += MAP_CONSUMERS * 2 * TOKMAX;
+#endif
+  uint16_t* lists = (uint16_t*)sp; sp += MAP_ROW_WAVES * 2 * TOKMAX;
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
   static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
@@ -1023,7 +1087,9 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     m.s.bcnt[i] = resume ? cold_n_at(w, m.rg, blockIdx.x * m.qf + q, b) : 0u;
   }
   if (tid < 4) m.s.misc[tid] = (resume && tid == 0) ? w.spill_n[blockIdx.x] : 0u;
+#if !MOX_MAP_SELF
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
+#endif
   if (tid < KSEL_N) {  // key byte 4 d + j = window byte sh + 4 d + j, or 0 past len (v_perm selector 0x0C)
     const uint32_t len = (uint32_t)tid >> 2, sh = (uint32_t)tid & 3u;
     uint32_t sel[4];
@@ -1044,6 +1110,85 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   const uint64_t rb = blockIdx.x * per + (blockIdx.x < rem ? blockIdx.x : rem);
   const uint32_t n = (uint32_t)(per + (blockIdx.x < rem ? 1 : 0));
 
+#if MOX_MAP_SELF
+  {
+    // ---------------- every wave: rows by ticket, each loaded by its own wave
+    // one row ahead.  At the start of a row the wave issues the LDS-DMA of its
+    // next row into its other buffer and takes the ticket of the row after
+    // that; the current row's DMA (issued one row earlier) is then waited for
+    // by a counted vmcnt: younger than it are only the previous row's cold
+    // stores (counted by the token passes, a lower bound) and the next row's
+    // DMA, so the wait never drains the stores the wave just issued.  A row
+    // thus has a whole row's processing time to arrive, and there is no loader
+    // wave, ring, or ready / free hand-off.
+    uint16_t* list = lists + wv * TOKMAX;
+    uint32_t e_lo = rb < 2 ? (uint32_t)(2 - rb) : 0u;  // edge rows: see the consumers of the ring build below
+    const uint32_t e_hi = __builtin_amdgcn_readfirstlane(nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u);
+    if (c.own_hi > base0 && nrows * PAY < c.own_hi - base0) e_lo = n;
+    uint8_t* mybuf = rowbufs + wv * (2 * SLOT);
+    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)mybuf);
+#ifdef MOX_STAMP
+    Cyc cyc{0, 0, 0, 0, 0, 0};
+    Cyc* cp = &cyc;
+#else
+    Cyc* cp = nullptr;
+#endif
+    // tickets: lane 0's LDS atomic, read (readfirstlane) one row later, so the
+    // atomic's round trip is not waited for where it is issued
+    auto ticket = [&]() -> uint32_t {
+      uint32_t u = 0;
+      if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
+      return u;
+    };
+    // row u's slot, lane block: interior rows from one loop-invariant per-lane
+    // base; edge rows clamped like raw16 (their out-of-range bytes are fixed up
+    // after the read)
+    const uint8_t* lbase = c.base + (base0 + rb * PAY - 16 + 16 * (uint64_t)lane);
+    auto dma = [&](uint32_t u, uint32_t bi) {
+      const uint8_t* src;
+      if (u < e_lo || u >= e_hi) src = c.base + dma_src(c, base0 + (rb + u) * PAY - 16 + 16 * (uint64_t)lane);
+      else src = lbase + (uint64_t)u * PAY;
+      row_dma(src, lds0 + bi * SLOT);
+    };
+    uint32_t cur = __builtin_amdgcn_readfirstlane(ticket());
+    if (cur < n) dma(cur, 0);
+    uint32_t nxt_v = ticket();
+    uint32_t nst = 0;      // cold-store instructions of the previous row (issued after cur's DMA)
+    bool vclear = false;   // the previous row drained the wave's vector memory
+    for (uint32_t k = 0; cur < n; k++) {
+      const uint64_t tw = cp ? __builtin_amdgcn_s_memtime() : 0;
+      const uint32_t bi = k & 1u;
+      const uint32_t nxt = __builtin_amdgcn_readfirstlane(nxt_v);
+      uint32_t ahead = 0;
+      if (nxt < n) { dma(nxt, bi ^ 1u); ahead = 1; }
+      const uint32_t nn_v = ticket();
+      // cur's DMA has landed once at most (nst + ahead - 1) younger operations
+      // are outstanding (one fewer than counted: a margin of one store)
+      if (!vclear) vm_wait_le(nst + ahead > 0 ? nst + ahead - 1 : 0u);
+      nst = 0;
+      vclear = false;
+      uint8_t* sl = mybuf + bi * SLOT;
+      const uint64_t sbase = base0 + (rb + cur) * PAY - 16;
+      uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
+      const bool edge = cur < e_lo || cur >= e_hi;
+      if (edge && (sbase < c.lo || sbase + SLOT > c.hi)) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
+      if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
+      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge, nst, vclear);
+      else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
+      cur = nxt;
+      nxt_v = nn_v;
+    }
+    vm_wait_n<0>();  // (every DMA issued was waited for above; nothing may land in LDS after the loop)
+#ifdef MOX_STAMP
+    if (lane == 0 && w.stamps) {
+      unsigned long long* o = w.stamps + 8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8;
+      o[0] = cyc.wait; o[1] = cyc.byte; o[2] = cyc.pa; o[3] = cyc.pb; o[4] = cyc.miss; o[5] = cyc.rows;
+      o[6] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+  }
+#else
   if (wv < MAP_LOADERS) {
     // ---------------- loaders: loader wv owns row groups wv, wv + MAP_LOADERS, ...
     uint4 buf[LD_GROUPS][LD_GROUP];
@@ -1161,7 +1306,9 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       const bool edge = u < e_lo || u >= e_hi;
       if (edge && (sbase < c.lo || sbase + SLOT > c.hi)) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
       if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
-      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge);
+      uint32_t nst = 0;
+      bool vclear = false;
+      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge, nst, vclear);
       else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1174,6 +1321,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     }
 #endif
   }
+#endif
   __syncthreads();
   if (m.dict_n == 0) {  // records still parked in pair slots: written as singles
     for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {

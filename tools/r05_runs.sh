@@ -10,6 +10,7 @@
 #   evid     default C2 bench line (with the CPU baseline) and a rocprofv3
 #            kernel trace + stats of the C2 bench with one pass's timeline
 #   fast     the fast GPU suite (gpu and not slow)
+#   parity   the parity subset (test_gpu_parity, test_gpu_collide; not slow)
 #   slow     the slow GPU tests
 #   ab       interleaved per-kernel A/B of build variants: AB_VARS="v1 v2 v1 v2"
 #            AB_KERNELS="k_map" [AB_DBG="0"] [AB_ARGS="--workload C4 ..."]
@@ -40,6 +41,12 @@ evid)
   ;;
 fast)
   pyt gpu_fast.log 900 tests -m "gpu and not slow"
+  ;;
+parity)
+  # the parity subset of the GPU suite (every k_map path: KATs with and without
+  # the dictionary, fuzz, tile edges, corpora, huge tokens, misaligned ranges,
+  # split partitions, async passes, file ingest, forced collisions)
+  pyt parity.log 600 tests/test_gpu_parity.py tests/test_gpu_collide.py -m "gpu and not slow"
   ;;
 slow)
   pyt gpu_slow.log 1100 tests -m "gpu and slow"
