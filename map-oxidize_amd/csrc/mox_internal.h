@@ -36,7 +36,7 @@ constexpr int RING = MOX_RING;              // k_map row ring slots (LDS)
 // LDS hot dictionary: single-word slots, two choices per word (dict_s1 / dict_s2,
 // mox_kernels.hip); k_dict_pick picks up to DICT_MAX_WORDS candidates
 constexpr int DICT_SLOTS = MOX_DICT_SLOTS;
-constexpr int DICT_MAX_WORDS = 4096;
+constexpr int DICT_MAX_WORDS = DICT_SLOTS < 4096 ? DICT_SLOTS : 4096;
 static_assert(DICT_SLOTS % 32 == 0 && DICT_SLOTS <= 65536 && DICT_MAX_WORDS <= DICT_SLOTS, "dictionary geometry");
 constexpr int MAX_MAP_GRID = 1024;          // map workgroups
 constexpr int MAP_WAVES = MAP_THREADS / 64;
@@ -57,14 +57,29 @@ constexpr int KSEL_N = 17 * 4;              // k_map key selectors: key length 0
 constexpr int LD_GROUP = MOX_LD_GROUP;      // loader: rows per register group
 constexpr int LD_GROUPS = MOX_LD_GROUPS;    // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
-// k_map row supply.  MOX_MAP_SELF=1: every wave loads its own rows, one row
-// ahead, by LDS-DMA into two row buffers of its own (no loader wave, no ring);
-// the wait for a row's DMA counts the wave's cold-record stores issued since
-// (mox_kernels.hip, k_map).  0: one loader wave + the LDS ring (round 4).
+// k_map row supply.  0 (default): one loader wave + the LDS ring.  1: every
+// wave loads its own rows, MOX_MAP_AHEAD rows ahead, by LDS-DMA into row
+// buffers of its own (no loader wave, no ring); the wait for a row's DMA
+// counts the wave's cold-record stores issued since (mox_kernels.hip, k_map).
+// It removes the ring's supply floor (427-489 us at C2 -> 242 us one row
+// ahead, 174 us two ahead) but measured 1.5-4 % slower on the whole kernel
+// (DESIGN.md §8, round 5): the consumers, not the supply, bind.
 #ifndef MOX_MAP_SELF
-#define MOX_MAP_SELF 1
+#define MOX_MAP_SELF 0
 #endif
 constexpr int MAP_ROW_WAVES = MOX_MAP_SELF ? MAP_WAVES : MAP_CONSUMERS;  // waves that process rows
+#ifndef MOX_MAP_AHEAD
+#define MOX_MAP_AHEAD 1  // rows a wave keeps loading ahead of the one it processes (1 or 2)
+#endif
+constexpr int MAP_AHEAD = MOX_MAP_AHEAD;
+#ifndef MOX_MAP_PAIR
+#define MOX_MAP_PAIR 0  // 1: a wave processes two consecutive rows at once (do_pair), one pair loaded ahead
+                        // (MOX_MAP_SELF; its LDS needs a dictionary of <= 2,976 slots: a timing experiment)
+#endif
+constexpr int MAP_PAIRW = MOX_MAP_PAIR ? 2 : 1;  // rows per buffer / list unit
+static_assert(!MOX_MAP_PAIR || (MOX_MAP_SELF && MOX_MAP_AHEAD == 1), "row pairs: self-loading, one pair ahead");
+constexpr int MAP_BUFS = MAP_AHEAD + 1;     // row buffers per wave
+static_assert(MAP_AHEAD == 1 || MAP_AHEAD == 2, "k_map rows ahead");
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
@@ -73,8 +88,8 @@ constexpr uint32_t QF_MAX = 4;              // most cold regions per (map workgr
 // counters, misc, key selectors, dictionary keys, then the row supply (per-wave
 // row buffers, or the ring with its ready / free words) and the token lists
 constexpr size_t MAP_LDS_BYTES = (size_t)DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 +
-                                 (MOX_MAP_SELF ? (size_t)MAP_WAVES * 2 * SLOT : (size_t)RING * 8 + (size_t)RING * SLOT) +
-                                 (size_t)MAP_ROW_WAVES * 2 * TOKMAX;
+                                 (MOX_MAP_SELF ? (size_t)MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT : (size_t)RING * 8 + (size_t)RING * SLOT) +
+                                 (size_t)MAP_ROW_WAVES * 2 * TOKMAX * MAP_PAIRW;
 static_assert(MAP_LDS_BYTES <= 160 * 1024, "k_map LDS over 160 KiB");
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;

@@ -659,13 +659,16 @@ struct KeyLd {
   uint32_t E[5];
   uint4 S;  // v_perm selectors: alignment and length mask in one (seltab)
 };
+// PB: bits of the slot offset in a list entry (10: one row; 11: a row pair,
+// whose two slots are adjacent in LDS), the length field above them
+template <int PB = 10>
 __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf, uint32_t e, KeyLd& r) {
-  const uint32_t pos = e & 1023u, len = (e >> 10) & 31u;
+  const uint32_t pos = e & ((1u << PB) - 1u);
   const uint32_t* q = reinterpret_cast<const uint32_t*>(rowbuf + (pos & ~3u));
 #pragma unroll
   for (int i = 0; i < 5; i++) r.E[i] = q[i];
-  r.S = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s.seltab) + (((e >> 4) & 0x7C0u) | ((pos & 3u) << 4)));
-  (void)len;  // (entry 4 len + (pos & 3), as a byte offset straight from the list entry)
+  // (entry 4 len + (pos & 3), as a byte offset straight from the list entry)
+  r.S = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s.seltab) + (((e >> (PB - 6)) & 0x7C0u) | ((pos & 3u) << 4)));
 }
 __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
   (void)e;
@@ -728,22 +731,23 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
 // nst counts the cold-store instructions the wave issues (one per batch in
 // which any lane stores a record; spills and samples are extra), for the
 // counted wait on the next row's DMA (k_map, MOX_MAP_SELF).
-template <int TU>
+template <int TU, int PB = 10>
 __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
                                        uint32_t total, uint32_t& nst) {
   const int lane = threadIdx.x & 63;
+  constexpr uint32_t LMAX = PB == 10 ? TOKMAX : 2 * TOKMAX;  // list entries (the last is the sink)
   uint32_t e[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
-    e[u] = list[j < TOKMAX ? j : TOKMAX - 1];
+    e[u] = list[j < LMAX ? j : LMAX - 1];
   }
   SCHED_FENCE();  // every batch's list read in flight before the first is used
 #pragma unroll
-  for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : 0x8000u;  // inactive = odd
+  for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : (17u << PB);  // inactive = odd (slot offset 0)
   KeyLd ld[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
+  for (int u = 0; u < TU; u++) key_load<PB>(m.s, rowbuf, e[u], ld[u]);
   SCHED_FENCE();
   AFTER_FENCE(e);
   uint32_t K[TU][4], h[TU], s1[TU], s2[TU];
@@ -764,7 +768,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
   uint32_t pos[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    const bool valid = e[u] < LIST_ODD;
+    const bool valid = e[u] < (17u << PB);  // LIST_ODD of the format
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
     miss[u] = valid & !(hit1 | hit2);
     if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[hit1 ? s1[u] : s2[u]], 1u);
@@ -844,6 +848,12 @@ __device__ __forceinline__ uint64_t dma_src(const Corpus& c, uint64_t p) {
   p = p < first ? first : p;
   return c.hi <= c.lo ? first : p;
 }
+#ifndef MOX_MAP_STATIC
+#define MOX_MAP_STATIC 0  // 1: k_map waves take rows wv, wv + 16, ... instead of LDS tickets (MOX_MAP_SELF)
+#endif
+#ifndef MOX_DMA_MARGIN
+#define MOX_DMA_MARGIN 1  // the counted row-DMA wait leaves this many fewer operations outstanding than counted
+#endif
 template <int N>
 __device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
 // Wait until at most n (wave-uniform) of the wave's vector-memory operations
@@ -1023,6 +1033,105 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   wave_lds_fence();
 }
 
+#if MOX_MAP_PAIR
+// ASCII byte classification of one 16-byte lane block (do_row's common path):
+// whitespace flags of the 16 bytes in bits 0..15, and the control-byte flags
+// (bytes < 33 that are not whitespace, NUL included) as 0x80 per byte
+__device__ __forceinline__ uint32_t classify16(uint4 a, uint32_t& ctl) {
+  const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
+  uint32_t wsd[4];
+  ctl = 0;
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    const uint32_t x = ad[d];
+    const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
+    wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
+    ctl |= lt33 & ~wsd[d];
+  }
+  uint32_t lo = (wsd[0] >> 7) | (wsd[1] >> 3), hi = (wsd[2] >> 7) | (wsd[3] >> 3);
+  lo |= (lo >> 7) | (lo >> 14) | (lo >> 21);
+  hi |= (hi >> 7) | (hi >> 14) | (hi >> 21);
+  return __builtin_amdgcn_perm(hi, lo, 0x0C0C0400u);
+}
+// Two consecutive rows at once (MOX_MAP_PAIR): slots buf (row u) and buf + SLOT
+// (row u + 1), one list of both rows' tokens in 11-bit-offset entries (row
+// u + 1's at slot offset 1024 + ...).  The two rows' byte phases are
+// independent chains the scheduler interleaves; their start counts share one
+// packed wave scan (row u's in the low 16 bits) and one max scan, their list
+// entries one loop; the token pass runs over the joint list (fuller batches).
+// Rows with non-ASCII or control bytes take do_row one at a time.  The caller
+// passes interior rows only (no edge checks) and a pass with a dictionary.
+__device__ __forceinline__ void do_pair(const MapCtx& m, uint64_t sbase, uint4 a0, uint4 a1, unsigned long long& ntok,
+                                        uint8_t* buf, uint16_t* list, struct Cyc* cyc, uint32_t& nst, bool& vclear) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t keep = (uint32_t)(lane - 1) < 62u ? 0xFFFFFFFFu : 0u;
+  bool fall = __any((nonascii16(a0) | nonascii16(a1)) != 0);
+  uint32_t ws0 = 0, ws1 = 0, st0 = 0, st1 = 0;
+  if (!fall) {
+    uint32_t ctl0, ctl1;
+    const uint32_t w0 = classify16(a0, ctl0), w1 = classify16(a1, ctl1);
+    const uint32_t n0 = from_next_lane(w0), n1 = from_next_lane(w1);
+    const uint32_t q0 = from_prev_lane(w0), q1 = from_prev_lane(w1);
+    ws0 = w0 | (n0 << 16);
+    ws1 = w1 | (n1 << 16);
+    st0 = (~ws0) & ((ws0 << 1) | ((q0 >> 15) & 1u)) & 0xFFFFu & keep;
+    st1 = (~ws1) & ((ws1 << 1) | ((q1 >> 15) & 1u)) & 0xFFFFu & keep;
+    fall = __any(((ctl0 | ctl1) & 0x80808080u) != 0);  // control bytes (NUL checks): one row at a time
+  }
+  if (fall) {
+    do_row(m, sbase, a0, ntok, buf, list, cyc, false, nst, vclear);
+    do_row(m, sbase + PAY, a1, ntok, buf + SLOT, list, cyc, false, nst, vclear);
+    return;
+  }
+  const uint32_t c0 = __popc(st0), c1 = __popc(st1);
+  ntok += c0 + c1;
+  const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));  // (a row has at most 496 tokens: no carry)
+  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  const uint32_t t0 = tot & 0xFFFFu, total = t0 + (tot >> 16);
+  if (total == 0) return;
+  reinterpret_cast<uint4*>(buf)[lane] = lower16(a0);
+  reinterpret_cast<uint4*>(buf + SLOT)[lane] = lower16(a1);
+  uint32_t sm0 = ws0 >> 1, sm1 = ws1 >> 1;
+  sm0 |= sm0 >> 1; sm1 |= sm1 >> 1;
+  sm0 |= sm0 >> 2; sm1 |= sm1 >> 2;
+  sm0 |= sm0 >> 4; sm1 |= sm1 >> 4;
+  sm0 |= sm0 >> 8; sm1 |= sm1 >> 8;
+  const bool any_odd = ((st0 & ~sm0) | (st1 & ~sm1)) != 0;
+  const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(max(c0, c1)), 63);
+  uint16_t* const sink = list + (2 * TOKMAX - 1);
+  uint16_t* const mine0 = list + ((incl & 0xFFFFu) - c0);
+  uint16_t* const mine1 = list + (t0 + (incl >> 16) - c1);
+  const uint32_t lb0 = (uint32_t)(lane * 16), lb1 = lb0 + SLOT;
+  for (uint32_t it = 0; it < trips; it++) {
+    const uint32_t p0 = ffbl(st0), p1 = ffbl(st1);
+    st0 &= st0 - 1;
+    st1 &= st1 - 1;
+    const uint32_t l0 = ffbl(ws0 >> (p0 & 31u)), l1 = ffbl(ws1 >> (p1 & 31u));
+    *(it < c0 ? mine0 + it : sink) = (uint16_t)(lb0 + p0 + (l0 << 11));
+    *(it < c1 ? mine1 + it : sink) = (uint16_t)(lb1 + p1 + (l1 << 11));
+  }
+  wave_lds_fence();
+  if (__any(any_odd)) {  // rare: tokens over 16 bytes
+    for (uint32_t j = lane; j < total; j += 64) {
+      const uint32_t e = list[j];
+      if (e >= (17u << 11)) {
+        const uint32_t pos = e & 2047u;
+        generic_token(m, pos < SLOT ? sbase + pos : sbase + PAY + (pos - SLOT));
+      }
+    }
+    vm_settle();
+    vclear = true;
+  }
+  for (uint32_t j0 = 0; j0 < total;) {
+    const uint32_t rem = total - j0;
+    if (rem > 128) { pass_a<3, 11>(m, buf, list, j0, total, nst); j0 += 192; }
+    else if (rem > 64) { pass_a<2, 11>(m, buf, list, j0, total, nst); j0 += 128; }
+    else { pass_a<1, 11>(m, buf, list, j0, total, nst); j0 += 64; }
+  }
+  wave_lds_fence();
+}
+#endif
+
 // Map kernel.  One persistent 1024-thread workgroup per CU owns a contiguous
 // range of rows (992 payload bytes each).
 //  * waves 0..MAP_LOADERS-1 = loaders (alternate row groups): stream each row's slot (payload +16 B either side) with
@@ -1055,7 +1164,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.seltab = (uint4*)sp; sp += KSEL_N * 16;
   m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
 #if MOX_MAP_SELF
-  uint8_t* rowbufs = sp; sp += MAP_WAVES * 2 * SLOT;  // two row buffers per wave
+  uint8_t* rowbufs = sp; sp += MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT;  // MAP_AHEAD + 1 row (pair) buffers per wave
 #else
   uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
   uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
@@ -1064,8 +1173,10 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint16_t* lists = (uint16_t*)sp; sp += MAP_ROW_WAVES * 2 * TOKMAX;
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
+#ifndef MOX_TIMING_ONLY_SMALL_DICT  // (timing experiments with a smaller dictionary: dictionary passes only)
   static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
   static_assert(NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
@@ -1121,11 +1232,16 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     // DMA, so the wait never drains the stores the wave just issued.  A row
     // thus has a whole row's processing time to arrive, and there is no loader
     // wave, ring, or ready / free hand-off.
-    uint16_t* list = lists + wv * TOKMAX;
+#ifdef MOX_MAP_ACTIVE  // (timing experiment: only this many waves take rows)
+    if (wv < MOX_MAP_ACTIVE) {
+#else
+    {
+#endif
+    uint16_t* list = lists + wv * (MAP_PAIRW * TOKMAX);
     uint32_t e_lo = rb < 2 ? (uint32_t)(2 - rb) : 0u;  // edge rows: see the consumers of the ring build below
     const uint32_t e_hi = __builtin_amdgcn_readfirstlane(nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u);
     if (c.own_hi > base0 && nrows * PAY < c.own_hi - base0) e_lo = n;
-    uint8_t* mybuf = rowbufs + wv * (2 * SLOT);
+    uint8_t* mybuf = rowbufs + wv * (MAP_BUFS * MAP_PAIRW * SLOT);
     const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
         (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)mybuf);
 #ifdef MOX_STAMP
@@ -1136,11 +1252,17 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #endif
     // tickets: lane 0's LDS atomic, read (readfirstlane) one row later, so the
     // atomic's round trip is not waited for where it is issued
+#if MOX_MAP_STATIC
+    // static rows: wave wv takes rows wv, wv + 16, ... of the workgroup's range
+    uint32_t tk = __builtin_amdgcn_readfirstlane(wv);
+    auto ticket = [&]() -> uint32_t { const uint32_t u = tk; tk += MAP_WAVES; return u; };
+#else
     auto ticket = [&]() -> uint32_t {
       uint32_t u = 0;
       if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
       return u;
     };
+#endif
     // row u's slot, lane block: interior rows from one loop-invariant per-lane
     // base; edge rows clamped like raw16 (their out-of-range bytes are fixed up
     // after the read)
@@ -1151,21 +1273,98 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       else src = lbase + (uint64_t)u * PAY;
       row_dma(src, lds0 + bi * SLOT);
     };
+#if MOX_MAP_PAIR
+    // row pairs: ticket q = rows 2q, 2q + 1 (adjacent slots of a pair buffer),
+    // the next pair loaded one pair ahead (two DMAs)
+    const uint32_t np = (n + 1) / 2;
+    auto dma_pair = [&](uint32_t q, uint32_t bi) -> uint32_t {
+      dma(2 * q, bi * 2);
+      if (2 * q + 1 < n) { dma(2 * q + 1, bi * 2 + 1); return 2u; }
+      return 1u;
+    };
+    uint32_t cur = __builtin_amdgcn_readfirstlane(ticket());
+    if (cur < np) (void)dma_pair(cur, 0);
+    uint32_t nxt_v = ticket();
+    uint32_t nst = 0;
+    bool vclear = false;
+    uint32_t bi = 0;
+    for (; cur < np;) {
+      const uint32_t nxt = __builtin_amdgcn_readfirstlane(nxt_v);
+      const uint32_t ahead = nxt < np ? dma_pair(nxt, bi ^ 1u) : 0u;
+      const uint32_t nn_v = ticket();
+      const uint32_t young = nst + ahead;
+      if (!vclear) vm_wait_le(__builtin_amdgcn_readfirstlane(young > MOX_DMA_MARGIN ? young - MOX_DMA_MARGIN : 0u));
+      nst = 0;
+      vclear = false;
+      uint8_t* sl = mybuf + bi * (2 * SLOT);
+      const uint32_t u0 = 2 * cur;
+      const uint64_t sbase = base0 + (rb + u0) * PAY - 16;
+      uint4 a0 = reinterpret_cast<const uint4*>(sl)[lane];
+      const bool two = u0 + 1 < n;
+      uint4 a1 = two ? reinterpret_cast<const uint4*>(sl + SLOT)[lane] : make_uint4(0, 0, 0, 0);
+      const bool edge0 = u0 < e_lo || u0 >= e_hi, edge1 = u0 + 1 < e_lo || u0 + 1 >= e_hi;
+      if (two && !edge0 && !edge1 && m.dict_n) {
+        do_pair(m, sbase, a0, a1, ntok, sl, list, nullptr, nst, vclear);
+      } else {
+        if (edge0 && (sbase < c.lo || sbase + SLOT > c.hi)) a0 = fix16(c, sbase + 16 * (uint64_t)lane, a0);
+        do_row(m, sbase, a0, ntok, sl, list, nullptr, edge0, nst, vclear);
+        if (two) {
+          const uint64_t sb1 = sbase + PAY;
+          if (edge1 && (sb1 < c.lo || sb1 + SLOT > c.hi)) a1 = fix16(c, sb1 + 16 * (uint64_t)lane, a1);
+          do_row(m, sb1, a1, ntok, sl + SLOT, list, nullptr, edge1, nst, vclear);
+        }
+      }
+      cur = nxt;
+      nxt_v = nn_v;
+      bi ^= 1u;
+    }
+#else
+    // rows in flight: the wave's next MAP_AHEAD rows (tickets taken in order),
+    // row k in buffer k mod MAP_BUFS.  Younger than row k's DMA are the stores
+    // of the MAP_AHEAD rows before it and the DMAs issued since (one per row).
     uint32_t cur = __builtin_amdgcn_readfirstlane(ticket());
     if (cur < n) dma(cur, 0);
+#if MOX_MAP_AHEAD == 2
+    uint32_t nx1 = __builtin_amdgcn_readfirstlane(ticket());
+    uint32_t dm1 = 0;      // the DMA of nx1 issued (at the row before)
+    if (nx1 < n) { dma(nx1, 1); dm1 = 1; }
+    uint32_t nst1 = 0;     // stores of the row before the previous one
+    bool vclear1 = false;
+#endif
     uint32_t nxt_v = ticket();
     uint32_t nst = 0;      // cold-store instructions of the previous row (issued after cur's DMA)
     bool vclear = false;   // the previous row drained the wave's vector memory
+    uint32_t bi = 0;       // cur's buffer
     for (uint32_t k = 0; cur < n; k++) {
       const uint64_t tw = cp ? __builtin_amdgcn_s_memtime() : 0;
-      const uint32_t bi = k & 1u;
       const uint32_t nxt = __builtin_amdgcn_readfirstlane(nxt_v);
+      const uint32_t bnext = bi + MAP_AHEAD < MAP_BUFS ? bi + MAP_AHEAD : bi + MAP_AHEAD - MAP_BUFS;
       uint32_t ahead = 0;
-      if (nxt < n) { dma(nxt, bi ^ 1u); ahead = 1; }
+      if (nxt < n) { dma(nxt, bnext); ahead = 1; }
       const uint32_t nn_v = ticket();
-      // cur's DMA has landed once at most (nst + ahead - 1) younger operations
-      // are outstanding (one fewer than counted: a margin of one store)
-      if (!vclear) vm_wait_le(nst + ahead > 0 ? nst + ahead - 1 : 0u);
+      // cur's DMA has landed once at most (younger operations counted - margin)
+      // are outstanding; MOX_DMA_MARGIN fewer than counted: a safety margin of
+      // the oldest stores
+#if MOX_MAP_AHEAD == 2
+      const uint32_t young = nst1 + dm1 + nst + ahead;
+      const bool clear = vclear || vclear1;
+#else
+      const uint32_t young = nst + ahead;
+      const bool clear = vclear;
+#endif
+      const uint64_t tv = cp ? __builtin_amdgcn_s_memtime() : 0;
+#ifndef MOX_DMA_NOWAIT  // (timing experiment only: the row is read without waiting for its DMA)
+      if (!clear) vm_wait_le(__builtin_amdgcn_readfirstlane(young > MOX_DMA_MARGIN ? young - MOX_DMA_MARGIN : 0u));
+#else
+      (void)clear;
+      (void)young;
+#endif
+      if (cp) cp->pb += __builtin_amdgcn_s_memtime() - tv;  // (stamp builds: the counted wait alone)
+#if MOX_MAP_AHEAD == 2
+      nst1 = nst;
+      vclear1 = vclear;
+      dm1 = ahead;
+#endif
       nst = 0;
       vclear = false;
       uint8_t* sl = mybuf + bi * SLOT;
@@ -1176,10 +1375,18 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
       if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge, nst, vclear);
       else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
+#if MOX_MAP_AHEAD == 2
+      cur = nx1;
+      nx1 = nxt;
+#else
       cur = nxt;
+#endif
       nxt_v = nn_v;
+      bi = bi + 1 < MAP_BUFS ? bi + 1 : 0u;
     }
+#endif
     vm_wait_n<0>();  // (every DMA issued was waited for above; nothing may land in LDS after the loop)
+    }
 #ifdef MOX_STAMP
     if (lane == 0 && w.stamps) {
       unsigned long long* o = w.stamps + 8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8;

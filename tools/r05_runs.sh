@@ -54,6 +54,22 @@ slow)
 ab)
   bash tools/ab_kernel.sh "$AB_VARS" "${AB_DBG:-0}" "$AB_KERNELS" ${AB_ARGS:-} > $O/ab.txt 2>&1; rc=$?; cat $O/ab.txt; step ab $rc
   ;;
+mapdiag)
+  # k_map row supply A/B (build variants of tools/build_variant.sh): per-row
+  # consumer cycles (-DMOX_STAMP builds, MOX_DBG=1024) and the supply floor
+  # (-DMOX_ABLATE builds, MOX_DBG=4096: rows released untouched)
+  for v in ${DIAG_STAMP:-ringst selfst}; do
+    mkdir -p $O/$v
+    MOX_LIB=build/var_$v/libmox.so MOX_DBG=1024 MOX_DEBUG_DIR=$O/$v timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 \
+      --no-cpu-baseline > $O/$v.log 2>&1; step "stamps $v" $?
+    echo "$v"; python3 tools/mapcyc.py $O/$v/mapcyc.csv
+  done
+  bash tools/ab_kernel.sh "${DIAG_ABL:-ringabl selfabl}" "4096 0" "k_map" > $O/floor.txt 2>&1; rc=$?; cat $O/floor.txt; step floor $rc
+  ;;
+varc2)
+  # a build variant's C2 table against the oracle (full size, the bench's async mode)
+  MOX_LIB=build/var_${VAR}/libmox.so pyt varc2_$VAR.log 400 tests/test_gpu_scale.py -m gpu -k "async_bench_mode"
+  ;;
 pmc)
   bash tools/pmc_traffic_wl.sh C2 1073741824 ${2:-pmc}_traffic > $O/traffic.txt 2>&1; rc=$?; tail -5 $O/traffic.txt; step traffic $rc
   bash tools/pmc_sq.sh k_map ${2:-pmc}_sqmap > $O/sq_k_map.txt 2>&1; rc=$?; cat $O/sq_k_map.txt; step "sq k_map" $rc
