@@ -734,6 +734,9 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
 template <int TU, int PB = 10>
 __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
                                        uint32_t total, uint32_t& nst) {
+#ifdef MOX_ISA_MARKS  // (ISA reading aid: comment markers around the token pass)
+  asm volatile("; PASS_A begin TU=%0" ::"i"(TU));
+#endif
   const int lane = threadIdx.x & 63;
   constexpr uint32_t LMAX = PB == 10 ? TOKMAX : 2 * TOKMAX;  // list entries (the last is the sink)
   uint32_t e[TU];
@@ -793,6 +796,9 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     if (pos[u] < m.rc) *cold_at(m, b, 0, pos[u]) = key;
     else cold_spill(m, key);
   }
+#ifdef MOX_ISA_MARKS
+  asm volatile("; PASS_A end");
+#endif
 }
 
 // Token pass without a dictionary (high-cardinality input): every list entry
@@ -898,6 +904,9 @@ struct Cyc {
 // rare path), so the next row's DMA has landed.
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
                                        uint16_t* list, struct Cyc* cyc, bool edge, uint32_t& nst, bool& vclear) {
+#ifdef MOX_ISA_MARKS
+  asm volatile("; DO_ROW begin");
+#endif
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
   // lanes 0 and 63 are context only: their starts are cleared with a per-lane
@@ -1004,6 +1013,9 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     }
   }
   wave_lds_fence();
+#ifdef MOX_ISA_MARKS
+  asm volatile("; DO_ROW list done");
+#endif
   if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
     for (uint32_t j = lane; j < total; j += 64) {
       const uint32_t e = list[j];
@@ -3210,6 +3222,10 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       __syncthreads();
       if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the unit
         kk++;
+        // the redo must not see this attempt's keys (red_try reads a slot's key
+        // before its count: only a key that cannot be the one compared may sit
+        // in a slot being claimed)
+        for (int i = tid; i < RED_SLOTS; i += RED_THREADS) s.key[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         if (shift0 + kk > 32) {  // > RED_CAP distinct keys share every hash bit: cannot split
           if (tid == 0) atomicOr(&w.ctl->overflow, OVF_REDUCE);

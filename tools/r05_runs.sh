@@ -46,7 +46,7 @@ parity)
   # the parity subset of the GPU suite (every k_map path: KATs with and without
   # the dictionary, fuzz, tile edges, corpora, huge tokens, misaligned ranges,
   # split partitions, async passes, file ingest, forced collisions)
-  pyt parity.log 600 tests/test_gpu_parity.py tests/test_gpu_collide.py -m "gpu and not slow"
+  pyt parity.log 700 tests/test_gpu_parity.py tests/test_gpu_collide.py tests/test_gpu_exchange.py -m "gpu and not slow"
   ;;
 slow)
   pyt gpu_slow.log 1100 tests -m "gpu and slow"
