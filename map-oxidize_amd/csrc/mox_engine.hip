@@ -1027,6 +1027,9 @@ void mox_engine_destroy(mox_engine* e) {
   for (DevBuf* b : {&e->hx_send, &e->hx_recv}) if (b->p) (void)hipHostFree(b->p);
   dfree(e->d_xcnt);
   dfree(e->d_xcur);
+  dfree(e->d_xs);
+  dfree(e->d_xr);
+  if (e->h_xs) (void)hipHostFree(e->h_xs);
   if (e->h_xcnt) (void)hipHostFree(e->h_xcnt);
   if (e->h_ctl_x) (void)hipHostFree(e->h_ctl_x);
   if (e->h_ctl) (void)hipHostFree(e->h_ctl);

@@ -54,6 +54,9 @@ __global__ void k_mat(Work w, Corpus c);
 __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
 __global__ void k_xpack_short(Work w, WRec* out);
 __global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob);
+__global__ void k_xsample(Work w, uint64_t* out);
+__global__ void k_xcount_r(Work w, XSplit x, XCnt* xcnt);
+__global__ void k_xpack_r(Work w, XSplit x, XDir dir, unsigned long long* cur, WRec* out, uint8_t* blob);
 __global__ void k_xingest(Work w, XDir dir, uint64_t n_short);
 __global__ void k_gather_offs(const uint8_t* recv, GDir d, uint64_t* out);
 }
@@ -168,7 +171,10 @@ struct mox_engine {
   int nranks = 1, rank = 0;
   XCnt* d_xcnt = nullptr;                 // [0, MAX_RANKS) sent, [MAX_RANKS, 2 MAX_RANKS) received
   XCnt* h_xcnt = nullptr;                 // pinned mirror
-  unsigned long long* d_xcur = nullptr;   // 2 MAX_RANKS pack cursors
+  unsigned long long* d_xcur = nullptr;   // 3 MAX_RANKS pack cursors
+  uint64_t* d_xs = nullptr;               // sorted exchange: MAX_RANKS x XS_SAMPLES sampled prefixes sent (one copy per peer)
+  uint64_t* d_xr = nullptr;               // ... and received
+  uint64_t* h_xs = nullptr;               // pinned: every rank's samples
   DevBuf x_send_short, x_send_blob, x_recv_short, x_recv_blob;  // device
   DevBuf hx_send, hx_recv;                // pinned host staging (host transport)
   Ctl* h_ctl_x = nullptr;                 // pinned control block of an exchange pass

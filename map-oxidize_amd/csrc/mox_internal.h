@@ -317,6 +317,29 @@ struct XDir {
   uint64_t hpre[MAX_RANKS + 1];   // prefix of nlong (receive side)
 };
 
+// Sorted exchange (MOX_F_SORT_BYTES at exchange time, mox_multi.hip): words
+// are owned by byte range instead of by hash, so that every rank sorts its own
+// words and the gather in rank order is the bytewise-sorted table.  The owner of
+// a word is the number of splitters <= its first 8 bytes read big-endian (zero
+// padded): bytewise order never decreases that prefix, so owners never decrease
+// along the sorted table.  The splitters are quantiles of sampled prefixes of
+// every rank's local table (the same on every rank).
+constexpr uint32_t XS_SAMPLES = 1024;               // sampled prefixes per rank
+constexpr uint64_t XS_NONE = ~0ull;                 // sample of an empty table (no UTF-8 word starts with 0xFF)
+struct XSplit {
+  uint32_t P;
+  uint64_t sp[MAX_RANKS];       // sp[0 .. P-2]: ascending splitters
+  uint64_t soff[MAX_RANKS];     // first record of destination d in the short send buffer
+};
+__host__ __device__ __forceinline__ uint32_t range_owner(const XSplit& x, uint64_t pre) {
+  uint32_t lo = 0, hi = x.P - 1;  // owner = number of splitters <= pre, in [0, P - 1]
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (x.sp[mid] <= pre) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
 // mox_gather: where source rank s's offsets sit in the root's receive buffer,
 // and the row / byte base of its part of the gathered table.
 struct GDir {

@@ -4276,6 +4276,105 @@ extern "C" __global__ void k_xingest(Work w, XDir dir, uint64_t n_short) {
   if (threadIdx.x == 0 && s_tok) atomicAdd(&w.ctl->tokens, s_tok);  // one global atomic per workgroup
 }
 
+// ---- sorted exchange (byte-range ownership; XSplit, mox_internal.h)
+// The first 8 bytes of table row i, big-endian, zero padded.
+__device__ __forceinline__ uint64_t row_prefix(const Work& w, uint64_t i) {
+  const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;
+  uint64_t k = 0;
+  for (uint32_t j = 0; j < 8 && j < len; j++) k |= (uint64_t)w.t_bytes[o + j] << (56 - 8 * j);
+  return k;
+}
+// XS_SAMPLES prefixes of this rank's local table, evenly over its rows (the
+// table is in hash order, so they are a uniform sample of its distinct words);
+// XS_NONE for an empty table.
+extern "C" __global__ void k_xsample(Work w, uint64_t* out) {
+  const uint64_t n = w.ctl->n_total;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < XS_SAMPLES; j += gridDim.x * blockDim.x)
+    out[j] = n ? row_prefix(w, (uint64_t)j * n / XS_SAMPLES) : XS_NONE;
+}
+// Rows of the local table per block: a contiguous chunk each
+constexpr uint32_t XR_THREADS = 256;
+__device__ __forceinline__ void xr_chunk(uint64_t n, uint64_t& r0, uint64_t& r1) {
+  const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+  r0 = (uint64_t)blockIdx.x * per;
+  r0 = r0 < n ? r0 : n;
+  r1 = r0 + per < n ? r0 + per : n;
+}
+// Per-destination counts of the sorted exchange (xcnt zeroed by the host): short
+// words (table rows < n_short) and long words (the rest), by range owner.  One
+// global atomic per (workgroup, destination) for the short words.
+extern "C" __global__ __launch_bounds__(XR_THREADS) void k_xcount_r(Work w, XSplit x, XCnt* xcnt) {
+  __shared__ uint32_t lc[MAX_RANKS];
+  const uint32_t t = threadIdx.x;
+  if (t < MAX_RANKS) lc[t] = 0;
+  __syncthreads();
+  const uint64_t ns = w.ctl->n_short, n = w.ctl->n_total;
+  uint64_t r0, r1;
+  xr_chunk(n, r0, r1);
+  for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) {
+    const uint32_t d = range_owner(x, row_prefix(w, i));
+    if (i < ns) {
+      atomicAdd(&lc[d], 1u);
+    } else {
+      atomicAdd(&xcnt[d].n_long, 1ull);
+      atomicAdd(&xcnt[d].long_bytes, (unsigned long long)((w.t_offs[i + 1] - w.t_offs[i] + 7) & ~7ull));
+    }
+  }
+  __syncthreads();
+  if (t < x.P && lc[t]) atomicAdd(&xcnt[t].n_short, (unsigned long long)lc[t]);
+}
+// Pack of the sorted exchange: short words as WRec (key = the row's bytes, zero
+// padded) at x.soff[d] + a range the workgroup reserves per destination
+// (cur[d]); long words as XHdr + bytes into destination d's blob (cursors
+// cur[P + d] headers, cur[2 P + d] bytes; their FNV-1a-64 hash recomputed from
+// the bytes, as the map computed it).  cur: 3 P words zeroed by the host.  The
+// order inside a destination is not the row order (the receiver's reduce does
+// not depend on it).
+extern "C" __global__ __launch_bounds__(XR_THREADS) void k_xpack_r(Work w, XSplit x, XDir dir, unsigned long long* cur,
+                                                                 WRec* out, uint8_t* blob) {
+  __shared__ uint32_t lc[MAX_RANKS];
+  __shared__ unsigned long long lb[MAX_RANKS];
+  const uint32_t t = threadIdx.x, P = x.P;
+  if (t < MAX_RANKS) lc[t] = 0;
+  __syncthreads();
+  const uint64_t ns = w.ctl->n_short, n = w.ctl->n_total;
+  uint64_t r0, r1;
+  xr_chunk(ns, r0, r1);  // short rows: counted, then written at the reserved ranges
+  for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) atomicAdd(&lc[range_owner(x, row_prefix(w, i))], 1u);
+  __syncthreads();
+  if (t < P) {
+    lb[t] = lc[t] ? x.soff[t] + atomicAdd(&cur[t], (unsigned long long)lc[t]) : 0ull;
+    lc[t] = 0;
+  }
+  __syncthreads();
+  for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) {
+    const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;
+    uint64_t k0 = 0, k1 = 0;
+    for (uint32_t j = 0; j < len; j++) {  // a short word: at most 16 bytes
+      const uint64_t b = w.t_bytes[o + j];
+      if (j < 8) k0 |= b << (8 * j); else k1 |= b << (8 * (j - 8));
+    }
+    const uint64_t pre = __builtin_bswap64(k0);
+    const uint32_t d = range_owner(x, pre);
+    const uint32_t r = atomicAdd(&lc[d], 1u);
+    out[lb[d] + r] = WRec{k0, k1, w.t_counts[i]};
+  }
+  // long words (rare): one global atomic per word and cursor
+  for (uint64_t i = ns + (uint64_t)blockIdx.x * XR_THREADS + t; i < n; i += (uint64_t)gridDim.x * XR_THREADS) {
+    const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;
+    const uint32_t d = range_owner(x, row_prefix(w, i));
+    uint64_t h = FNV0;
+    for (uint64_t j = 0; j < len; j++) h = fnv_step(h, w.t_bytes[o + j]);
+    h = fnv_finish(h);
+    const uint64_t k = atomicAdd(&cur[P + d], 1ull);
+    const uint64_t bo = atomicAdd(&cur[2 * P + d], (unsigned long long)((len + 7) & ~7ull));
+    uint8_t* base = blob + dir.blob[d];
+    reinterpret_cast<XHdr*>(base)[k] = XHdr{h, len, w.t_counts[i], bo};
+    uint8_t* ob = base + dir.nlong[d] * sizeof(XHdr) + bo;
+    for (uint64_t j = 0; j < len; j++) ob[j] = w.t_bytes[o + j];
+  }
+}
+
 // ------------------------------------------------------------------ gather
 // Root of mox_gather: offsets of the concatenated table.  Row t of the
 // gathered table belongs to source s with base_n[s] <= t < base_n[s + 1];

@@ -185,6 +185,8 @@ int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, co
 //   x_reduce: reduce-only pass over the received partials (synchronous)
 struct XPlan {
   int P = 1;
+  bool ranged = false;  // sorted exchange (MOX_F_SORT_BYTES): byte-range owners, every rank sorts its words
+  XSplit split{};
   uint64_t s_short_off[MAX_RANKS], s_short_len[MAX_RANKS], s_blob_off[MAX_RANKS], s_blob_len[MAX_RANKS];
   uint64_t r_short_off[MAX_RANKS], r_short_len[MAX_RANKS], r_blob_off[MAX_RANKS], r_blob_len[MAX_RANKS];
   uint64_t ns = 0, sb = 0, rs = 0, rb = 0, r_long = 0;
@@ -202,7 +204,7 @@ int x_alloc(mox_engine* e) {
   int rc;
   if (!e->d_xcnt) {
     if ((rc = dalloc(e, (void**)&e->d_xcnt, 2 * MAX_RANKS * sizeof(XCnt)))) return rc;
-    if ((rc = dalloc(e, (void**)&e->d_xcur, 2 * MAX_RANKS * 8))) return rc;
+    if ((rc = dalloc(e, (void**)&e->d_xcur, 3 * MAX_RANKS * 8))) return rc;
     HIPCHK(hipHostMalloc((void**)&e->h_xcnt, 2 * MAX_RANKS * sizeof(XCnt), hipHostMallocDefault));
     HIPCHK(hipHostMalloc((void**)&e->h_ctl_x, sizeof(Ctl), hipHostMallocDefault));
   }
@@ -213,7 +215,10 @@ int x_alloc(mox_engine* e) {
   return MOX_OK;
 }
 
-// Phase 1: k_xcount into the device send rows d_xcnt[0, P).
+// Phase 1: k_xcount into the device send rows d_xcnt[0, P).  Sorted exchange
+// (MOX_F_SORT_BYTES): k_xsample instead, into d_xs (one copy per peer); the
+// caller moves every rank's samples to every rank and calls x_split, which
+// picks the splitters and runs k_xcount_r.
 int x_begin(mox_engine* e, int P) {
   if (int rc = drain_async(e)) return rc;
   if (!e->have_result || !e->res.pass) return fail(MOX_ESTATE, "no local result: mox_run_range first");
@@ -222,10 +227,40 @@ int x_begin(mox_engine* e, int P) {
   if (int rc = x_alloc(e)) return rc;
   XPlan& x = *e->xp;
   x.P = P;
+  x.ranged = (e->flags & MOX_F_SORT_BYTES) != 0;
   x.t0 = std::chrono::steady_clock::now();
   x.local = e->stats;  // the exchange pass reuses the phase events
   HIPCHK(hipMemsetAsync(e->d_xcnt, 0, P * sizeof(XCnt), e->stream));
-  hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, e->stream, e->w, (uint32_t)P, e->d_xcnt);
+  if (x.ranged) {
+    int rc;
+    constexpr size_t SB = (size_t)MAX_RANKS * XS_SAMPLES * 8;
+    if (!e->d_xs && ((rc = dalloc(e, (void**)&e->d_xs, SB)) || (rc = dalloc(e, (void**)&e->d_xr, SB)))) return rc;
+    if (!e->h_xs) HIPCHK(hipHostMalloc((void**)&e->h_xs, SB, hipHostMallocDefault));
+    hipLaunchKernelGGL(k_xsample, dim3(4), dim3(256), 0, e->stream, e->w, e->d_xs);
+    for (int d = 1; d < P; d++)
+      HIPCHK(hipMemcpyAsync(e->d_xs + (size_t)d * XS_SAMPLES, e->d_xs, XS_SAMPLES * 8, hipMemcpyDeviceToDevice, e->stream));
+  } else {
+    hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, e->stream, e->w, (uint32_t)P, e->d_xcnt);
+  }
+  HIPCHK(hipGetLastError());
+  return MOX_OK;
+}
+
+// Sorted exchange: splitters from every rank's samples (all[0, m), the same
+// on every rank, so every rank picks the same ones): P - 1 quantiles of the
+// valid samples; then the per-destination counts by range owner (k_xcount_r).
+int x_split(mox_engine* e, const uint64_t* all, size_t m) {
+  HIPCHK(hipSetDevice(e->device));
+  XPlan& x = *e->xp;
+  std::vector<uint64_t> v;
+  v.reserve(m);
+  for (size_t i = 0; i < m; i++)
+    if (all[i] != XS_NONE) v.push_back(all[i]);
+  std::sort(v.begin(), v.end());
+  x.split = XSplit{};
+  x.split.P = (uint32_t)x.P;
+  for (int i = 0; i + 1 < x.P; i++) x.split.sp[i] = v.empty() ? 0 : v[(size_t)(i + 1) * v.size() / x.P];
+  hipLaunchKernelGGL(k_xcount_r, dim3(1024), dim3(256), 0, e->stream, e->w, x.split, e->d_xcnt);
   HIPCHK(hipGetLastError());
   return MOX_OK;
 }
@@ -269,9 +304,16 @@ int x_pack(mox_engine* e) {
       (rc = grow_dev(e->x_recv_short, x.rs * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_recv_blob, x.rb + 64)))
     return rc;
   hipStream_t s = e->stream;
-  hipLaunchKernelGGL(k_xpack_short, dim3(1024), dim3(256), 0, s, e->w, (WRec*)e->x_send_short.p);
-  HIPCHK(hipMemsetAsync(e->d_xcur, 0, 2 * MAX_RANKS * 8, s));
-  hipLaunchKernelGGL(k_xpack_long, dim3(256), dim3(256), 0, s, e->w, x.sdir, e->d_xcur, (uint8_t*)e->x_send_blob.p);
+  if (x.ranged) {
+    for (int d = 0; d < P; d++) x.split.soff[d] = x.s_short_off[d] / sizeof(WRec);
+    HIPCHK(hipMemsetAsync(e->d_xcur, 0, 3 * MAX_RANKS * 8, s));
+    hipLaunchKernelGGL(k_xpack_r, dim3(1024), dim3(256), 0, s, e->w, x.split, x.sdir, e->d_xcur, (WRec*)e->x_send_short.p,
+                       (uint8_t*)e->x_send_blob.p);
+  } else {
+    hipLaunchKernelGGL(k_xpack_short, dim3(1024), dim3(256), 0, s, e->w, (WRec*)e->x_send_short.p);
+    HIPCHK(hipMemsetAsync(e->d_xcur, 0, 2 * MAX_RANKS * 8, s));
+    hipLaunchKernelGGL(k_xpack_long, dim3(256), dim3(256), 0, s, e->w, x.sdir, e->d_xcur, (uint8_t*)e->x_send_blob.p);
+  }
   HIPCHK(hipGetLastError());
   return MOX_OK;
 }
@@ -279,13 +321,23 @@ int x_pack(mox_engine* e) {
 // Phase 3: the reduce-only pass over the received partials (the local table
 // is no longer needed: buffers may be regrown).  Afterwards this rank owns the
 // final counts of its words.
+// Sorted exchange: this rank's words are a byte range, sorted here (its own
+// GPU, in parallel with the other ranks), so the gather in rank order is the
+// sorted table.  A table the device sort cannot take stays in engine order
+// (the gathered table is then sorted where it is fetched).
 int x_reduce(mox_engine* e) {
   HIPCHK(hipSetDevice(e->device));
   const XPlan& x = *e->xp;
   if (int rc = reduce_received(e, x.rs, x.rb, x.r_long, x.rdir, x.local, x.t0)) return rc;
-  e->stats.x_bytes_sent = x.ns * sizeof(WRec) + x.sb + x.P * sizeof(XCnt);
-  e->stats.x_bytes_recv = x.rs * sizeof(WRec) + x.rb + x.P * sizeof(XCnt);
+  e->stats.x_bytes_sent = x.ns * sizeof(WRec) + x.sb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_SAMPLES * 8 : 0);
+  e->stats.x_bytes_recv = x.rs * sizeof(WRec) + x.rb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_SAMPLES * 8 : 0);
   e->res.exchanged = true;
+  if (x.ranged) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = bsort_table(e);
+    if (rc != MOX_OK && rc != MOX_ENOMEM) return rc;
+    e->stats.ms_sort = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  }
   return MOX_OK;
 }
 
@@ -293,6 +345,17 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   (void)me;
   int rc;
   if ((rc = x_begin(e, P))) return rc;
+  if (e->xp->ranged) {  // every rank's samples to every rank
+    uint64_t off[MAX_RANKS], len[MAX_RANKS];
+    for (int d = 0; d < P; d++) {
+      off[d] = (uint64_t)d * XS_SAMPLES * 8;
+      len[d] = XS_SAMPLES * 8;
+    }
+    if ((rc = T.alltoallv((const uint8_t*)e->d_xs, off, len, (uint8_t*)e->d_xr, off, len))) return rc;
+    HIPCHK(hipMemcpyAsync(e->h_xs, e->d_xr, (size_t)P * XS_SAMPLES * 8, hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(hipStreamSynchronize(e->stream));
+    if ((rc = x_split(e, e->h_xs, (size_t)P * XS_SAMPLES))) return rc;
+  }
   if ((rc = T.counts(e->d_xcnt, e->d_xcnt + MAX_RANKS, e->h_xcnt, e->h_xcnt + MAX_RANKS))) return rc;
   if ((rc = x_pack(e))) return rc;
   const XPlan& x = *e->xp;
@@ -334,7 +397,7 @@ int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
   XCnt* d_recv = e->d_xcnt + MAX_RANKS;
   XCnt* h_send = e->h_xcnt;
   XCnt* h_recv = e->h_xcnt + MAX_RANKS;
-  for (int d = 0; d < P; d++) h_send[d] = XCnt{n, nb, r.tokens, 0};
+  for (int d = 0; d < P; d++) h_send[d] = XCnt{n, nb, r.tokens, r.sorted ? 1ull : 0ull};  // pad: this rank's table is sorted
   HIPCHK(hipMemcpyAsync(d_send, h_send, P * sizeof(XCnt), hipMemcpyHostToDevice, s));
   if ((rc = T.counts(d_send, d_recv, h_send, h_recv))) return rc;
   // 2. this rank's block -> the root
@@ -347,6 +410,7 @@ int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
   }
   uint64_t soff[MAX_RANKS], slen[MAX_RANKS], roff[MAX_RANKS], rlen[MAX_RANKS];
   uint64_t so = 0, ro = 0, N = 0, NBt = 0, tok = 0;
+  bool all_sorted = true;  // every rank sorted its byte range (sorted exchange): the concatenation is sorted
   GDir gd{};
   gd.P = (uint32_t)P;
   for (int d = 0; d < P; d++) {
@@ -363,6 +427,7 @@ int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
     N += bn;
     NBt += bb;
     tok += h_recv[d].long_bytes;
+    all_sorted = all_sorted && h_recv[d].pad != 0;
   }
   gd.base_n[P] = N;
   gd.base_b_total = NBt;
@@ -391,7 +456,7 @@ int gather_impl(mox_engine* e, int P, int me, int root, Transport& T) {
     e->res.tokens = tok;
     e->res.pass = false;
     e->res.exchanged = false;  // gathered: final, not gathered again
-    e->res.sorted = false;
+    e->res.sorted = all_sorted && e->xp && e->xp->ranged;
   } else {
     HIPCHK(hipStreamSynchronize(s));  // the send buffer is reused by the next exchange
     e->res.exchanged = false;  // sent to the root: a table takes part in one gather
@@ -594,6 +659,17 @@ int group_exchange(Group& G) {
   const int P = G.n;
   for (int i = 0; i < P; i++)
     if (int rc = x_begin(G.m[i], P)) return rc;
+  if (G.m[0]->xp->ranged) {  // sorted exchange: every member's samples, read by the host, give every member's splitters
+    std::vector<uint64_t> all((size_t)P * XS_SAMPLES);
+    for (int i = 0; i < P; i++) {
+      HIPCHK(hipSetDevice(G.m[i]->device));
+      HIPCHK(hipMemcpyAsync(G.m[i]->h_xs, G.m[i]->d_xs, XS_SAMPLES * 8, hipMemcpyDeviceToHost, G.m[i]->stream));
+    }
+    if (int rc = sync_members(G)) return rc;
+    for (int i = 0; i < P; i++) std::memcpy(all.data() + (size_t)i * XS_SAMPLES, G.m[i]->h_xs, XS_SAMPLES * 8);
+    for (int i = 0; i < P; i++)
+      if (int rc = x_split(G.m[i], all.data(), all.size())) return rc;
+  }
   if (int rc = group_counts(G)) return rc;
   for (int i = 0; i < P; i++)
     if (int rc = x_pack(G.m[i])) return rc;
@@ -606,11 +682,13 @@ int group_gather(Group& G) {
   const int P = G.n;
   mox_engine* root = G.m[0];
   uint64_t N = 0, NBt = 0, tok = 0, recv_bytes = 0;
+  bool all_sorted = root->xp && root->xp->ranged;  // sorted exchange: the members' sorted ranges in member order
   GDir gd{};
   gd.P = (uint32_t)P;
   for (int i = 0; i < P; i++) {
     const auto& r = G.m[i]->res;
     if (!r.exchanged) return fail(MOX_ESTATE, "member %d has no exchanged table", i);
+    all_sorted = all_sorted && r.sorted;
     gd.roff[i] = 8 * N;  // member i's offsets inside g_recv
     gd.base_n[i] = N;
     gd.base_b[i] = NBt;
@@ -675,7 +753,7 @@ int group_gather(Group& G) {
   res.tokens = tok;
   res.pass = false;
   res.exchanged = false;
-  res.sorted = false;
+  res.sorted = all_sorted;
   root->have_result = true;
   root->stats.gather_bytes = recv_bytes;
   return MOX_OK;
@@ -724,12 +802,18 @@ int group_run(mox_engine* e, const std::vector<Corpus>& c, const std::vector<uin
   const double ms_g = ms_since(t2);
   double ms_s = 0;
   if (e->flags & MOX_F_SORT_BYTES) {
-    // a table too big for the sort's device scratch stays in engine order here:
-    // mox_fetch_table then sorts it on the host, as for one engine
-    const auto t3 = std::chrono::steady_clock::now();
-    rc = bsort_table(e);
-    if (rc != MOX_OK && rc != MOX_ENOMEM) return rc;
-    ms_s = ms_since(t3);
+    if (e->res.sorted) {
+      // sorted exchange: every member sorted its byte range on its own GPU
+      // inside the exchange; the slowest member's sort
+      for (int i = 0; i < G.n; i++) ms_s = std::max(ms_s, G.m[i]->stats.ms_sort);
+    } else {
+      // a table too big for the sort's device scratch stays in engine order here:
+      // mox_fetch_table then sorts it on the host, as for one engine
+      const auto t3 = std::chrono::steady_clock::now();
+      rc = bsort_table(e);
+      if (rc != MOX_OK && rc != MOX_ENOMEM) return rc;
+      ms_s = ms_since(t3);
+    }
   }
   mox_stats& st = e->stats;  // member 0's pass stats are replaced by the group's
   const uint64_t gb = st.gather_bytes;

@@ -32,18 +32,20 @@ def mixed_corpus(n, seed):
     return z[: n // 2] + b" " + u + b"\n" + extra + b" " + z[n // 2:]
 
 
-def run_ranks(data, world, gather_root=None, lib_path=None, stats=None):
+def run_ranks(data, world, gather_root=None, lib_path=None, stats=None, flags=0, table_order=False):
     """Each rank: engine on device 0, its shard, exchange over ThreadAlltoall;
     with gather_root, then the gather of every table into that rank's engine
     (out[root] is then the gathered table, the others their own).  lib_path:
-    a check build; stats: a list that receives every rank's mox_stats."""
+    a check build; stats: a list that receives every rank's mox_stats; flags:
+    the engines' flags (MOX_F_SORT_BYTES: the sorted exchange); table_order:
+    items in the table's own order instead of sorted."""
     x = mdist.ThreadAlltoall(world)
     out, errs = [None] * world, []
 
     def rank_main(r):
         try:
             lo, hi, ob, oe, at_end = mdist.shard_range(len(data), world, r)
-            e = mox.Engine(device=0, lib_path=lib_path)
+            e = mox.Engine(device=0, lib_path=lib_path, flags=flags)
             try:
                 buf = data[lo:hi]
                 d = e.alloc(max(1, len(buf)))
@@ -55,7 +57,7 @@ def run_ranks(data, world, gather_root=None, lib_path=None, stats=None):
                     if gather_root is not None:
                         e.gather_host(world, r, x.fn(r), root=gather_root)
                     t = e.fetch()
-                    out[r] = (t.sorted_items(), t.tokens)
+                    out[r] = (list(t.items()) if table_order else t.sorted_items(), t.tokens)
                     t.close()
                     if stats is not None:
                         stats.append(e.stats())
@@ -302,6 +304,42 @@ def test_world8_threads_c3_path():
     data = c3_like_corpus(world, per, 0x5EED0003)
     assert all(mdist.shard_range(len(data), world, r)[2] in (0, 64) for r in range(world))
     out = run_ranks(data, world, gather_root=0)
+    want, wtok = coracle.count(data, nthreads=16)
+    assert out[0][1] == wtok
+    assert out[0][0] == want
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sorted_exchange_threads(world):
+    """The sorted exchange (MOX_F_SORT_BYTES at exchange time): words are owned
+    by byte range (splitters from every rank's sampled prefixes), every rank
+    sorts its own words, and the gather in rank order is the bytewise-sorted
+    table.  Before the gather: every rank's table is in bytewise order and the
+    ranks' ranges follow each other; after it: the root's table IS the
+    oracle's sorted list, without a sort at the root."""
+    data = mixed_corpus(6 << 20, 60 + world)
+    want, wtok = coracle.count(data)
+    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, table_order=True)
+    for items, tok in out:
+        assert [w for w, _ in items] == sorted(w for w, _ in items)
+        assert sum(c for _, c in items) == tok
+    firsts = [items for items, _ in out if items]
+    assert all(a[-1][0] < b[0][0] for a, b in zip(firsts, firsts[1:]))  # ranges in rank order, disjoint
+    assert len(firsts) >= min(world, 2)  # the splitters spread the words over the ranks
+    assert [x for items, _ in out for x in items] == want
+    stats = []
+    out = run_ranks(data, world, gather_root=0, flags=mox.MOX_F_SORT_BYTES, table_order=True, stats=stats)
+    assert out[0] == (want, wtok)
+    assert all(st["ms_sort"] > 0 for st in stats)
+
+
+def test_sorted_exchange_c3_path_world8():
+    """The sorted exchange on test_world8_threads_c3_path's corpus (8 x 32 MiB,
+    items straddling every cut): the gathered table at rank 0 is the oracle's
+    sorted list, in order."""
+    world, per = 8, 32 << 20
+    data = c3_like_corpus(world, per, 0x5EED0003)
+    out = run_ranks(data, world, gather_root=0, flags=mox.MOX_F_SORT_BYTES, table_order=True)
     want, wtok = coracle.count(data, nthreads=16)
     assert out[0][1] == wtok
     assert out[0][0] == want

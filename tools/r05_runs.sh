@@ -66,6 +66,14 @@ mapdiag)
   done
   bash tools/ab_kernel.sh "${DIAG_ABL:-ringabl selfabl}" "4096 0" "k_map" > $O/floor.txt 2>&1; rc=$?; cat $O/floor.txt; step floor $rc
   ;;
+xsort)
+  # the sorted exchange: exchange + group tests, the C3 2 x 8 GiB group test,
+  # and the N = 2 engine-group bench line (2 x 8 GiB C3 shards on GPU 0)
+  pyt xsort_tests.log 900 tests/test_gpu_exchange.py tests/test_gpu_group.py -m "gpu and not slow"
+  pyt xsort_c3.log 900 tests/test_gpu_scale.py -m gpu -k "c3_group"
+  timeout -k 10 400 python -u bench.py --gpus 2 --xport host --device 0 --steps 3 --warmup 1 > $O/n2.json 2> $O/n2.err; step "bench n2" $?
+  python3 -c "import json;d=json.load(open('$O/n2.json'));print(d['value'],d['phases_ms'],d.get('hash_order'))"
+  ;;
 varc2)
   # a build variant's C2 table against the oracle (full size, the bench's async mode)
   MOX_LIB=build/var_${VAR}/libmox.so pyt varc2_$VAR.log 400 tests/test_gpu_scale.py -m gpu -k "async_bench_mode"
