@@ -13,8 +13,8 @@ copied to HBM before timing.
 With --gpus N > 1 and no torchrun environment, ONE process drives all N GPUs
 through an engine group (mox_config.n_gpus, include/mox.h): a step is one
 mox_run_shards call (local passes on all GPUs at once, the all-to-all as one
-RCCL group over the members' communicators, per-owner reduce, gather and the
-bytewise sort of the result on GPU 0).  Under torchrun (RANK / WORLD_SIZE
+RCCL group over the members' communicators, per-owner reduce and bytewise sort
+of every member's byte range on its own GPU, gather in member order).  Under torchrun (RANK / WORLD_SIZE
 set) every rank is one process per GPU (mox_comm_init, mox_exchange,
 mox_gather); rank 0 prints the line.
 
@@ -189,10 +189,11 @@ def roofline_fields(per_rank, map_avg, workload, traffic_json):
 def main_group(a):
     """--gpus N > 1 without torchrun: one process, one engine group over N GPUs.
     A timed step is one mox_run_shards call with MOX_F_SORT_BYTES: local passes,
-    exchange, per-owner reduce, gather at GPU 0 and the bytewise sort of the
-    gathered table (north_star: "a gather of the sorted result").  The same K
-    steps without the sort (gathered table in engine / hash order) are timed
-    after them and reported beside the value."""
+    the sorted exchange (words owned by byte range), per-owner reduce and
+    bytewise sort on every member's GPU, and the gather at GPU 0 in member
+    order, which is then the sorted table (north_star: "a gather of the sorted
+    result").  The same K steps without the sort (hash-owned exchange, gathered
+    table in engine order) are timed before them and reported beside the value."""
     n = a.gpus
     if not a.workload:
         a.workload = "C3"
@@ -261,8 +262,8 @@ def main_group(a):
         "data": "synthetic: mox_corpus kind=%d seed=%#x (%s, host-generated, copied to HBM before timing)"
                 % (kind, seed, KIND_DESC.get(kind, "?")),
         "config": {"workload": desc, "bytes_per_gpu": per_rank, "total_bytes": total,
-                   "parallelism": "dp%d byte-range shards + %s all-to-all + gather and bytewise sort at GPU 0 "
-                                  "(one process, engine group%s)" % (
+                   "parallelism": "dp%d byte-range shards + %s all-to-all (byte-range owners) + bytewise sort per "
+                                  "GPU + gather in member order at GPU 0 (one process, engine group%s)" % (
                                       n, "RCCL" if xport == mox.XPORT_RCCL else "device-copy",
                                       "" if n_dev == n else "; %d members on %d GPU(s)" % (n, n_dev))},
         "words_per_s": round(last["tokens"] / (elapsed / a.steps), 1),
@@ -292,7 +293,8 @@ def main_group(a):
             "gather_ms": mean(rows, "ms_gather"),
             "gather_bytes": int(last["gather_bytes"]),
             "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens,
-                               "order": "bytewise (device sort on GPU 0 inside the timed step)"},
+                               "order": "bytewise (sorted exchange: each member sorts its byte range on its GPU "
+                                        "inside the timed step; sort_bytes = the slowest member's sort)"},
         },
         "check_sum_counts_eq_tokens": ok,
         "cpu_baseline": None,
@@ -350,6 +352,12 @@ def main():
     use_async = world == 1 and not a.sync_passes
 
     gather = world > 1 and not a.no_gather
+    if gather:
+        # the sorted result (north_star: "a gather of the sorted result"): the
+        # sorted exchange (MOX_F_SORT_BYTES: words owned by byte range, every
+        # rank sorts its own range on its GPU), so the gather at rank 0 is
+        # already in bytewise order and sort_result() there finds nothing to do
+        eng.set_flags(base_flags | mox.MOX_F_TIMING_MAP | mox.MOX_F_SORT_BYTES)
 
     def step(sync=False, sort=True):
         if use_async and not sync:
@@ -391,9 +399,10 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    sort_ms = eng.stats()["ms_sort"] if gather and rank == 0 else 0.0
+    sort_ms = eng.stats()["ms_sort"] if gather else 0.0  # this rank's sort of its byte range (sorted exchange)
     el_hash = None
     if world > 1 and gather:  # the same steps without the sort, reported beside the value
+        eng.set_flags(base_flags | mox.MOX_F_TIMING_MAP)  # hash-owned exchange, gathered table in engine order
         if dist:
             dist.barrier()
         t1 = time.perf_counter()
@@ -446,7 +455,7 @@ def main():
         # exchange's; the local pass counted what this rank's shard holds)
         loc = torch.tensor([float(local_tokens(eng, d_buf, hi - lo, own_b, own_e, at_end)), last["x_bytes_sent"],
                             last["x_bytes_recv"], statistics.mean(xms) if xms else 0.0,
-                            statistics.mean(gms) if gms else 0.0], dtype=torch.float64)
+                            statistics.mean(gms) if gms else 0.0, sort_ms], dtype=torch.float64)
         rows = [torch.zeros_like(loc) for _ in range(world)]
         dist.all_gather(rows, loc)
         rows = [r.tolist() for r in rows]
@@ -463,13 +472,14 @@ def main():
             "exchange_ms_max_over_ranks": round(max(r[3] for r in rows), 4),
             "gather_ms_max_over_ranks": round(max(r[4] for r in rows), 4) if gather else None,
             "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens,
-                               "order": "bytewise (mox_sort_result on rank 0's GPU inside the timed step)"} if gather else None,
-            "sort_bytes_ms_rank0": round(sort_ms, 4) if gather else None,
+                               "order": "bytewise (sorted exchange: every rank sorts its byte range inside the timed "
+                                        "step, the gather concatenates in rank order)"} if gather else None,
+            "sort_bytes_ms_max_over_ranks": round(max(r[5] for r in rows), 4) if gather else None,
             "hash_order": {"value": round(total / (el_hash / a.steps) / 1e9, 3), "ms_per_step": round(el_hash / a.steps * 1e3, 4),
                            "note": "the same steps without the sort at rank 0"} if el_hash else None,
-            "note": "exchange = counts all-to-all + pack + payload all-to-all (RCCL send/recv in one group) + "
-                    "reduce-only pass; gather = every rank's final table to rank 0 (mox_gather), then the bytewise "
-                    "device sort at rank 0 (mox_sort_result), both inside the timed step",
+            "note": "exchange = sampled byte-range splitters + counts all-to-all + pack + payload all-to-all "
+                    "(RCCL send/recv in one group) + reduce-only pass + the rank's bytewise sort of its range; "
+                    "gather = every rank's sorted table to rank 0 (mox_gather) in rank order, inside the timed step",
         }
     else:
         tokens_all = last["tokens"]

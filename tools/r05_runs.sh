@@ -78,6 +78,10 @@ varc2)
   # a build variant's C2 table against the oracle (full size, the bench's async mode)
   MOX_LIB=build/var_${VAR}/libmox.so pyt varc2_$VAR.log 400 tests/test_gpu_scale.py -m gpu -k "async_bench_mode"
   ;;
+stages)
+  # k_map SQ instruction counts per ablation stage (tools/pmc_map_stages.sh, build/var_abl)
+  bash tools/pmc_map_stages.sh ${2:-stages} "${STAGES:-4096 1 2 8 16 0}" > $O/stages.txt 2>&1; rc=$?; cat $O/stages.txt; step stages $rc
+  ;;
 pmc)
   bash tools/pmc_traffic_wl.sh C2 1073741824 ${2:-pmc}_traffic > $O/traffic.txt 2>&1; rc=$?; tail -5 $O/traffic.txt; step traffic $rc
   bash tools/pmc_sq.sh k_map ${2:-pmc}_sqmap > $O/sq_k_map.txt 2>&1; rc=$?; cat $O/sq_k_map.txt; step "sq k_map" $rc
