@@ -87,7 +87,8 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   Work n = e->w;
   // a multiple of 2 QF_MAX: every one of a region's QF_MAX slices holds an even
   // number of records, so k_map's paired records stay sector-aligned
-  n.cold_cap = (uint32_t)std::min<uint64_t>((c.cold_cap + 2 * QF_MAX - 1) & ~(uint64_t)(2 * QF_MAX - 1), 0xFFFFFFF0u);
+  n.cold_cap = (uint32_t)std::min<uint64_t>((c.cold_cap + 2 * QF_MAX - 1) & ~(uint64_t)(2 * QF_MAX - 1), COLD_CAP_MAX);
+  static_assert(COLD_CAP_MAX % (2 * QF_MAX) == 0 && COLD_CAP_MAX < (1u << 24), "cold_cap clamp (k_map: __umul24)");
   n.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
   n.w_cap = c.w_cap;
   n.u_cap = c.u_cap;
@@ -426,6 +427,7 @@ void set_result(mox_engine* e, const Ctl& h) {
 // Check builds (-DMOX_CHECK): a device bounds check failed during the pass
 // (mox_internal.h, MOX_CHK).  Production builds never fail here.
 int check_failed(const Ctl& h) {
+  if (h.layout_err) return fail(MOX_EHIP, "k_map: dynamic LDS does not start at address 0 (static LDS in the kernel?)");
 #ifdef MOX_CHECK
   if (h.dbg_cnt[0])
     return fail(MOX_EHIP, "device bounds check failed %llu times (largest site id %llu)", h.dbg_cnt[0], h.dbg_cnt[1]);

@@ -81,15 +81,24 @@ static_assert(!MOX_MAP_PAIR || (MOX_MAP_SELF && MOX_MAP_AHEAD == 1), "row pairs:
 constexpr int MAP_BUFS = MAP_AHEAD + 1;     // row buffers per wave
 static_assert(MAP_AHEAD == 1 || MAP_AHEAD == 2, "k_map rows ahead");
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
+// A k_map token list: up to TOKMAX entries of a row, then 64 entries of tail
+// (LIST_ODD, written after every row's list) that the token pass reads past
+// the row's last entry instead of bounds-checking every batch
+constexpr int LIST_N = TOKMAX + 64;
 constexpr int NB_LOG2 = 10;                 // cold-record partitions (hash top bits)
 constexpr int NB = 1 << NB_LOG2;
+// k_map addresses a workgroup's NB x cold_cap cold records with 32-bit byte
+// offsets (cold_at); a bigger region would need more than 4 GiB per workgroup
+// (4 MiB x cold_cap over 256 workgroups: past HBM long before), and records past a
+// region's end spill, so the host clamps cold_cap here
+constexpr uint64_t COLD_CAP_MAX = (1ull << 32) / (16ull * NB);
 constexpr uint32_t QF_MAX = 4;              // most cold regions per (map workgroup, partition) (k_map without a dictionary)
 // k_map dynamic LDS (carved in this order by k_map): dictionary counts, region
 // counters, misc, key selectors, dictionary keys, then the row supply (per-wave
 // row buffers, or the ring with its ready / free words) and the token lists
 constexpr size_t MAP_LDS_BYTES = (size_t)DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 +
                                  (MOX_MAP_SELF ? (size_t)MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT : (size_t)RING * 8 + (size_t)RING * SLOT) +
-                                 (size_t)MAP_ROW_WAVES * 2 * TOKMAX * MAP_PAIRW;
+                                 (size_t)MAP_ROW_WAVES * 2 * LIST_N * MAP_PAIRW;
 static_assert(MAP_LDS_BYTES <= 160 * 1024, "k_map LDS over 160 KiB");
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;
@@ -193,6 +202,7 @@ struct Ctl {
   unsigned long long n_mid;       // entries of mid_units (k_reduce_sort2 work list)
   unsigned long long n_small;     // entries of small_units (k_reduce_small work list)
   unsigned long long paths[8];    // PATH_* hit counters (MOX_PATHS builds only; zero otherwise)
+  unsigned long long layout_err;  // k_map: its dynamic LDS did not start at address 0 (mox_kernels.hip L_*)
 };
 
 // ---- forced-collision check build (libmox_hc.so, `make hc`)

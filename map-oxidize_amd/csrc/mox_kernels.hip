@@ -257,6 +257,25 @@ __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2
   // key hashing to 0 would spin on a "free" slot); 1 simply shares its hash
   return max(collide32(a, MOX_H32_BITS), 1u);  // collide32: identity except in the collision build
 }
+// k_map's token passes: hash32 without the max (one VALU instruction per key
+// less).  It differs from hash32 only where hash32 is 1 and this is 0, which
+// give the same partition (top bits) and dictionary slots (dict_s1 / dict_s2 of
+// 0 and 1 are both 0), so cold records and dictionary probes agree with every
+// other kernel; where k_map stores the hash itself (note_sample: 0 = no
+// record) it takes the max.  (Setting bit 0 instead, (a ^ a >> 13) | 1 in one
+// v_bitop3, changed the low bits k_reduce's slot choice uses: k_reduce +4 %.)
+__device__ __forceinline__ uint32_t hash32_map(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+#ifdef MOX_HASH_COLLIDE
+  return hash32(k0, k1, k2, k3);
+#else
+  uint32_t a = __builtin_amdgcn_bitop3_b32(k0, __builtin_rotateleft32(k1, 11), __builtin_rotateleft32(k2, 21), 0x96);
+  a ^= __builtin_rotateleft32(k3, 6);
+  a *= 0x9E3779B1u;
+  a ^= a >> 15;
+  a *= 0x85EBCA6Bu;
+  return a ^ (a >> 13);
+#endif
+}
 __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
   return hash32((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
 }
@@ -297,6 +316,15 @@ __device__ __forceinline__ uint32_t key_len16(uint4 k) {
 // tags, no second probe pass.
 __device__ __forceinline__ uint32_t dict_s1(uint32_t h) { return ((h & 0xFFFFu) * (uint32_t)DICT_SLOTS) >> 16; }
 __device__ __forceinline__ uint32_t dict_s2(uint32_t h) { return ((h >> 16) * (uint32_t)DICT_SLOTS) >> 16; }
+// k_map's token pass: a slot's key byte offset (16 B keys), dict_s1 / dict_s2
+// scaled, from the fastrange product p in one v_lshlrev_b32_sdwa ((p >> 16) << 4:
+// the shift reads p's high half).  Left to the compiler it took two
+// instructions, since the slot also addressed the count array.
+__device__ __forceinline__ uint32_t slot_off16(uint32_t p) {
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(r) : "v"(p));
+  return r;
+}
 
 // LDS pair slot states (k_map without a dictionary, k_split_scatter): a
 // record waits in its slot until the next record for the same region arrives,
@@ -308,10 +336,37 @@ struct MapLds {
   uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's space)
   uint32_t* misc;   // [0] spills [1] row ticket
   uint4* seltab;    // [KSEL_N]: v_perm selectors of a len-byte key at byte offset sh (entry 4 len + sh)
+  uint32_t kmask;   // 0x3FC in a VGPR (key_load's v_bitop3_b32 takes no literal)
   // no dictionary (dict_n == 0): pair slots per region, inside dkey's space
   uint4* pend;      // NB x qf parked records
   uint32_t* pst;    // NB x qf slot states (PS_*)
 };
+
+// k_map LDS layout: byte offsets from the dynamic LDS base, which is address 0
+// (k_map has no static LDS; checked at entry, Ctl::layout_err).  As constants
+// the compiler folds them into the LDS instructions' 16-bit offset field (from
+// the extern array's symbol it added the base per access, v_add_u32 v, 0, v).
+// The row supply comes first, so every row slot (row pair) is SLOT-aligned and
+// key_load ORs a token's 4-aligned offset into its slot address (v_and_or_b32).
+constexpr uint32_t L_ROWS = 0;
+constexpr uint32_t L_ROWS_BYTES = MOX_MAP_SELF ? MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT : RING * SLOT;
+constexpr uint32_t L_DCNT = L_ROWS + L_ROWS_BYTES;
+constexpr uint32_t L_BCNT = L_DCNT + DICT_SLOTS * 4;
+constexpr uint32_t L_MISC = L_BCNT + NB * 4;
+constexpr uint32_t L_SELTAB = L_MISC + 16;
+constexpr uint32_t L_DKEY = L_SELTAB + KSEL_N * 16;
+constexpr uint32_t L_RFLAGS = L_DKEY + DICT_SLOTS * 16;  // ring only: ready[RING], free[RING]
+constexpr uint32_t L_LISTS = L_RFLAGS + (MOX_MAP_SELF ? 0u : RING * 8u);
+static_assert(L_LISTS + (size_t)MAP_ROW_WAVES * 2 * LIST_N * MAP_PAIRW == MAP_LDS_BYTES, "k_map LDS layout");
+static_assert(L_ROWS % (SLOT * MAP_PAIRW) == 0 && (SLOT & (SLOT - 1)) == 0, "row slots aligned to their size");
+static_assert(L_DCNT % 16 == 0 && L_SELTAB % 16 == 0 && L_DKEY % 16 == 0 && L_LISTS % 16 == 0, "LDS table alignment");
+typedef __attribute__((address_space(3))) uint8_t LdsByte;
+// LDS address of a generic pointer into LDS, and a pointer from an LDS address
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(const LdsByte*)p; }
+template <class T>
+__device__ __forceinline__ T* lds_ptr(uint32_t a) {
+  return (T*)(__attribute__((address_space(3))) T*)(uintptr_t)a;
+}
 
 typedef const __attribute__((address_space(4))) Work* KWork;  // constant (kernarg) address space: scalar loads
 struct MapCtx {
@@ -323,12 +378,17 @@ struct MapCtx {
   uint32_t qf, qb;   // regions per partition (QF, 1 with a dictionary) and log2(qf)
   uint32_t rg, rc;   // regions per partition over the grid (qf map_grid), records per region (cold_cap / qf)
   uint4* wcold;      // this workgroup's first region (q = 0, b = 0): cold + blockIdx qf NB rc
+  uint32_t keep;     // do_row: ~0 in lanes 1..62, 0 in the context lanes 0 and 63 (opaque VGPR)
 };
 // Record pos of this workgroup's region q of partition b: one 64-bit
 // multiply-add and one address add from the workgroup's region base (the
 // full region index needed four more instructions per cold store)
+// A workgroup's regions span NB cold_cap records (cold_cap <= COLD_CAP_MAX), so
+// the byte offset fits 32 bits: one v_mad_u32_u24 and a shift, and the store
+// takes the 64-bit base from SGPRs (a v_mad_u64_u32 and two v_lshl_add_u64 in
+// 64-bit form)
 __device__ __forceinline__ uint4* cold_at(const MapCtx& m, uint32_t b, uint32_t q, uint32_t pos) {
-  return m.wcold + ((uint64_t)(q * NB + b) * m.rc + pos);
+  return reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(m.wcold) + ((__umul24(q * NB + b, m.rc) + pos) << 4));
 }
 // Work fields of the rare paths (spills, Unicode lane, long words, error
 // flags), loaded where they are used: the opaque pointer keeps the compiler from
@@ -441,7 +501,7 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
         } else {
           if (pos < SPLIT_PER_REGION) {
             note_sample(m, b, qr, pos, hash32(q.x, q.y, q.z, q.w));
-            note_sample(m, b, qr, pos + 1, h);
+            note_sample(m, b, qr, pos + 1, max(h, 1u));  // (h: hash32_map)
           }
           if (pos + 1 < m.rc) {
             uint4* o = cold_at(m, b, qr, pos);
@@ -468,13 +528,13 @@ __device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t 
     if (!MOX_ABL(m.w.dbg, DBG_NOPAIR)) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key, nst); return; }
     const uint32_t B = h >> (32 - NB_LOG2 - m.qb), qr = B & (m.qf - 1);
     const uint32_t pos = atomicAdd(&m.s.bcnt[B], 1u);
-    if (pos < SPLIT_PER_REGION) note_sample(m, b, qr, pos, h);
+    if (pos < SPLIT_PER_REGION) note_sample(m, b, qr, pos, max(h, 1u));  // (h: hash32_map)
     if (pos < m.rc) *cold_at(m, b, qr, pos) = key;
     else cold_spill(m, key);
     return;
   }
   const uint32_t pos = atomicAdd(&m.s.bcnt[b], 1u);
-  if (pos < SPLIT_PER_REGION) note_sample(m, b, 0, pos, h);
+  if (pos < SPLIT_PER_REGION) note_sample(m, b, 0, pos, max(h, 1u));  // (h: hash32_map)
   if (pos < m.rc) {
     *cold_at(m, b, 0, pos) = key;
     return;
@@ -566,7 +626,11 @@ __device__ __forceinline__ uint32_t zero_mask16(uint4 v) {
 // operations: the 64-bit form's constant pairs were held in SGPRs across the
 // k_map row loop and spilled (a VGPR-lane reload and write-back per row)
 __device__ __forceinline__ uint32_t lower4(uint32_t x) {
-  return x | ((((x + 0x3F3F3F3Fu) & ~(x + 0x25252525u)) & 0x80808080u) >> 2);
+  // upper-case flag in bit 7 of each byte (x + 0x3F >= 0x80 and x + 0x25 < 0x80):
+  // the two sums and their AND with the byte mask in one v_bitop3_b32 (5 VALU
+  // instructions per dword instead of 6)
+  const uint32_t up = __builtin_amdgcn_bitop3_b32(x + 0x3F3F3F3Fu, ~(x + 0x25252525u), 0x80808080u, 0x80);
+  return x | (up >> 2);
 }
 __device__ __forceinline__ uint4 lower16(uint4 v) { return make_uint4(lower4(v.x), lower4(v.y), lower4(v.z), lower4(v.w)); }
 // Whole-wave lane shifts by one on the VALU (DPP wave_shl:1 / wave_shr:1; gfx9
@@ -663,12 +727,21 @@ struct KeyLd {
 // whose two slots are adjacent in LDS), the length field above them
 template <int PB = 10>
 __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf, uint32_t e, KeyLd& r) {
-  const uint32_t pos = e & ((1u << PB) - 1u);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(rowbuf + (pos & ~3u));
+  (void)s;
+  // rowbuf is a row slot (row pair), aligned to its size (L_ROWS): the 4-aligned
+  // token offset ORs in, (e & mask) | slot in one v_bitop3_b32 (truth table 0xEA)
+  static_assert(((1u << PB) - 1u & ~3u) == (PB == 10 ? 0x3FCu : 0x7FCu), "key offset mask");
+  const uint32_t* q = lds_ptr<const uint32_t>(
+      PB == 10 ? __builtin_amdgcn_bitop3_b32(e, s.kmask, lds_addr(rowbuf), 0xEA) : (lds_addr(rowbuf) | (e & 0x7FCu)));
 #pragma unroll
   for (int i = 0; i < 5; i++) r.E[i] = q[i];
-  // (entry 4 len + (pos & 3), as a byte offset straight from the list entry)
-  r.S = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(s.seltab) + (((e >> (PB - 6)) & 0x7C0u) | ((pos & 3u) << 4)));
+  // (entry 4 len + (pos & 3), as a byte offset straight from the list entry:
+  // bits 6.. from len (e >> (PB - 6); nothing above it in a 16-bit entry) and
+  // bits 0..5 from e << 4 (pos & 3 in bits 4..5, zero below): bit i = bit i of
+  // 63 ? (e << 4) : (e >> (PB - 6)), one v_bitop3_b32 with an inline constant
+  // (truth table 0xD8).  An odd entry's offset may pass the table's end: it
+  // reads other LDS, unused.)
+  r.S = *lds_ptr<const uint4>(L_SELTAB + __builtin_amdgcn_bitop3_b32(e >> (PB - 6), e << 4, 63u, 0xD8));
 }
 __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
   (void)e;
@@ -714,7 +787,15 @@ __device__ __forceinline__ void after_fence(uint32_t (&v)[TU]) {
 // builtin keeps the combiner from splitting it into four compares and a
 // boolean tree, and (unlike inline asm, which it replaces) lets the scheduler
 // interleave the chains without a wait state after every step.
+#ifndef MOX_EQ64
+#define MOX_EQ64 0  // 1: two v_cmp_eq_u64 per key compare (lane masks ANDed on the SALU)
+#endif
 __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
+#if MOX_EQ64
+  const uint64_t a0 = ((uint64_t)k.y << 32) | k.x, a1 = ((uint64_t)k.w << 32) | k.z;
+  const uint64_t b0 = ((uint64_t)K[1] << 32) | K[0], b1 = ((uint64_t)K[3] << 32) | K[2];
+  return (a0 == b0) & (a1 == b1);
+#endif
   uint32_t d = k.x ^ K[0];
   d = __builtin_amdgcn_bitop3_b32(k.y, K[1], d, 0xBE);
   d = __builtin_amdgcn_bitop3_b32(k.z, K[2], d, 0xBE);
@@ -730,40 +811,51 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
 // zero, so nothing hits), but that case takes pass_c.
 // nst counts the cold-store instructions the wave issues (one per batch in
 // which any lane stores a record; spills and samples are extra), for the
-// counted wait on the next row's DMA (k_map, MOX_MAP_SELF).
+// counted wait on the next row's DMA (k_map, MOX_MAP_SELF).  nvalid counts the
+// entries taken (SALU: the valid masks' bit counts); fewer than the row's
+// total means odd entries for the generic walk (do_row).
+// A one-row list (PB 10) is read past its last entry into the LIST_ODD tail
+// (LIST_N; the batch sizes keep j < total + 64), so the reads need neither a
+// bounds clamp nor an inactive-lane select.
 template <int TU, int PB = 10>
 __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t total, uint32_t& nst) {
+                                       uint32_t total, uint32_t& nst, uint32_t& nvalid) {
 #ifdef MOX_ISA_MARKS  // (ISA reading aid: comment markers around the token pass)
   asm volatile("; PASS_A begin TU=%0" ::"i"(TU));
 #endif
   const int lane = threadIdx.x & 63;
-  constexpr uint32_t LMAX = PB == 10 ? TOKMAX : 2 * TOKMAX;  // list entries (the last is the sink)
   uint32_t e[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const uint32_t j = j0 + u * 64 + lane;
-    e[u] = list[j < LMAX ? j : LMAX - 1];
+    if constexpr (PB == 10) {
+      e[u] = list[j];
+    } else {
+      constexpr uint32_t LMAX = 2 * TOKMAX;  // row-pair list entries (the last is the sink)
+      e[u] = list[j < LMAX ? j : LMAX - 1];
+    }
   }
   SCHED_FENCE();  // every batch's list read in flight before the first is used
+  if constexpr (PB != 10) {
 #pragma unroll
-  for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : (17u << PB);  // inactive = odd (slot offset 0)
+    for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : (17u << PB);  // inactive = odd (slot offset 0)
+  }
   KeyLd ld[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) key_load<PB>(m.s, rowbuf, e[u], ld[u]);
   SCHED_FENCE();
   AFTER_FENCE(e);
-  uint32_t K[TU][4], h[TU], s1[TU], s2[TU];
+  uint32_t K[TU][4], h[TU], s1[TU], s2[TU];  // s1, s2: the two slots' key byte offsets (16 s)
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     key_make(e[u], ld[u], K[u]);
-    h[u] = hash32(K[u][0], K[u][1], K[u][2], K[u][3]);
-    s1[u] = dict_s1(h[u]);
-    s2[u] = dict_s2(h[u]);
+    h[u] = hash32_map(K[u][0], K[u][1], K[u][2], K[u][3]);
+    s1[u] = slot_off16((h[u] & 0xFFFFu) * (uint32_t)DICT_SLOTS);  // 16 dict_s1(h)
+    s2[u] = slot_off16((h[u] >> 16) * (uint32_t)DICT_SLOTS);      // 16 dict_s2(h)
   }
   uint4 d1[TU], d2[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) { d1[u] = m.s.dkey[s1[u]]; d2[u] = m.s.dkey[s2[u]]; }
+  for (int u = 0; u < TU; u++) { d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]); d2[u] = *lds_ptr<const uint4>(L_DKEY + s2[u]); }
   SCHED_FENCE();
   // hits count in LDS; every miss reserves its region slot (the LDS returning
   // atomics of all batches issued together), then the misses are stored
@@ -772,9 +864,10 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     const bool valid = e[u] < (17u << PB);  // LIST_ODD of the format
+    nvalid += (uint32_t)__popcll(__ballot(valid));
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
     miss[u] = valid & !(hit1 | hit2);
-    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[hit1 ? s1[u] : s2[u]], 1u);
+    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
 #if defined(MOX_PATHS) && MOX_PATHS
     if (miss[u]) {
       if ((d1[u].x | d1[u].y | d1[u].z | d1[u].w) && hash32(d1[u].x, d1[u].y, d1[u].z, d1[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
@@ -783,16 +876,27 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 #endif
   }
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) return;
+  // (a dictionary pass: the region counters are at L_BCNT, an immediate offset;
+  // pos and bk are read under miss only.  The partition is computed once and
+  // kept opaque: the compiler otherwise formed the counter address from h
+  // directly and shifted h again for the store.)
+  uint32_t bk[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) pos[u] = miss[u] ? atomicAdd(&m.s.bcnt[bucket_of(h[u])], 1u) : 0u;
+  for (int u = 0; u < TU; u++) {
+    if (miss[u]) {
+      bk[u] = bucket_of(h[u]);
+      asm("" : "+v"(bk[u]));
+      pos[u] = atomicAdd(lds_ptr<uint32_t>(L_BCNT + 4 * bk[u]), 1u);
+    }
+  }
   SCHED_FENCE();
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     nst += __any(miss[u] && pos[u] < m.rc) ? 1u : 0u;
     if (!miss[u]) continue;
-    const uint32_t b = bucket_of(h[u]);
+    const uint32_t b = bk[u];
     const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
-    if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, 0, pos[u], h[u]);
+    if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, 0, pos[u], max(h[u], 1u));  // (hash32_map)
     if (pos[u] < m.rc) *cold_at(m, b, 0, pos[u]) = key;
     else cold_spill(m, key);
   }
@@ -803,19 +907,17 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 
 // Token pass without a dictionary (high-cardinality input): every list entry
 // straight to the cold path.
+// (list read into its LIST_ODD tail as in pass_a; nvalid likewise)
 template <int TU>
 __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t total, uint32_t& nst) {
+                                       uint32_t& nst, uint32_t& nvalid) {
   const int lane = threadIdx.x & 63;
   uint32_t e[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) {
-    const uint32_t j = j0 + u * 64 + lane;
-    e[u] = list[j < TOKMAX ? j : TOKMAX - 1];
-  }
+  for (int u = 0; u < TU; u++) e[u] = list[j0 + u * 64 + lane];
   SCHED_FENCE();  // every batch's list read in flight before the first is used
 #pragma unroll
-  for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : 0x8000u;  // inactive = odd
+  for (int u = 0; u < TU; u++) nvalid += (uint32_t)__popcll(__ballot(e[u] < LIST_ODD));
   KeyLd ld[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
@@ -828,7 +930,7 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
   for (int u = 0; u < TU; u++) {
     if (e[u] >= LIST_ODD) continue;
     const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
-    cold_word(m, hash32(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1, &nst);
+    cold_word(m, hash32_map(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1, &nst);
   }
 }
 
@@ -884,6 +986,24 @@ __device__ __forceinline__ void vm_wait_le(uint32_t n) {
   }
 }
 
+// The byte flags (bit 7 of every byte) of two dwords f0, f1 into byte 3: f0's
+// bytes k at bit 24 + k, f1's at 28 + k.  t holds f0's flags at 3 + 8 k and
+// f1's at 7 + 8 k; copies shifted by 21 - 7 k land byte k's pair in byte 3,
+// and no other flag reaches byte 3 (one v_lshrrev, one v_or, three
+// v_lshl_or_b32; the former shift-right form took about 9)
+__device__ __forceinline__ uint32_t gather8(uint32_t f0, uint32_t f1) {
+  const uint32_t t = (f0 >> 4) | f1;
+  // (as asm: left to itself the compiler folds the three into a v_mul_lo_u32 by
+  // 0x204080, a quarter-rate instruction)
+  uint32_t r;
+  asm("v_lshl_or_b32 %0, %1, 7, %1\n\tv_lshl_or_b32 %0, %0, 7, %1\n\tv_lshl_or_b32 %0, %0, 7, %1" : "=&v"(r) : "v"(t));
+  return r;
+}
+// the 16 byte flags of a lane's 4 dwords into bits 0..15 (bit i = byte i)
+__device__ __forceinline__ uint32_t gather16(const uint32_t (&wsd)[4]) {
+  return __builtin_amdgcn_perm(gather8(wsd[2], wsd[3]), gather8(wsd[0], wsd[1]), 0x0C0C0703u);
+}
+
 // per-phase cycle accounting of a map consumer wave (-DMOX_STAMP builds only)
 struct Cyc {
   uint64_t wait, byte, pa, pb, miss, rows;
@@ -910,35 +1030,39 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   const int lane = threadIdx.x & 63;
   const uint64_t p0 = sbase + (uint64_t)lane * 16;
   // lanes 0 and 63 are context only: their starts are cleared with a per-lane
-  // mask (a loop-invariant VGPR; as a lane-mask bool it took an SGPR pair)
-  const uint32_t keep = (uint32_t)(lane - 1) < 62u ? 0xFFFFFFFFu : 0u;
+  // mask (m.keep: a loop-invariant VGPR the compiler cannot see through; as a
+  // lane-mask bool it took an SGPR pair, spilled to VGPR lanes and reloaded
+  // with two v_readlane per row)
+  const uint32_t keep = m.keep;
   const bool ctx = keep == 0;
-  const bool slow = __any(nonascii16(a) != 0);
+  // per dword (exact for ASCII bytes: no carries between bytes): whitespace =
+  // byte < 33 and (byte == 32 or 9 <= byte <= 13); control = the other bytes
+  // < 33 (NUL included), flagged in bit 7 by lt33 ^ ws (ws is inside lt33 & 0x80)
+  uint32_t ws16, cx = 0;
+  {
+    const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
+    uint32_t wsd[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      const uint32_t x = ad[d];
+      const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
+      wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
+      cx = d == 0 ? (lt33 ^ wsd[0]) : __builtin_amdgcn_bitop3_b32(lt33, wsd[d], cx, 0xBE);  // (a ^ b) | c
+    }
+    ws16 = gather16(wsd);
+  }
+  // one test for both rare kinds of row: a non-ASCII byte (bit 7 set; the
+  // classification above is then meaningless and the row takes the Unicode
+  // walk) or a control byte (NULs are found exactly below)
+  bool slow = false, anyz = false;
+  if (__any(((a.x | a.y | a.z | a.w | cx) & 0x80808080u) != 0)) {
+    slow = __any(nonascii16(a) != 0);
+    anyz = !slow && __any((cx & 0x80808080u) != 0);
+  }
   uint32_t ws32 = 0, z32 = 0, start;
   bool chk = false;  // rows with NUL bytes or near a non-final buffer end need the odd checks
   uint32_t lim = 64;
   if (!slow) {
-    // per dword (ASCII bytes, no carries between bytes): whitespace = byte < 33
-    // and (byte == 32 or 9 <= byte <= 13); ctl = other bytes < 33 (NUL included)
-    uint32_t ws16, ctl = 0;
-    {
-      const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
-      uint32_t wsd[4];
-#pragma unroll
-      for (int d = 0; d < 4; d++) {
-        const uint32_t x = ad[d];
-        const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
-        wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
-        ctl |= lt33 & ~wsd[d];
-      }
-      // the 16 byte flags (bit 7 of every byte) into bits 0..15: two dwords'
-      // flags interleave at bits 8 k and 8 k + 4, three shifted copies move
-      // bytes 1..3's into bits 1..3 / 5..7, and v_perm joins the two low bytes
-      uint32_t lo = (wsd[0] >> 7) | (wsd[1] >> 3), hi = (wsd[2] >> 7) | (wsd[3] >> 3);
-      lo |= (lo >> 7) | (lo >> 14) | (lo >> 21);
-      hi |= (hi >> 7) | (hi >> 14) | (hi >> 21);
-      ws16 = __builtin_amdgcn_perm(hi, lo, 0x0C0C0400u);
-    }
     const uint32_t wsn = from_next_lane(ws16);
     const uint32_t wsp = from_prev_lane(ws16);
     ws32 = ws16 | (wsn << 16);
@@ -948,7 +1072,6 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       if (p0 < m.c.own_lo) start &= ~((1u << (uint32_t)(m.c.own_lo - p0 < 16 ? m.c.own_lo - p0 : 16)) - 1u);
       if (p0 + 16 > m.c.own_hi) start &= (m.c.own_hi > p0) ? ((1u << (uint32_t)(m.c.own_hi - p0)) - 1u) : 0u;
     }
-    const bool anyz = __any((ctl & 0x80808080u) != 0);  // any control byte: NULs are found exactly below
     if (anyz) {
       const uint32_t z16 = zero_mask16(a);
       z32 = z16 | (from_next_lane(z16) << 16);
@@ -964,6 +1087,9 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     vm_settle();
     vclear = true;
   }
+#ifdef MOX_ISA_MARKS
+  asm volatile("; MARK BP_START");
+#endif
   if MOX_ABL(m.w.dbg, DBG_NO_TOKENS) { asm volatile("" ::"v"(start), "v"(z32)); return; }
   const uint32_t cnt = __popc(start);
   ntok += cnt;
@@ -971,36 +1097,39 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   const uint32_t incl = wave_incl_scan(cnt);
   const uint32_t pre = incl - cnt, total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
   if (total == 0) return;
+#ifdef MOX_ISA_MARKS
+  asm volatile("; MARK BP_SCAN");
+#endif
   reinterpret_cast<uint4*>(rowbuf)[lane] = lower16(a);
   // list entries: see LIST_ODD
-  uint32_t k = pre;
-  bool any_odd = false;
   if (!chk && !slow) {
-    // common rows: a loop with a wave-uniform trip count (the most starts in
-    // any lane) and no divergence; a lane that has run out of starts writes
-    // the sink entry list[TOKMAX - 1], which no row reaches (<= PAY / 2
-    // tokens).  v_ffbl of 0 is ~0: such a start or length reads as odd.
-    // A token longer than 16 bytes has no whitespace in the 16 bytes after
-    // its start: found once per row from the smeared whitespace mask.
-    uint32_t sm = ws32 >> 1;
-    sm |= sm >> 1;
-    sm |= sm >> 2;
-    sm |= sm >> 4;
-    sm |= sm >> 8;  // bit p: whitespace somewhere in bits p + 1 .. p + 16
-    any_odd = (start & ~sm) != 0;
-    const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(cnt), 63);
+    // common rows: a lane's starts in order, unrolled (the entry offsets are
+    // immediates) and exec-masked (a lane leaves the loop when its starts run
+    // out).  A token longer than 16 bytes (or with no whitespace in the
+    // window: v_ffbl of 0 is ~0) lands at or above LIST_ODD by itself and is
+    // found by the token pass's valid count.
     uint32_t st = start;
-    uint16_t* const sink = list + (TOKMAX - 1);
     uint16_t* const mine = list + pre;  // this lane's entries: mine[0 .. cnt)
     const uint32_t lbase = (uint32_t)(lane * 16);
-    for (uint32_t it = 0; it < trips; it++) {
-      const uint32_t p = ffbl(st);  // ~0 once the lane has run out of starts
-      st &= st - 1;
-      const uint32_t len = ffbl(ws32 >> (p & 31u));
-      // len > 16 (or no whitespace in the window: ffbl ~0) lands at or above LIST_ODD by itself
-      *(it < cnt ? mine + it : sink) = (uint16_t)(lbase + p + (len << 10));
-    }
+#ifdef MOX_ISA_MARKS
+    asm volatile("; MARK LIST_PRE");
+#endif
+#define MOX_LIST_STEP(I)                                   \
+  {                                                        \
+    if (st == 0) goto list_done;                           \
+    const uint32_t p = ffbl(st);                           \
+    st &= st - 1;                                          \
+    const uint32_t len = ffbl(ws32 >> p);                  \
+    mine[I] = (uint16_t)(lbase + p + (len << 10));         \
+  }
+    MOX_LIST_STEP(0) MOX_LIST_STEP(1) MOX_LIST_STEP(2) MOX_LIST_STEP(3)
+    MOX_LIST_STEP(4) MOX_LIST_STEP(5) MOX_LIST_STEP(6) MOX_LIST_STEP(7)
+    MOX_LIST_STEP(8) MOX_LIST_STEP(9) MOX_LIST_STEP(10) MOX_LIST_STEP(11)
+    MOX_LIST_STEP(12) MOX_LIST_STEP(13) MOX_LIST_STEP(14) MOX_LIST_STEP(15)
+#undef MOX_LIST_STEP
+  list_done:;
   } else {
+    uint32_t k = pre;
     while (start) {
       const uint32_t p = __builtin_ctz(start);
       start &= start - 1;
@@ -1008,38 +1137,42 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       const uint32_t len = rest ? __builtin_ctz(rest) : 32;
       bool odd = slow || len > 16;
       if (chk) odd = odd || p + len >= lim || ((z32 >> p) & ((1u << (len & 31)) - 1u)) != 0;
-      any_odd |= odd;
       list[k++] = (uint16_t)((uint32_t)(lane * 16) + p + (odd ? 0x8000u : (len << 10)));
     }
   }
+  list[total + lane] = (uint16_t)LIST_ODD;  // the tail the token pass reads past the last entry
   wave_lds_fence();
 #ifdef MOX_ISA_MARKS
   asm volatile("; DO_ROW list done");
 #endif
-  if (__any(any_odd)) {  // rare: long tokens, NUL bytes, non-ASCII rows
+  if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
+  uint64_t t1 = 0;
+  if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
+  uint32_t nvalid = 0;
+  if (m.dict_n == 0) {  // no dictionary: no probes (uniform branch)
+    for (uint32_t j0 = 0; j0 < total;) {
+      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, nst, nvalid); j0 += 128; }
+      else { pass_c<1>(m, rowbuf, list, j0, nst, nvalid); j0 += 64; }
+    }
+  } else {
+    for (uint32_t j0 = 0; j0 < total;) {
+      const uint32_t rem = total - j0;
+      if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, total, nst, nvalid); j0 += 192; }
+      else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, total, nst, nvalid); j0 += 128; }
+      else { pass_a<1>(m, rowbuf, list, j0, total, nst, nvalid); j0 += 64; }
+    }
+  }
+  // the row has odd entries iff fewer than total were valid (tail entries are
+  // not valid; uniform)
+  if (nvalid != total) {
+    // rare: long tokens, NUL bytes, non-ASCII rows (the order against the
+    // token pass is free: every token is counted once either way)
     for (uint32_t j = lane; j < total; j += 64) {
       const uint32_t e = list[j];
       if (e >= LIST_ODD) generic_token(m, sbase + (e & 1023u));
     }
     vm_settle();
     vclear = true;
-  }
-  if MOX_ABL(m.w.dbg, DBG_NO_EMIT) { wave_lds_fence(); return; }
-  uint64_t t1 = 0;
-  if (cyc) { t1 = __builtin_amdgcn_s_memtime(); cyc->byte += t1; }
-  if (m.dict_n == 0) {  // no dictionary: no probes (uniform branch)
-    for (uint32_t j0 = 0; j0 < total;) {
-      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, total, nst); j0 += 128; }
-      else { pass_c<1>(m, rowbuf, list, j0, total, nst); j0 += 64; }
-    }
-    wave_lds_fence();
-    return;
-  }
-  for (uint32_t j0 = 0; j0 < total;) {
-    const uint32_t rem = total - j0;
-    if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, total, nst); j0 += 192; }
-    else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, total, nst); j0 += 128; }
-    else { pass_a<1>(m, rowbuf, list, j0, total, nst); j0 += 64; }
   }
   if (cyc) cyc->pa += __builtin_amdgcn_s_memtime() - t1;
   wave_lds_fence();
@@ -1060,10 +1193,7 @@ __device__ __forceinline__ uint32_t classify16(uint4 a, uint32_t& ctl) {
     wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
     ctl |= lt33 & ~wsd[d];
   }
-  uint32_t lo = (wsd[0] >> 7) | (wsd[1] >> 3), hi = (wsd[2] >> 7) | (wsd[3] >> 3);
-  lo |= (lo >> 7) | (lo >> 14) | (lo >> 21);
-  hi |= (hi >> 7) | (hi >> 14) | (hi >> 21);
-  return __builtin_amdgcn_perm(hi, lo, 0x0C0C0400u);
+  return gather16(wsd);
 }
 // Two consecutive rows at once (MOX_MAP_PAIR): slots buf (row u) and buf + SLOT
 // (row u + 1), one list of both rows' tokens in 11-bit-offset entries (row
@@ -1134,11 +1264,12 @@ __device__ __forceinline__ void do_pair(const MapCtx& m, uint64_t sbase, uint4 a
     vm_settle();
     vclear = true;
   }
+  uint32_t nv_unused = 0;  // (the pair path finds its odd entries from the smeared masks)
   for (uint32_t j0 = 0; j0 < total;) {
     const uint32_t rem = total - j0;
-    if (rem > 128) { pass_a<3, 11>(m, buf, list, j0, total, nst); j0 += 192; }
-    else if (rem > 64) { pass_a<2, 11>(m, buf, list, j0, total, nst); j0 += 128; }
-    else { pass_a<1, 11>(m, buf, list, j0, total, nst); j0 += 64; }
+    if (rem > 128) { pass_a<3, 11>(m, buf, list, j0, total, nst, nv_unused); j0 += 192; }
+    else if (rem > 64) { pass_a<2, 11>(m, buf, list, j0, total, nst, nv_unused); j0 += 128; }
+    else { pass_a<1, 11>(m, buf, list, j0, total, nst, nv_unused); j0 += 64; }
   }
   wave_lds_fence();
 }
@@ -1167,22 +1298,28 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   // alignment after c); taking &w instead would copy it to scratch
   m.wk = (KWork)((const __attribute__((address_space(4))) char*)__builtin_amdgcn_kernarg_segment_ptr() +
                  ((sizeof(Corpus) + alignof(Work) - 1) & ~(alignof(Work) - 1)));
-  uint8_t* sp = smem;
-  // the arrays the token pass indexes per token first: their offsets fit the
-  // LDS instructions' 16-bit offset field, so no address add per access
-  m.s.dcnt = (uint32_t*)sp; sp += DICT_SLOTS * 4;
-  m.s.bcnt = (uint32_t*)sp; sp += NB * 4;
-  m.s.misc = (uint32_t*)sp; sp += 16;          // [0] spills [1] ticket
-  m.s.seltab = (uint4*)sp; sp += KSEL_N * 16;
-  m.s.dkey = (uint4*)sp; sp += DICT_SLOTS * 16;
+  if (lds_addr(smem) != 0u) {  // the layout constants (L_*) assume it: never with no static LDS
+    if (threadIdx.x == 0) w.ctl->layout_err = 1;
+    return;
+  }
+  // (layout: L_ROWS ...; the per-token tables' offsets fit the LDS
+  // instructions' 16-bit offset field, so no address add per access)
+  m.s.dcnt = lds_ptr<uint32_t>(L_DCNT);
+  m.s.bcnt = lds_ptr<uint32_t>(L_BCNT);
+  m.s.misc = lds_ptr<uint32_t>(L_MISC);  // [0] spills [1] ticket
+  m.s.seltab = lds_ptr<uint4>(L_SELTAB);
+  m.s.dkey = lds_ptr<uint4>(L_DKEY);
+  asm("v_mov_b32 %0, 0x3fc" : "=v"(m.s.kmask));
+  m.keep = (uint32_t)((threadIdx.x & 63) - 1) < 62u ? 0xFFFFFFFFu : 0u;
+  asm volatile("" : "+v"(m.keep));
 #if MOX_MAP_SELF
-  uint8_t* rowbufs = sp; sp += MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT;  // MAP_AHEAD + 1 row (pair) buffers per wave
+  uint8_t* rowbufs = lds_ptr<uint8_t>(L_ROWS);  // MAP_AHEAD + 1 row (pair) buffers per wave
 #else
-  uint32_t* sready = (uint32_t*)sp; sp += RING * 4;  // row ticket + 1 once loaded
-  uint32_t* sfree = (uint32_t*)sp; sp += RING * 4;   // row ticket + 1 once consumed
-  uint8_t* ring = sp; sp += RING * SLOT;
+  uint32_t* sready = lds_ptr<uint32_t>(L_RFLAGS);         // row ticket + 1 once loaded
+  uint32_t* sfree = lds_ptr<uint32_t>(L_RFLAGS + RING * 4);  // row ticket + 1 once consumed
+  uint8_t* ring = lds_ptr<uint8_t>(L_ROWS);
 #endif
-  uint16_t* lists = (uint16_t*)sp; sp += MAP_ROW_WAVES * 2 * TOKMAX;
+  uint16_t* lists = lds_ptr<uint16_t>(L_LISTS);
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
 #ifndef MOX_TIMING_ONLY_SMALL_DICT  // (timing experiments with a smaller dictionary: dictionary passes only)
@@ -1249,7 +1386,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #else
     {
 #endif
-    uint16_t* list = lists + wv * (MAP_PAIRW * TOKMAX);
+    uint16_t* list = lists + wv * (MAP_PAIRW * LIST_N);
     uint32_t e_lo = rb < 2 ? (uint32_t)(2 - rb) : 0u;  // edge rows: see the consumers of the ring build below
     const uint32_t e_hi = __builtin_amdgcn_readfirstlane(nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u);
     if (c.own_hi > base0 && nrows * PAY < c.own_hi - base0) e_lo = n;
@@ -1492,7 +1629,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     }
   } else {
     // ---------------- consumers
-    uint16_t* list = lists + (wv - MAP_LOADERS) * TOKMAX;
+    uint16_t* list = lists + (wv - MAP_LOADERS) * LIST_N;
     // Edge rows: only they can reach a buffer or ownership bound.  Row r's slot
     // starts at base0 + r PAY - 16 and nrows PAY covers own_hi - base0, so every
     // row r >= 1 starts past lo and own_lo, and every row r <= nrows - 3 ends
@@ -1561,9 +1698,13 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     }
   }
   // workgroup totals first: one global atomic each per workgroup (a per-thread
-  // atomic on one control-block word serialises 256K updates at the L2)
-  __shared__ unsigned long long s_tok;
-  __shared__ uint32_t s_cmax;
+  // atomic on one control-block word serialises 256K updates at the L2).  They
+  // live in the (now idle) token lists: k_map has no static LDS, so dynamic
+  // LDS starts at address 0 and the compiler folds table bases into the LDS
+  // instructions' offsets (with 16 B of static LDS it added the base per key).
+  unsigned long long& s_tok = *reinterpret_cast<unsigned long long*>(lists);
+  uint32_t& s_cmax = *reinterpret_cast<uint32_t*>(lists + 4);
+  static_assert(MAP_LDS_BYTES % 8 == 0 && (2 * LIST_N) % 8 == 0, "totals alignment in the lists");
   if (tid == 0) { s_tok = 0; s_cmax = 0; }
   __syncthreads();
   uint32_t cmax = 0;
