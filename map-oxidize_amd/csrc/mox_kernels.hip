@@ -680,6 +680,18 @@ __device__ __forceinline__ uint32_t ffbl(uint32_t x) {
   asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
   return r;
 }
+// LDS fetch-add issued by one lane (called under lane == 0; the result is
+// lane 0's).  As inline asm because the compiler's atomic optimizer turns any
+// atomic on a uniform address into a wave-aggregated one (v_mbcnt x 2, a
+// compare, a bit count, two v_readfirstlane: ~8 VALU) even when one lane is
+// active.  Waits for the wave's LDS operations (lgkmcnt(0)) before returning.
+// a: the LDS address (a constant of the k_map layout: from a generic pointer
+// the cast added a null check and SGPR spills)
+__device__ __forceinline__ uint32_t lds_fetch_add1(uint32_t a, uint32_t v) {
+  uint32_t r;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a), "v"(v) : "memory");
+  return r;
+}
 // compiler + LDS ordering between lanes of one wave (LDS executes a wave's
 // instructions in order; this keeps the compiler from reordering across it)
 __device__ __forceinline__ void wave_lds_fence() {
@@ -723,11 +735,26 @@ struct KeyLd {
   uint32_t E[5];
   uint4 S;  // v_perm selectors: alignment and length mask in one (seltab)
 };
+#ifndef MOX_KEY_UNALIGNED
+#define MOX_KEY_UNALIGNED 0  // 1: one-row keys read at their exact (unaligned) start and masked by AND (no v_perm)
+#endif
+static_assert(!(MOX_KEY_UNALIGNED && MOX_MAP_PAIR), "the row-pair path keeps the v_perm keys");
 // PB: bits of the slot offset in a list entry (10: one row; 11: a row pair,
 // whose two slots are adjacent in LDS), the length field above them
 template <int PB = 10>
 __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf, uint32_t e, KeyLd& r) {
-  (void)s;
+#if MOX_KEY_UNALIGNED
+  if constexpr (PB == 10) {
+    // the 16 bytes at the token's start (LDS reads take any byte alignment on
+    // gfx950), and the byte mask of its length (seltab[len], 16 B each)
+    typedef uint32_t U32U __attribute__((aligned(1)));
+    const U32U* q = lds_ptr<const U32U>(__builtin_amdgcn_bitop3_b32(e, s.kmask, lds_addr(rowbuf), 0xEA));
+#pragma unroll
+    for (int i = 0; i < 4; i++) r.E[i] = q[i];
+    r.S = *lds_ptr<const uint4>(L_SELTAB + ((e >> 6) & 0x3F0u));
+    return;
+  }
+#endif
   // rowbuf is a row slot (row pair), aligned to its size (L_ROWS): the 4-aligned
   // token offset ORs in, (e & mask) | slot in one v_bitop3_b32 (truth table 0xEA)
   static_assert(((1u << PB) - 1u & ~3u) == (PB == 10 ? 0x3FCu : 0x7FCu), "key offset mask");
@@ -745,6 +772,13 @@ __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf,
 }
 __device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
   (void)e;
+#if MOX_KEY_UNALIGNED
+  K[0] = r.E[0] & r.S.x;
+  K[1] = r.E[1] & r.S.y;
+  K[2] = r.E[2] & r.S.z;
+  K[3] = r.E[3] & r.S.w;
+  return;
+#endif
   // byte 4 d + j of the key = byte S.d[j] of (E[d + 1]:E[d]) (0x0C: zero): one
   // v_perm_b32 per dword aligns and masks at once
   K[0] = __builtin_amdgcn_perm(r.E[1], r.E[0], r.S.x);
@@ -787,6 +821,12 @@ __device__ __forceinline__ void after_fence(uint32_t (&v)[TU]) {
 // builtin keeps the combiner from splitting it into four compares and a
 // boolean tree, and (unlike inline asm, which it replaces) lets the scheduler
 // interleave the chains without a wait state after every step.
+#ifndef MOX_BK_ONCE
+#define MOX_BK_ONCE 1
+#endif
+#ifndef MOX_PROBE_LAZY
+#define MOX_PROBE_LAZY 0  // 1: second dictionary slot read only where the first missed (k_map pass_a)
+#endif
 #ifndef MOX_EQ64
 #define MOX_EQ64 0  // 1: two v_cmp_eq_u64 per key compare (lane masks ANDed on the SALU)
 #endif
@@ -854,9 +894,28 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     s2[u] = slot_off16((h[u] >> 16) * (uint32_t)DICT_SLOTS);      // 16 dict_s2(h)
   }
   uint4 d1[TU], d2[TU];
+#if MOX_PROBE_LAZY
+  // (timing experiment) the second slot read only by the lanes whose key is
+  // not in the first: fewer LDS bytes, one more round trip per pass
+#pragma unroll
+  for (int u = 0; u < TU; u++) d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]);
+  SCHED_FENCE();
+  bool h1[TU];
+#pragma unroll
+  for (int u = 0; u < TU; u++) {
+    h1[u] = key_eq4(d1[u], K[u]);
+    if (e[u] < (17u << PB) && !h1[u]) d2[u] = *lds_ptr<const uint4>(L_DKEY + s2[u]);
+  }
+  SCHED_FENCE();
+#elif defined(MOX_TIMING_ONE_PROBE)  // (timing only, counts wrong: no second slot read)
+#pragma unroll
+  for (int u = 0; u < TU; u++) { d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]); d2[u] = d1[u]; }
+  SCHED_FENCE();
+#else
 #pragma unroll
   for (int u = 0; u < TU; u++) { d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]); d2[u] = *lds_ptr<const uint4>(L_DKEY + s2[u]); }
   SCHED_FENCE();
+#endif
   // hits count in LDS; every miss reserves its region slot (the LDS returning
   // atomics of all batches issued together), then the misses are stored
   bool miss[TU];
@@ -865,7 +924,11 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
   for (int u = 0; u < TU; u++) {
     const bool valid = e[u] < (17u << PB);  // LIST_ODD of the format
     nvalid += (uint32_t)__popcll(__ballot(valid));
+#if MOX_PROBE_LAZY
+    const bool hit1 = h1[u], hit2 = valid && !hit1 && key_eq4(d2[u], K[u]);
+#else
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
+#endif
     miss[u] = valid & !(hit1 | hit2);
     if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
 #if defined(MOX_PATHS) && MOX_PATHS
@@ -877,15 +940,15 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
   }
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) return;
   // (a dictionary pass: the region counters are at L_BCNT, an immediate offset;
-  // pos and bk are read under miss only.  The partition is computed once and
-  // kept opaque: the compiler otherwise formed the counter address from h
-  // directly and shifted h again for the store.)
+  // pos and bk are read under miss only.  MOX_BK_ONCE keeps the partition
+  // opaque so that it is computed once (the compiler forms the counter address
+  // from h directly and shifts h again for the store): k_map +1 % with it.)
   uint32_t bk[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     if (miss[u]) {
       bk[u] = bucket_of(h[u]);
-      asm("" : "+v"(bk[u]));
+      if (MOX_BK_ONCE) asm("" : "+v"(bk[u]));
       pos[u] = atomicAdd(lds_ptr<uint32_t>(L_BCNT + 4 * bk[u]), 1u);
     }
   }
@@ -1042,12 +1105,17 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   {
     const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
     uint32_t wsd[4];
+    // Four adds and three v_bitop3_b32 per dword, all of the fast VALU class
+    // (profiles/r05/valu_issue_probe.txt: add / bitop3 ~3 cycles, and_or / or3
+    // ~5): t = (ge9 & ~ge14) | ge32 (0xBA), ws = ~ge33 & t & 0x80 (0x08),
+    // control |= ~ge33 ^ ws (0xEB: (~a ^ b) | c)
 #pragma unroll
     for (int d = 0; d < 4; d++) {
       const uint32_t x = ad[d];
-      const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
-      wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
-      cx = d == 0 ? (lt33 ^ wsd[0]) : __builtin_amdgcn_bitop3_b32(lt33, wsd[d], cx, 0xBE);  // (a ^ b) | c
+      const uint32_t ge33 = x + 0x5F5F5F5Fu, ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
+      const uint32_t t = __builtin_amdgcn_bitop3_b32(ge9, ge14, ge32, 0xBA);
+      wsd[d] = __builtin_amdgcn_bitop3_b32(ge33, t, 0x80808080u, 0x08);
+      cx = __builtin_amdgcn_bitop3_b32(ge33, wsd[d], cx, 0xEB);
     }
     ws16 = gather16(wsd);
   }
@@ -1055,7 +1123,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   // classification above is then meaningless and the row takes the Unicode
   // walk) or a control byte (NULs are found exactly below)
   bool slow = false, anyz = false;
-  if (__any(((a.x | a.y | a.z | a.w | cx) & 0x80808080u) != 0)) {
+  const uint32_t any3 = __builtin_amdgcn_bitop3_b32(a.x, a.y, a.z, 0xFE);  // (3-input ORs as bitop3: fast class)
+  if (__any((__builtin_amdgcn_bitop3_b32(a.w, any3, cx, 0xFE) & 0x80808080u) != 0)) {
     slow = __any(nonascii16(a) != 0);
     anyz = !slow && __any((cx & 0x80808080u) != 0);
   }
@@ -1105,7 +1174,8 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   if (!chk && !slow) {
     // common rows: a lane's starts in order, unrolled (the entry offsets are
     // immediates) and exec-masked (a lane leaves the loop when its starts run
-    // out).  A token longer than 16 bytes (or with no whitespace in the
+    // out).  The entry's fields are disjoint bits (lane base 16 lane, start
+    // 0..15, length << 10): one 3-input OR (v_bitop3, fast) instead of v_add3.  A token longer than 16 bytes (or with no whitespace in the
     // window: v_ffbl of 0 is ~0) lands at or above LIST_ODD by itself and is
     // found by the token pass's valid count.
     uint32_t st = start;
@@ -1120,7 +1190,7 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
     const uint32_t p = ffbl(st);                           \
     st &= st - 1;                                          \
     const uint32_t len = ffbl(ws32 >> p);                  \
-    mine[I] = (uint16_t)(lbase + p + (len << 10));         \
+    mine[I] = (uint16_t)__builtin_amdgcn_bitop3_b32(lbase, p, len << 10, 0xFE); \
   }
     MOX_LIST_STEP(0) MOX_LIST_STEP(1) MOX_LIST_STEP(2) MOX_LIST_STEP(3)
     MOX_LIST_STEP(4) MOX_LIST_STEP(5) MOX_LIST_STEP(6) MOX_LIST_STEP(7)
@@ -1309,7 +1379,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.misc = lds_ptr<uint32_t>(L_MISC);  // [0] spills [1] ticket
   m.s.seltab = lds_ptr<uint4>(L_SELTAB);
   m.s.dkey = lds_ptr<uint4>(L_DKEY);
-  asm("v_mov_b32 %0, 0x3fc" : "=v"(m.s.kmask));
+  if (MOX_KEY_UNALIGNED) asm("v_mov_b32 %0, 0x3ff" : "=v"(m.s.kmask));
+  else asm("v_mov_b32 %0, 0x3fc" : "=v"(m.s.kmask));
   m.keep = (uint32_t)((threadIdx.x & 63) - 1) < 62u ? 0xFFFFFFFFu : 0u;
   asm volatile("" : "+v"(m.keep));
 #if MOX_MAP_SELF
@@ -1350,7 +1421,16 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #if !MOX_MAP_SELF
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
 #endif
-  if (tid < KSEL_N) {  // key byte 4 d + j = window byte sh + 4 d + j, or 0 past len (v_perm selector 0x0C)
+  if (MOX_KEY_UNALIGNED && tid < 17) {  // byte masks of a len-byte key
+    uint32_t mk[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+      mk[d] = 0;
+#pragma unroll
+      for (int j = 0; j < 4; j++) mk[d] |= (4 * d + j < tid ? 0xFFu : 0u) << (8 * j);
+    }
+    m.s.seltab[tid] = make_uint4(mk[0], mk[1], mk[2], mk[3]);
+  } else if (!MOX_KEY_UNALIGNED && tid < KSEL_N) {  // key byte 4 d + j = window byte sh + 4 d + j, or 0 past len (v_perm selector 0x0C)
     const uint32_t len = (uint32_t)tid >> 2, sh = (uint32_t)tid & 3u;
     uint32_t sel[4];
 #pragma unroll
@@ -1408,7 +1488,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
 #else
     auto ticket = [&]() -> uint32_t {
       uint32_t u = 0;
-      if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
+      if (lane == 0) u = lds_fetch_add1(L_MISC + 4, 1u);  // m.s.misc[1]
       return u;
     };
 #endif
@@ -1649,7 +1729,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     for (;;) {
       const uint64_t tw = cp ? __builtin_amdgcn_s_memtime() : 0;
       uint32_t u = 0;
-      if (lane == 0) u = atomicAdd(&m.s.misc[1], 1u);
+      if (lane == 0) u = lds_fetch_add1(L_MISC + 4, 1u);  // m.s.misc[1]
       u = __builtin_amdgcn_readfirstlane(u);
       if (u >= n) break;
       const uint32_t slot = u % RING;
