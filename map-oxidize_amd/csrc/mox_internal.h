@@ -145,7 +145,9 @@ enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO
                   DBG_PAIR_NOSTORE = 8192u, // no dictionary: pairs formed, their global stores skipped (timing only)
                   DBG_NOPAIR = 16384u,      // no dictionary: every record stored alone, no pair slots (timing A/B)
                   DBG_PAIR_SEQ = 32768u,    // no dictionary: pairs stored at consecutive addresses (timing only: wrong regions)
-                  DBG_S1_SORT2 = 65536u };  // k_reduce_sort1/2 sort every unit's keys twice (timing only, same result)
+                  DBG_S1_SORT2 = 65536u,    // k_reduce_sort1/2 sort every unit's keys twice (timing only, same result)
+                  DBG_COLD_SEQ = 131072u,   // k_map dictionary pass: cold records all into partition 0's region (timing only)
+                  DBG_COLD_NOSTORE = 262144u };  // k_map dictionary pass: region slots reserved, records not stored (timing only)
 // Bounds checks of derived indices (UnitDesc ranges, scatter cursors, table
 // offsets), compiled in only with -DMOX_CHECK (libmox_check.so, `make check`):
 // a failed check counts into ctl->dbg_cnt[0], records the largest site id in

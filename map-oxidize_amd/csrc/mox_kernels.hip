@@ -692,6 +692,14 @@ __device__ __forceinline__ uint32_t lds_fetch_add1(uint32_t a, uint32_t v) {
   asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a), "v"(v) : "memory");
   return r;
 }
+// The same without the wait, for a compiler-managed result: the address is
+// passed through a VGPR the compiler cannot see through, so it treats it as
+// divergent and leaves the atomic alone (one v_mov instead of ~8 VALU).
+__device__ __forceinline__ uint32_t lds_fetch_add_lane(uint32_t* p, uint32_t v) {
+  uint32_t a = lds_addr(p);
+  asm("" : "+v"(a));
+  return atomicAdd(lds_ptr<uint32_t>(a), v);
+}
 // compiler + LDS ordering between lanes of one wave (LDS executes a wave's
 // instructions in order; this keeps the compiler from reordering across it)
 __device__ __forceinline__ void wave_lds_fence() {
@@ -960,8 +968,12 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     const uint32_t b = bk[u];
     const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
     if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, 0, pos[u], max(h[u], 1u));  // (hash32_map)
-    if (pos[u] < m.rc) *cold_at(m, b, 0, pos[u]) = key;
-    else cold_spill(m, key);
+    if (pos[u] < m.rc) {
+      if (MOX_ABL(m.w.dbg, DBG_COLD_NOSTORE)) asm volatile("" ::"v"(key.x), "v"(key.w));
+      else *cold_at(m, MOX_ABL(m.w.dbg, DBG_COLD_SEQ) ? 0u : b, 0, pos[u]) = key;
+    } else {
+      cold_spill(m, key);
+    }
   }
 #ifdef MOX_ISA_MARKS
   asm volatile("; PASS_A end");
@@ -2481,10 +2493,20 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 // hash bits used: partition = top NB_LOG2 bits, sub-pass = the next kk bits,
 // bucket = a multiplicative hash of the low bits
-__device__ __forceinline__ uint32_t red_bucket(uint32_t h) {
-  return (uint32_t)(((uint64_t)((h * 0x9E3779B1u) >> 8) * RED_BK) >> 24);
+// (fastrange of the key hash's low 16 bits: one v_mul_u32_u24 (SDWA word
+// select) and a shift; the hash is already mixed, and within a partition its
+// top bits are fixed while the low ones are not.  Was a 32-bit multiply by the
+// golden ratio and a 24 x 10-bit product split in three instructions.)
+__device__ __forceinline__ uint32_t red_bucket(uint32_t h) { return ((h & 0xFFFFu) * (uint32_t)RED_BK) >> 16; }
+// (one xor and three (a ^ b) | c v_bitop3: the plain expression compiled to
+// four compares, four selects and 16-bit shuffles, ~16 VALU)
+__device__ __forceinline__ bool key_eq16(uint4 a, uint4 b) {
+  uint32_t d = a.x ^ b.x;
+  d = __builtin_amdgcn_bitop3_b32(a.y, b.y, d, 0xBE);
+  d = __builtin_amdgcn_bitop3_b32(a.z, b.z, d, 0xBE);
+  d = __builtin_amdgcn_bitop3_b32(a.w, b.w, d, 0xBE);
+  return d == 0;
 }
-__device__ __forceinline__ bool key_eq16(uint4 a, uint4 b) { return ((a.x ^ b.x) | (a.y ^ b.y) | (a.z ^ b.z) | (a.w ^ b.w)) == 0; }
 
 // Exact insert (slow path).  A slot is claimed by CAS on its tag (keys with tag
 // h fill the first free slot of the first bucket with room, so every insert of
@@ -2570,15 +2592,18 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
 __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   const uint32_t b = red_bucket(h), b2 = b + 1 == RED_BK ? 0 : b + 1;
   const uint4 t = s.tag4[b], t2 = s.tag4[b2];
-  int sl = t2.w == h ? (int)(4 * b2 + 3) : -1;
-  sl = t2.z == h ? (int)(4 * b2 + 2) : sl;
-  sl = t2.y == h ? (int)(4 * b2 + 1) : sl;
-  sl = t2.x == h ? (int)(4 * b2 + 0) : sl;
-  sl = t.w == h ? (int)(4 * b + 3) : sl;
-  sl = t.z == h ? (int)(4 * b + 2) : sl;
-  sl = t.y == h ? (int)(4 * b + 1) : sl;
-  sl = t.x == h ? (int)(4 * b + 0) : sl;
-  if (sl < 0) return false;
+  // first matching tag as an index 0..7 (8: none), each select taking an inline
+  // constant; slots 4 b .. 4 b + 3 then 4 b2 ..
+  uint32_t ix = t2.w == h ? 7u : 8u;
+  ix = t2.z == h ? 6u : ix;
+  ix = t2.y == h ? 5u : ix;
+  ix = t2.x == h ? 4u : ix;
+  ix = t.w == h ? 3u : ix;
+  ix = t.z == h ? 2u : ix;
+  ix = t.y == h ? 1u : ix;
+  ix = t.x == h ? 0u : ix;
+  if (ix == 8u) return false;
+  const int sl = (int)(ix < 4u ? 4 * b + ix : 4 * b2 + (ix - 4u));
   const uint4 kk = s.key[sl];
   const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (cv == 0 || !key_eq16(kk, k)) return false;
@@ -3274,7 +3299,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         const uint32_t a1 = n;
         auto grab = [&]() -> uint32_t {
           uint32_t v = 0;
-          if (lane == 0) v = atomicAdd(&s.misc[2], SCH);
+          if (lane == 0) v = lds_fetch_add_lane(&s.misc[2], SCH);
           return __builtin_amdgcn_readfirstlane(v);
         };
         const uint32_t a0 = grab();
@@ -3285,22 +3310,22 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 #endif
         const uint4* ubase = split ? w.split_k + kin0 : w.cold + b * RC;  // region g at + g NB RC
         const uint64_t gstride = (uint64_t)NB * RC;
-        // lane state: region r holds flat records [rs, re)
+        // lane state: region r holds flat records [rs, re).  (A per-lane 64-bit
+        // region base instead of the multiply-add per load cost 2 VGPRs, which
+        // at 64 VGPRs doubled the scratch spills.)
         uint32_t r = 0, rs = 0, re = split ? 0xFFFFFFFFu : 0u;
         auto seek = [&](uint32_t c) {  // region of record c: last r with rpre[r] <= c (wave-uniform search)
           if (split || c >= a1) return;
           if (tab) {  // c is a ticket start
             r = rtab[c / SCH];
-            rs = rpre[r];
-            re = rpre[r + 1];
-            return;
+          } else {
+            uint32_t lo = 0, hi = G - 1;
+            while (lo < hi) {
+              const uint32_t mid = (lo + hi + 1) >> 1;
+              if (rpre[mid] <= c) lo = mid; else hi = mid - 1;
+            }
+            r = lo;
           }
-          uint32_t lo = 0, hi = G - 1;
-          while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (rpre[mid] <= c) lo = mid; else hi = mid - 1;
-          }
-          r = lo;
           rs = rpre[r];
           re = rpre[r + 1];
         };
@@ -3392,7 +3417,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         while (c < a1) {
           load(c + 2 * CH, C);
           uint32_t tv = 0;
-          if (lane == 0) tv = atomicAdd(&s.misc[2], SCH);
+          if (lane == 0) tv = lds_fetch_add_lane(&s.misc[2], SCH);
           process(A, c);
           const uint32_t cn = __builtin_amdgcn_readfirstlane(tv);
           seek(cn);
@@ -3410,7 +3435,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           load(c + CH, B);
           // the next ticket's LDS atomic goes out before this chunk's probes
           uint32_t tv = 0;
-          if (lane == 0) tv = atomicAdd(&s.misc[2], SCH);
+          if (lane == 0) tv = lds_fetch_add_lane(&s.misc[2], SCH);
           process(A, c);
           const uint32_t cn = __builtin_amdgcn_readfirstlane(tv);
           seek(cn);
