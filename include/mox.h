@@ -237,7 +237,11 @@ int mox_comm_unique_id(uint8_t id[MOX_UNIQUE_ID_BYTES]);
 int mox_comm_init(mox_engine* e, int nranks, int rank, const uint8_t id[MOX_UNIQUE_ID_BYTES]);
 /* After mox_run_range on every rank: hash-partition the local table, exchange
  * it with one RCCL all-to-all, and reduce the received partials.  Afterwards
- * this rank owns the final counts of its hash range (disjoint across ranks). */
+ * this rank owns the final counts of its hash range (disjoint across ranks).
+ * With MOX_F_SORT_BYTES the words are owned by byte range instead (splitters
+ * from 1,024 sampled 8-byte prefixes per rank, exchanged first) and every rank
+ * sorts its own range on its GPU, so mox_gather in rank order is the table in
+ * bytewise order (no sort at the root). */
 int mox_exchange(mox_engine* e);
 /* Host-staged transport for the same exchange (several ranks sharing one GPU,
  * or no RCCL): the library calls fn once per all-to-all with pinned host
