@@ -2585,6 +2585,9 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
   (void)eqtag;
 }
 
+#ifndef MOX_RED_FASTINS
+#define MOX_RED_FASTINS 1  // red_try also inserts a new key whose home bucket has room
+#endif
 // Fast path for records whose key is already published in its home bucket or
 // the next one (keys overflow at most one bucket at this table load): two tag
 // reads issued together, one key read, one add.  Returns false when the slow
@@ -2602,7 +2605,36 @@ __device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, ui
   ix = t.z == h ? 2u : ix;
   ix = t.y == h ? 1u : ix;
   ix = t.x == h ? 0u : ix;
-  if (ix == 8u) return false;
+  if (ix == 8u) {
+#if MOX_RED_FASTINS
+    // Not in its first two buckets.  If its home bucket has room the key is in
+    // no bucket at all (a key goes to the first bucket with room when it is
+    // inserted, and buckets never empty): claim the bucket's first free slot
+    // from the home slot on -- the rule red_insert uses, so that two inserters
+    // of one key always race for the same slot -- and publish it here,
+    // instead of sending the lane into red_insert's wave loop (which ~90 % of
+    // 64-record chunks entered for their ~2 new keys).
+    const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
+    int e = -1;
+#pragma unroll
+    for (int j = 3; j >= 0; j--) {
+      const int i = (int)((h + (uint32_t)j) & 3u);
+      if (tv[i] == 0) e = i;
+    }
+    if (e < 0) return false;
+    const uint32_t fs = 4 * b + (uint32_t)e;
+    if (atomicCAS(reinterpret_cast<uint32_t*>(s.tag4) + fs, 0u, h) != 0u) return false;  // lost it: red_insert re-reads
+    s.key[fs] = k;
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    atomicAdd(&s.cnt[fs], (unsigned long long)c);
+    const uint32_t u = atomicAdd(&s.misc[0], 1u);
+    if (u >= RED_CAP) s.misc[1] = 1;
+    return true;
+#else
+    return false;
+#endif
+  }
   const int sl = (int)(ix < 4u ? 4 * b + ix : 4 * b2 + (ix - 4u));
   const uint4 kk = s.key[sl];
   const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
