@@ -14,6 +14,7 @@
 #   slow     the slow GPU tests
 #   ab       interleaved per-kernel A/B of build variants: AB_VARS="v1 v2 v1 v2"
 #            AB_KERNELS="k_map" [AB_DBG="0"] [AB_ARGS="--workload C4 ..."]
+#   lines    bench lines of C5, C4 and the N = 2 engine group (C3 shards on GPU 0)
 #   pmc      k_map FETCH/WRITE traffic at C2 and SQ counters of k_map
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -81,6 +82,16 @@ varc2)
 stages)
   # k_map SQ instruction counts per ablation stage (tools/pmc_map_stages.sh, build/var_abl)
   bash tools/pmc_map_stages.sh ${2:-stages} "${STAGES:-4096 1 2 8 16 0}" > $O/stages.txt 2>&1; rc=$?; cat $O/stages.txt; step stages $rc
+  ;;
+lines)
+  # bench lines of the other configs: C5, C4 (16 GiB each), and the N = 2
+  # engine group (2 x 8 GiB C3 shards on GPU 0, device-copy transport, sorted result)
+  timeout -k 10 420 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --workload C5 > $O/bench_c5.json 2> $O/bench_c5.err; step "bench C5" $?
+  cut -c1-200 $O/bench_c5.json
+  timeout -k 10 600 python -u bench.py --steps 3 --warmup 2 --no-cpu-baseline --workload C4 > $O/bench_c4.json 2> $O/bench_c4.err; step "bench C4" $?
+  cut -c1-200 $O/bench_c4.json
+  timeout -k 10 500 python -u bench.py --gpus 2 --xport host --device 0 --steps 3 --warmup 1 > $O/bench_n2.json 2> $O/bench_n2.err; step "bench N2 group" $?
+  cut -c1-200 $O/bench_n2.json
   ;;
 pmc)
   bash tools/pmc_traffic_wl.sh C2 1073741824 ${2:-pmc}_traffic > $O/traffic.txt 2>&1; rc=$?; tail -5 $O/traffic.txt; step traffic $rc
