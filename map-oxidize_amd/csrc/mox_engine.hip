@@ -341,6 +341,9 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = fals
   // 1. hot dictionary from a sample
   if (sided) {
     use_dset(e, e->dcur ^ 1);
+    // after the previous pass's k_map (ev_mapped): beside its reduce tail
+    if (e->mapped_pending) (void)hipStreamWaitEvent(e->dstream, e->ev_mapped, 0);
+    e->mapped_pending = false;
     hipLaunchKernelGGL(k_dict_zero, dim3(64), dim3(256), 0, e->dstream, w);
     launch_dict(e, c, e->dstream, q);
     (void)hipEventRecord(e->ev_dready, e->dstream);
@@ -358,6 +361,13 @@ void enqueue_pass(mox_engine* e, const Corpus& c, const Seq& q, bool side = fals
   hipLaunchKernelGGL(k_map, dim3(grid), dim3(MAP_THREADS), map_lds_bytes(), s, c, w, nrows, 0u);
   q.step("k_map");
   q.rec(2);
+#ifndef MOX_SIDE_AFTER_MAP
+#define MOX_SIDE_AFTER_MAP 0  // 1: measured slower end to end (profiles/r05/c2_side_dict_overlap.txt)
+#endif
+  if (MOX_SIDE_AFTER_MAP && side && !q.timing && !q.sync_each) {  // the next async pass's side build waits for this k_map
+    (void)hipEventRecord(e->ev_mapped, s);
+    e->mapped_pending = true;
+  }
   // 3. lanes
   hipLaunchKernelGGL(k_unicode, dim3(1024), dim3(256), 0, s, c, w, e->tables);  // + dictionary totals
   q.step("k_unicode");
@@ -684,7 +694,8 @@ int engine_create_one(const mox_config* cfg, int dev, mox_engine** out) {
   }
   for (auto& ev : e->ev) (void)hipEventCreate(&ev);
   if (hipStreamCreateWithFlags(&e->dstream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_dready, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&e->ev_dready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_mapped, hipEventDisableTiming) != hipSuccess) {
     mox_engine_destroy(e);
     return fail(MOX_EHIP, "side stream / events: creation failed");
   }
@@ -1048,6 +1059,7 @@ void mox_engine_destroy(mox_engine* e) {
   if (e->stream) (void)hipStreamDestroy(e->stream);
   if (e->dstream) (void)hipStreamDestroy(e->dstream);
   if (e->ev_dready) (void)hipEventDestroy(e->ev_dready);
+  if (e->ev_mapped) (void)hipEventDestroy(e->ev_mapped);
   delete e;
 }
 

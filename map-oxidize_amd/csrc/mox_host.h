@@ -111,6 +111,14 @@ struct mox_engine {
   // returns), so the side stream waits for nothing.
   hipStream_t dstream = nullptr;
   hipEvent_t ev_dready = nullptr;
+  // MOX_SIDE_AFTER_MAP=1 (mox_engine.hip): recorded right after an async
+  // pass's k_map, and the next pass's side build waits for it, so that the
+  // build runs beside the reduce tail rather than beside k_map (where the
+  // trace shows k_sample stretching k_map's launches by 10-120 us).  Measured
+  // 1.1 % slower end to end (the tail pays more than k_map saves), so off by
+  // default (profiles/r05/c2_side_dict_overlap.txt).
+  hipEvent_t ev_mapped = nullptr;
+  bool mapped_pending = false;  // ev_mapped recorded by a pass whose successor has not waited on it yet
   struct DictSet {
     WRec* cand = nullptr;
     uint32_t* dict_hist = nullptr;
