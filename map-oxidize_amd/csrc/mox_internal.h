@@ -69,12 +69,14 @@ constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
 #endif
 constexpr int MAP_ROW_WAVES = MOX_MAP_SELF ? MAP_WAVES : MAP_CONSUMERS;  // waves that process rows
 #ifndef MOX_MAP_AHEAD
-#define MOX_MAP_AHEAD 1  // rows a wave keeps loading ahead of the one it processes (1 or 2)
+#define MOX_MAP_AHEAD 1  // rows a wave keeps loading ahead of the one it processes (1 or 2; 2 fits with
+                         // -DMOX_DICT_SLOTS=4544 -DMOX_TIMING_ONLY_SMALL_DICT, a timing experiment)
 #endif
 constexpr int MAP_AHEAD = MOX_MAP_AHEAD;
 #ifndef MOX_MAP_PAIR
 #define MOX_MAP_PAIR 0  // 1: a wave processes two consecutive rows at once (do_pair), one pair loaded ahead
-                        // (MOX_MAP_SELF; its LDS needs a dictionary of <= 2,976 slots: a timing experiment)
+                        // (MOX_MAP_SELF; its LDS needs a dictionary of <= 2,784 slots with the list tails,
+                        // -DMOX_DICT_SLOTS=2784 -DMOX_TIMING_ONLY_SMALL_DICT: a timing experiment)
 #endif
 constexpr int MAP_PAIRW = MOX_MAP_PAIR ? 2 : 1;  // rows per buffer / list unit
 static_assert(!MOX_MAP_PAIR || (MOX_MAP_SELF && MOX_MAP_AHEAD == 1), "row pairs: self-loading, one pair ahead");
