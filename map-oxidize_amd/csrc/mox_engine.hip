@@ -87,7 +87,11 @@ int realloc_sized(mox_engine* e, const Caps& c) {
   Work n = e->w;
   // a multiple of 2 QF_MAX: every one of a region's QF_MAX slices holds an even
   // number of records, so k_map's paired records stay sector-aligned
-  n.cold_cap = (uint32_t)std::min<uint64_t>((c.cold_cap + 2 * QF_MAX - 1) & ~(uint64_t)(2 * QF_MAX - 1), COLD_CAP_MAX);
+#ifndef MOX_COLD_PAD
+#define MOX_COLD_PAD 0  // experiment: extra 2 QF_MAX-record steps per region (region stride off a power of two)
+#endif
+  n.cold_cap = (uint32_t)std::min<uint64_t>(((c.cold_cap + 2 * QF_MAX - 1) & ~(uint64_t)(2 * QF_MAX - 1)) + MOX_COLD_PAD * 2 * QF_MAX,
+                                            COLD_CAP_MAX);
   static_assert(COLD_CAP_MAX % (2 * QF_MAX) == 0 && COLD_CAP_MAX < (1u << 24), "cold_cap clamp (k_map: __umul24)");
   n.spill_cap = (uint32_t)std::min<uint64_t>(c.spill_cap, 0xFFFFFFF0u);
   n.w_cap = c.w_cap;
@@ -234,7 +238,7 @@ int alloc_fixed(mox_engine* e) {
 }
 
 constexpr size_t map_lds_bytes() { return MAP_LDS_BYTES; }  // (mox_internal.h)
-size_t reduce_lds_bytes() { return 2432 * (4 + 16 + 8) + 2048 * 2 + (2048 + 8) * 2 + 2048 * 2 + 16; }  // RED_SLOTS, RED_CAP, RED_SORTB (mox_kernels.hip)
+size_t reduce_lds_bytes() { return RED_LDS_BYTES; }
 
 float ev_ms(mox_engine* e, int a, int b) {
   float ms = 0;

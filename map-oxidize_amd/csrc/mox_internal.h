@@ -108,6 +108,17 @@ constexpr int SAMPLE_PIECE = 4096;          // one 256-thread workgroup x 16 B
 constexpr int SAMPLE_SLOTS = 2048;
 constexpr int DH_N = 258, DH_T = 259;       // dict_hist words after the histogram and pick counters
 constexpr int RED_THREADS = 1024;
+// k_reduce's LDS table: RED_BK home buckets of 4 slots plus one spare bucket
+// (bucket RED_BK - 1's overflow), RED_CAP distinct keys per (sub-)pass, then the
+// sort scratch (slot index, RED_SORTB bins, fill cursors) and 4 counters; 2
+// workgroups per CU
+constexpr int RED_BK = 608;
+constexpr int RED_BUCKETS = RED_BK + 1;
+constexpr int RED_SLOTS = 4 * RED_BUCKETS;
+constexpr int RED_CAP = 2048;
+constexpr int RED_SORTB = 2048;
+constexpr size_t RED_LDS_BYTES = (size_t)RED_SLOTS * (4 + 16 + 8) + RED_CAP * 2 + (RED_SORTB + 8) * 2 + RED_SORTB * 2 + 16;
+static_assert(RED_SLOTS * 4 % 16 == 0 && RED_LDS_BYTES + 256 <= 80 * 1024, "k_reduce LDS: 2 workgroups per CU");
 // High-cardinality split: a partition whose sampled records are
 // mostly distinct is scattered into 2^kk sub-buckets (the next kk hash bits), and
 // every (partition, sub-bucket) "unit" is reduced by its own workgroup.

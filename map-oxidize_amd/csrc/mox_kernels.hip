@@ -2450,13 +2450,13 @@ extern "C" __global__ __launch_bounds__(1024) void k_scatter(Work w) {
 // One workgroup per partition (2 per CU): group its cold records (count 1, one
 // contiguous region per map workgroup, streamed by one wave per region) and its
 // weighted records by exact 16-byte key in an LDS hash table of RED_BK buckets
-// x 4 slots (one ds_read_b128 of tags resolves a probe), sort the distinct keys
+// x 4 slots (one ds_read_b128 of tags resolves a probe; bucket RED_BK is spare:
+// only bucket RED_BK - 1 overflows into it, so a key's second bucket is always
+// the next one in LDS), sort the distinct keys
 // in key_less order (bucket sort + insertion sort in LDS) and write them out.  A partition with
 // more distinct keys than RED_CAP is redone in 2^k sub-passes over the next
 // hash bits.
-constexpr int RED_BK = 608;    // 2 workgroups per CU: table + sort scratch <= 80 KiB
-constexpr int RED_SLOTS = 4 * RED_BK;
-constexpr int RED_CAP = 2048;     // distinct keys per (sub-)pass; also the sort width
+// RED_BK, RED_SLOTS, RED_CAP, RED_SORTB: mox_internal.h (the host sizes the LDS)
 #ifndef MOX_RED_UNROLL
 #define MOX_RED_UNROLL 1  // 64-record chunks (round-4 A/B, profiles/r04/c2_k_reduce_depth_ab.txt)
 #endif
@@ -2464,7 +2464,6 @@ constexpr int RED_UNROLL = MOX_RED_UNROLL;
 #ifndef MOX_RED_DYN
 #define MOX_RED_DYN 1  // k_reduce waves take chunk pairs from an LDS ticket (0: static equal shares)
 #endif
-constexpr int RED_SORTB = 2048;  // bucket-sort bins (hash bits below the partition bits)
 #ifndef MOX_RED_TAB
 #define MOX_RED_TAB 1  // k_reduce: ticket -> region table (0: binary search per ticket)
 #endif
@@ -2546,15 +2545,10 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
         if (retry) {
           if (s.dbg) atomicAdd(&s.dbg[2], 1u);
         } else {
-          // the first free slot from the key's home slot (h & 3) on, wrapping
-          // inside the bucket: a key that finds its home free takes it, so
-          // red_home (MOX_RED_HOME) finds it in one LDS round trip
-          int e = -1;
-#pragma unroll
-          for (int j = 3; j >= 0; j--) {
-            const int i = (int)((h + (uint32_t)j) & 3u);
-            if (tv[i] == 0) e = i;
-          }
+          // the bucket's first free slot: a bucket fills from slot 0 on and
+          // slots never empty, so its taken slots are a prefix (red_try relies
+          // on it)
+          const int e = tv[0] == 0 ? 0 : tv[1] == 0 ? 1 : tv[2] == 0 ? 2 : tv[3] == 0 ? 3 : -1;
           if (e >= 0) {
             const uint32_t sl = 4 * b + e;
             if (atomicCAS(const_cast<uint32_t*>(&tags[sl]), 0u, h) == 0u) {
@@ -2567,13 +2561,13 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
               done = true;
             }  // lost the slot: re-read this bucket
           } else {
-            b = b + 1 == RED_BK ? 0 : b + 1;
+            b = b + 1 == RED_BUCKETS ? 0 : b + 1;
             ++probes;
           }
         }
         // every bucket seen full, or (never expected) a publication that does
         // not land: the table overflows, the unit is redone in sub-passes
-        if (!done && (probes >= (uint32_t)RED_BK || ++it >= 64u * RED_BK)) {
+        if (!done && (probes >= (uint32_t)RED_BUCKETS || ++it >= 64u * RED_BUCKETS)) {
           s.misc[1] = 1;
           done = true;
         }
@@ -2586,71 +2580,64 @@ __device__ void red_insert(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
 }
 
 #ifndef MOX_RED_FASTINS
-#define MOX_RED_FASTINS 1  // red_try also inserts a new key whose home bucket has room
+#define MOX_RED_FASTINS 1  // red_try also inserts a new key into a free slot of its first two buckets
 #endif
-// Fast path for records whose key is already published in its home bucket or
-// the next one (keys overflow at most one bucket at this table load): two tag
-// reads issued together, one key read, one add.  Returns false when the slow
-// path is needed (new key, further bucket, publication pending).
-__device__ __forceinline__ bool red_try(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
-  const uint32_t b = red_bucket(h), b2 = b + 1 == RED_BK ? 0 : b + 1;
-  const uint4 t = s.tag4[b], t2 = s.tag4[b2];
-  // first matching tag as an index 0..7 (8: none), each select taking an inline
-  // constant; slots 4 b .. 4 b + 3 then 4 b2 ..
-  uint32_t ix = t2.w == h ? 7u : 8u;
-  ix = t2.z == h ? 6u : ix;
-  ix = t2.y == h ? 5u : ix;
-  ix = t2.x == h ? 4u : ix;
-  ix = t.w == h ? 3u : ix;
-  ix = t.z == h ? 2u : ix;
-  ix = t.y == h ? 1u : ix;
-  ix = t.x == h ? 0u : ix;
-  if (ix == 8u) {
-#if MOX_RED_FASTINS
-    // Not in its first two buckets.  If its home bucket has room the key is in
-    // no bucket at all (a key goes to the first bucket with room when it is
-    // inserted, and buckets never empty): claim the bucket's first free slot
-    // from the home slot on -- the rule red_insert uses, so that two inserters
-    // of one key always race for the same slot -- and publish it here,
-    // instead of sending the lane into red_insert's wave loop (which ~90 % of
-    // 64-record chunks entered for their ~2 new keys).
-    const uint32_t tv[4] = {t.x, t.y, t.z, t.w};
-    int e = -1;
-#pragma unroll
-    for (int j = 3; j >= 0; j--) {
-      const int i = (int)((h + (uint32_t)j) & 3u);
-      if (tv[i] == 0) e = i;
-    }
-    if (e < 0) return false;
-    const uint32_t fs = 4 * b + (uint32_t)e;
-    if (atomicCAS(reinterpret_cast<uint32_t*>(s.tag4) + fs, 0u, h) != 0u) return false;  // lost it: red_insert re-reads
-    s.key[fs] = k;
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    atomicAdd(&s.cnt[fs], (unsigned long long)c);
-    const uint32_t u = atomicAdd(&s.misc[0], 1u);
-    if (u >= RED_CAP) s.misc[1] = 1;
-    return true;
-#else
-    return false;
-#endif
-  }
-  const int sl = (int)(ix < 4u ? 4 * b + ix : 4 * b2 + (ix - 4u));
+enum : int { RED_MISS = 0, RED_ADDED = 1, RED_NEW = 2 };
+// Fast path: the key's home bucket and the next one (keys overflow at most one
+// bucket at this table load), their tags read together.  A bucket's taken
+// slots are a prefix (red_insert), and a key sits in the first bucket that had
+// room when it was inserted, so along those 8 slots the key is at the first
+// slot that holds its tag or is free -- if that slot is free, the key is in
+// no bucket at all and is claimed there, published in place instead of in
+// red_insert's wave loop.  The slot's tag, key and count are read in one
+// round trip.  RED_MISS (slow path): both buckets full without the key, a
+// publication pending, a lost claim, or another key with the same tag.
+__device__ __forceinline__ int red_try(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
+  const uint32_t b = red_bucket(h);
+  const uint4 t = s.tag4[b], t2 = s.tag4[b + 1];
+  // first slot whose tag has no bit outside h: tag h or free (0), or -- about
+  // 1e-4 of other tags -- a tag whose bits are a subset of h's, caught by the
+  // re-read below; each select takes an inline constant
+  const uint32_t nh = ~h;
+  uint32_t ix = (t2.w & nh) == 0 ? 7u : 8u;
+  ix = (t2.z & nh) == 0 ? 6u : ix;
+  ix = (t2.y & nh) == 0 ? 5u : ix;
+  ix = (t2.x & nh) == 0 ? 4u : ix;
+  ix = (t.w & nh) == 0 ? 3u : ix;
+  ix = (t.z & nh) == 0 ? 2u : ix;
+  ix = (t.y & nh) == 0 ? 1u : ix;
+  ix = (t.x & nh) == 0 ? 0u : ix;
+  if (ix == 8u) return RED_MISS;
+  const uint32_t sl = 4 * b + ix;
+  uint32_t* tags = reinterpret_cast<uint32_t*>(s.tag4);
+  const uint32_t tg = __hip_atomic_load(&tags[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   const uint4 kk = s.key[sl];
   const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (cv == 0 || !key_eq16(kk, k)) return false;
-  if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
-  else atomicAdd(&s.cnt[sl], (unsigned long long)c);
-  return true;
+  if (tg == h) {
+    if (cv == 0 || !key_eq16(kk, k)) return RED_MISS;
+    if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
+    else atomicAdd(&s.cnt[sl], (unsigned long long)c);
+    return RED_ADDED;
+  }
+#if MOX_RED_FASTINS
+  if (tg != 0 || atomicCAS(&tags[sl], 0u, h) != 0u) return RED_MISS;  // taken since: red_insert re-reads
+  s.key[sl] = k;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  atomicAdd(&s.cnt[sl], (unsigned long long)c);
+  return RED_NEW;  // the caller counts it in misc[0]
+#else
+  return RED_MISS;
+#endif
 }
 
-// Fast path for a key sitting in its home slot (the slot red_insert tries
-// first): tag, key and count read in one LDS round trip, 28 bytes.
+// Fast path for a key sitting in its home bucket's first slot: tag, key and
+// count read in one LDS round trip, 28 bytes.
 #ifndef MOX_RED_HOME
 #define MOX_RED_HOME 0
 #endif
 __device__ __forceinline__ bool red_home(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
-  const uint32_t sl = 4 * red_bucket(h) + (h & 3u);
+  const uint32_t sl = 4 * red_bucket(h);
   const uint32_t t = reinterpret_cast<const uint32_t*>(s.tag4)[sl];
   const uint4 kk = s.key[sl];
   const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -3422,9 +3409,20 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
               for (int u2 = 0; u2 < RED_UNROLL; u2++)
                 if (todo[u2]) todo[u2] = !red_home(s, h[u2], cur[u2], 1);
             }
+            uint32_t nnew = 0;
 #pragma unroll
-            for (int u2 = 0; u2 < RED_UNROLL; u2++)
-              if (todo[u2]) todo[u2] = !red_try(s, h[u2], cur[u2], 1);
+            for (int u2 = 0; u2 < RED_UNROLL; u2++) {
+              int r = RED_MISS;
+              if (todo[u2]) r = red_try(s, h[u2], cur[u2], 1);
+              todo[u2] = todo[u2] && r == RED_MISS;
+              nnew += (uint32_t)__popcll(__ballot(r == RED_NEW));
+            }
+            // the chunk's new keys counted at once (one lane, one LDS atomic);
+            // past RED_CAP the unit is redone in sub-passes
+            if (nnew && lane == 0) {
+              const uint32_t u0 = lds_fetch_add_lane(&s.misc[0], nnew);
+              if (u0 + nnew > (uint32_t)RED_CAP) s.misc[1] = 1;
+            }
             RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
@@ -3493,9 +3491,15 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         const WRec rr = wsrc[i];
         const uint4 k = make_uint4((uint32_t)rr.w0, (uint32_t)(rr.w0 >> 32), (uint32_t)rr.w1, (uint32_t)(rr.w1 >> 32));
         const uint32_t h = hash32(k.x, k.y, k.z, k.w);
-        if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && in_sub(h, shift0, kk, sub) &&
-            !red_try(s, h, k, rr.count))
-          red_insert(s, h, k, rr.count);
+        if (!__hip_atomic_load(&s.misc[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) && in_sub(h, shift0, kk, sub)) {
+          const int r = red_try(s, h, k, rr.count);
+          if (r == RED_MISS) {
+            red_insert(s, h, k, rr.count);
+          } else if (r == RED_NEW) {
+            const uint32_t u0 = atomicAdd(&s.misc[0], 1u);
+            if (u0 >= (uint32_t)RED_CAP) s.misc[1] = 1;
+          }
+        }
       }
       __syncthreads();
       if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the unit
