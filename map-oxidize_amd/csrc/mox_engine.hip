@@ -461,8 +461,12 @@ FILE* debug_file(const char* name) {
   return fopen((std::string(dir) + "/" + name).c_str(), "w");
 }
 void debug_dump(mox_engine* e, const Ctl& h) {
-  if (e->w.dbg & DBG_COUNT)  // k_reduce slow path: inserts, lane iterations not done, publication retries
-    fprintf(stderr, "mox dbg_cnt %llu %llu %llu\n", h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2]);
+  // k_reduce slow path: inserts, lane iterations not done, publication retries,
+  // cold-stream slow lanes; red_try misses: two buckets full, publication
+  // pending, same tag + other key, lost claim not resolved
+  if (e->w.dbg & DBG_COUNT)
+    fprintf(stderr, "mox dbg_cnt %llu %llu %llu %llu | %llu %llu %llu %llu\n", h.dbg_cnt[0], h.dbg_cnt[1], h.dbg_cnt[2],
+            h.dbg_cnt[3], h.dbg_cnt[4], h.dbg_cnt[5], h.dbg_cnt[6], h.dbg_cnt[7]);
   if ((e->w.dbg & DBG_STAMP) && e->w.stamps) {
     std::vector<unsigned long long> st(8 * NB);
     (void)hipMemcpy(st.data(), e->w.stamps, st.size() * 8, hipMemcpyDeviceToHost);

@@ -205,7 +205,7 @@ struct Ctl {
   unsigned long long cold_need;   // max records any (workgroup, partition) region asked for
   unsigned long long spill_need;  // max spill records of any map workgroup
   unsigned long long w_total;     // weighted + spilled records
-  unsigned long long dbg_cnt[4];  // MOX_DBG & DBG_COUNT instrumentation
+  unsigned long long dbg_cnt[8];  // MOX_DBG & DBG_COUNT instrumentation
   unsigned long long n_units;     // reduce units (>= NB; > NB when partitions were split)
   unsigned long long red_ticket;  // k_reduce work queue
   unsigned long long split_k;     // cold records of split partitions

@@ -246,7 +246,6 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 // dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
 // bits.  Final table order is (h32, hash32b, key) (key_less), so it is deterministic.
 __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  // 3-input xor in one v_bitop3_b32 (0x96)
   uint32_t a = __builtin_amdgcn_bitop3_b32(k0, __builtin_rotateleft32(k1, 11), __builtin_rotateleft32(k2, 21), 0x96);
   a ^= __builtin_rotateleft32(k3, 6);
   a *= 0x9E3779B1u;
@@ -2607,25 +2606,71 @@ __device__ __forceinline__ int red_try(const RedLds& s, uint32_t h, uint4 k, uin
   ix = (t.z & nh) == 0 ? 2u : ix;
   ix = (t.y & nh) == 0 ? 1u : ix;
   ix = (t.x & nh) == 0 ? 0u : ix;
-  if (ix == 8u) return RED_MISS;
+  if (ix == 8u) {
+    if (s.dbg) atomicAdd(&s.dbg[4], 1u);  // DBG_COUNT: miss reasons [4] .. [7]
+    return RED_MISS;
+  }
   const uint32_t sl = 4 * b + ix;
   uint32_t* tags = reinterpret_cast<uint32_t*>(s.tag4);
+  // count before key (one round trip: LDS runs a wave's reads in order): a
+  // published count (> 0) means the key read after it sees the key, stored
+  // before the count by its claimant.  (Key first, ~275 K records per C2
+  // pass read a stale key beside a fresh count and took the slow path.)
   const uint32_t tg = __hip_atomic_load(&tags[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  const uint4 kk = s.key[sl];
-  const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  uint4 kk = s.key[sl];
   if (tg == h) {
-    if (cv == 0 || !key_eq16(kk, k)) return RED_MISS;
+    if (cv == 0) {  // claimed, not yet published (its claimant is a few LDS operations from it): once more
+      cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      kk = s.key[sl];
+    }
+    if (cv == 0 || !key_eq16(kk, k)) {
+      if (s.dbg) atomicAdd(&s.dbg[cv == 0 ? 5 : 6], 1u);
+      return RED_MISS;
+    }
     if (s.plain) s.cnt[sl] = cv + c;  // timing experiment only (DBG_RED_PLAINADD): loses counts
     else atomicAdd(&s.cnt[sl], (unsigned long long)c);
     return RED_ADDED;
   }
 #if MOX_RED_FASTINS
-  if (tg != 0 || atomicCAS(&tags[sl], 0u, h) != 0u) return RED_MISS;  // taken since: red_insert re-reads
-  s.key[sl] = k;
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-  atomicAdd(&s.cnt[sl], (unsigned long long)c);
-  return RED_NEW;  // the caller counts it in misc[0]
+  // claim: CAS from this slot on along the two buckets.  A slot lost to
+  // another key moves the claim to the next slot (the slots before it are
+  // taken by other keys and stay so); a slot lost to tag h was most often
+  // claimed by the same key from another lane of this wave, whose claim is
+  // published by the time the lane reads it -- the count is added there.
+  // (At a partition's start ~1,000 lanes of 16 waves insert into the empty
+  // table at once and about half of them meet in a slot.)
+  for (uint32_t slc = sl;;) {
+    const uint32_t prev = atomicCAS(&tags[slc], 0u, h);
+    if (prev == 0u) {
+      s.key[slc] = k;
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      atomicAdd(&s.cnt[slc], (unsigned long long)c);
+    }
+    // the wave's claims are published above before any lane reads below (LDS
+    // executes a wave's instructions in order; the compiler may not move the
+    // reads up into or above the branch)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (prev == 0u) return RED_NEW;  // the caller counts it in misc[0]
+    if (prev == h) {
+      const unsigned long long c2 = __hip_atomic_load(&s.cnt[slc], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      const uint4 k2 = s.key[slc];
+      if (c2 == 0 || !key_eq16(k2, k)) {
+        if (s.dbg) atomicAdd(&s.dbg[7], 1u);
+        return RED_MISS;
+      }
+      atomicAdd(&s.cnt[slc], (unsigned long long)c);
+      return RED_ADDED;
+    }
+    if (++slc == 4 * b + 8) {  // both buckets full: red_insert walks on
+      if (s.dbg) atomicAdd(&s.dbg[4], 1u);
+      return RED_MISS;
+    }
+  }
 #else
   return RED_MISS;
 #endif
@@ -3200,7 +3245,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   s.bin = (uint16_t*)sp; sp += (RED_SORTB + 8) * 2;
   s.fill = (uint16_t*)sp; sp += RED_SORTB * 2;
   s.misc = (uint32_t*)sp; sp += 16;
-  __shared__ uint32_t dbgc[4];
+  __shared__ uint32_t dbgc[8];
   __shared__ uint32_t s_unit;
   __shared__ uint64_t red_wsum[RED_THREADS / 64];
   uint32_t* rpre = reinterpret_cast<uint32_t*>(s.idx);  // region prefix (G + 1 words in the idx + bin space)
@@ -3209,7 +3254,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
   s.dbg = MOX_ABL(w.dbg, DBG_COUNT) ? dbgc : nullptr;
   s.plain = MOX_ABL(w.dbg, DBG_RED_PLAINADD) != 0;
   s.ctl = w.ctl;
-  if (threadIdx.x < 4) dbgc[threadIdx.x] = 0;
+  if (threadIdx.x < 8) dbgc[threadIdx.x] = 0;
   const int tid = threadIdx.x, lane = tid & 63;
   [[maybe_unused]] const int wv = tid >> 6;
   [[maybe_unused]] constexpr int NWV = RED_THREADS / 64;
@@ -3308,6 +3353,10 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 #endif
         const uint32_t n = split ? kin_n : rpre[G];
         constexpr uint32_t CH = 64 * RED_UNROLL;
+        // in_sub as one masked compare: hash bits [32 - shift0 - kk, 32 - shift0)
+        // equal sub (shift0 + kk <= 32 in every pass that runs; kk == 0: all)
+        const uint32_t sub_mask = kk ? ((1u << kk) - 1u) << (32 - shift0 - kk) : 0u;
+        const uint32_t sub_val = kk ? sub << (32 - shift0 - kk) : 0u;
 #if MOX_RED_DYN
         // dynamic shares: waves take the next 2 chunks from an LDS ticket, so
         // they finish within ~2 chunks of each other (static equal shares left
@@ -3400,7 +3449,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 #pragma unroll
           for (int u2 = 0; u2 < RED_UNROLL; u2++) {
             h[u2] = hash32(cur[u2].x, cur[u2].y, cur[u2].z, cur[u2].w);
-            todo[u2] = c + u2 * 64 + lane < a1 && in_sub(h[u2], shift0, kk, sub);
+            todo[u2] = c + u2 * 64 + lane < a1 && ((h[u2] ^ sub_val) & sub_mask) == 0u;  // in_sub
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
@@ -3426,7 +3475,10 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
             RED_MARK(2);
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++)
-              if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) red_insert(s, h[u2], cur[u2], 1);
+              if (todo[u2] && !MOX_ABL(w.dbg, DBG_RED_NOSLOW)) {
+                if (s.dbg) atomicAdd(&s.dbg[3], 1u);  // cold-stream lanes on the slow path
+                red_insert(s, h[u2], cur[u2], 1);
+              }
             RED_MARK(3);
           } else {
 #pragma unroll
@@ -3504,9 +3556,9 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       __syncthreads();
       if (s.misc[1]) {  // too many distinct keys for one table: split further, redo the unit
         kk++;
-        // the redo must not see this attempt's keys (red_try reads a slot's key
-        // before its count: only a key that cannot be the one compared may sit
-        // in a slot being claimed)
+        // the redo does not see this attempt's keys (readers take a slot's key
+        // only after its published count, and counts restart at 0; cleared
+        // anyway, so no stale key ever sits in a slot being claimed)
         for (int i = tid; i < RED_SLOTS; i += RED_THREADS) s.key[i] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         if (shift0 + kk > 32) {  // > RED_CAP distinct keys share every hash bit: cannot split
@@ -3603,7 +3655,7 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
 #endif
   if (tid == 0) {
     if (max_kk) atomicMax(&w.ctl->max_sub, 1u << max_kk);
-    if (s.dbg) for (int i = 0; i < 3; i++) atomicAdd(&w.ctl->dbg_cnt[i], (unsigned long long)dbgc[i]);
+    if (s.dbg) for (int i = 0; i < 8; i++) atomicAdd(&w.ctl->dbg_cnt[i], (unsigned long long)dbgc[i]);
   }
 }
 
