@@ -241,13 +241,25 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 
 // ------------------------------------------------------------------ map kernel
 // 32-bit key hash of a short (<= 16 byte) key given as 4 little-endian dwords:
-// a rotate/xor fold then a two-round multiply-xorshift finaliser.  Bit use:
+// a multiply/xor fold then a two-round multiply-xorshift finaliser.  Bit use:
 // partition = top NB_LOG2 bits, dictionary home slot = low 12 bits, second
 // dictionary group = bits 12..21; reduce slots use a multiplicative hash of all
 // bits.  Final table order is (h32, hash32b, key) (key_less), so it is deterministic.
+// The fold: k0 ^ k1 C ^ rotl(k2, 21) ^ rotl(k3, 6) (C odd: the product a
+// bijection of k1), one v_mul_lo_u32, two v_alignbit and one 3-input v_bitop3
+// + xor.  Until round 5 k1 was rotated by 11 instead of multiplied, the same
+// instruction count, but the fold was then linear over GF(2) on ASCII bytes
+// whose high bits agree: over the ZIPF vocabulary's 3.76 M keys (with trailing
+// marks) it gave 173,889 colliding pairs against ~1,650 for a random 32-bit
+// hash (this fold: 2,353; three multiplies: 1,768, but k_map +1.5 %); HICARD-
+// like keys 8,031 against ~1,180 (this: 1,198).  Equal hashes of different
+// keys are correct everywhere but slow: k_reduce sent ~275 K records per C2
+// pass to its insert loop on them (profiles/r05/hash_fold_collisions.txt).
+__device__ __forceinline__ uint32_t hash_fold(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  return __builtin_amdgcn_bitop3_b32(k0, k1 * 0x85EBCA77u, __builtin_rotateleft32(k2, 21), 0x96) ^ __builtin_rotateleft32(k3, 6);
+}
 __device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t a = __builtin_amdgcn_bitop3_b32(k0, __builtin_rotateleft32(k1, 11), __builtin_rotateleft32(k2, 21), 0x96);
-  a ^= __builtin_rotateleft32(k3, 6);
+  uint32_t a = hash_fold(k0, k1, k2, k3);
   a *= 0x9E3779B1u;
   a ^= a >> 15;
   a *= 0x85EBCA6Bu;
@@ -267,8 +279,7 @@ __device__ __forceinline__ uint32_t hash32_map(uint32_t k0, uint32_t k1, uint32_
 #ifdef MOX_HASH_COLLIDE
   return hash32(k0, k1, k2, k3);
 #else
-  uint32_t a = __builtin_amdgcn_bitop3_b32(k0, __builtin_rotateleft32(k1, 11), __builtin_rotateleft32(k2, 21), 0x96);
-  a ^= __builtin_rotateleft32(k3, 6);
+  uint32_t a = hash_fold(k0, k1, k2, k3);
   a *= 0x9E3779B1u;
   a ^= a >> 15;
   a *= 0x85EBCA6Bu;
@@ -2695,7 +2706,8 @@ __device__ __forceinline__ bool red_home(const RedLds& s, uint32_t h, uint4 k, u
 // it (k_reduce, k_reduce_small, k_reduce_sort1), so the order does not depend
 // on which kernel a key's unit went to, nor on whether its partition was split.
 __device__ __forceinline__ uint32_t hash32b(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t a = k1 ^ __builtin_rotateleft32(k0, 7) ^ __builtin_rotateleft32(k3, 17) ^ __builtin_rotateleft32(k2, 27);
+  // (the tie-break after h32: a different fold, multiply/xor as hash_fold's)
+  uint32_t a = k1 ^ k0 * 0x2127599Bu ^ k3 * 0x165667B1u ^ k2 * 0xD3A2646Du;
   a *= 0x2C1B3C6Du;
   a ^= a >> 12;
   a *= 0x297A2D39u;
