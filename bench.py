@@ -61,8 +61,12 @@ WORKLOADS = {
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    # the GPU's first ~15 passes after the corpus upload run slower (a clock /
+    # power transient: C2 k_map 750-800 us in passes 3-6, ~690 from pass ~15 on,
+    # profiles/r05/bench_warmup_transient.txt); 20 untimed passes measure the
+    # steady state (C2: warmup 3 -> 927-931 GB/s, 10 -> 965-969, 20 -> 974-976)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workload", default="", choices=[""] + sorted(WORKLOADS),
                     help="default: C2 at N = 1, C3 (8 GiB shard per GPU) at N > 1")
     ap.add_argument("--no-gather", action="store_true", help="N > 1: leave the final tables on their owner ranks")
