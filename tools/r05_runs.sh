@@ -36,7 +36,7 @@ evid)
   timeout -k 10 400 python -u bench.py > $O/bench_c2.json 2> $O/bench_c2.err; step "bench C2" $?
   cut -c1-300 $O/bench_c2.json
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2 -o run -- \
-    python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > $O/c2_under_rocprof.log 2>&1; step "rocprof C2" $?
+    python3 bench.py --no-cpu-baseline > $O/c2_under_rocprof.log 2>&1; step "rocprof C2" $?
   python3 tools/trace_timeline.py $O/c2 > $O/c2_timeline.txt; step "timeline C2" $?
   tail -1 $O/c2_timeline.txt
   ;;
