@@ -258,12 +258,23 @@ __device__ void long_insert(const W& w, const uint8_t* base, uint64_t h, uint64_
 __device__ __forceinline__ uint32_t hash_fold(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
   return __builtin_amdgcn_bitop3_b32(k0, k1 * 0x85EBCA77u, __builtin_rotateleft32(k2, 21), 0x96) ^ __builtin_rotateleft32(k3, 6);
 }
-__device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
-  uint32_t a = hash_fold(k0, k1, k2, k3);
+// The finaliser, a bijection of the fold (collisions are the fold's alone).
+// MOX_HASH_FIN1: one multiply-xorshift round, a * C ^ (a * C) >> 16: its top
+// bits (partition), low and high 16 bits (dictionary slots, k_reduce bucket)
+// are as uniform over the ZIPF vocabulary as the two-round finaliser's
+// (chi2 / dof 0.89-1.03, tools/hash_collisions.py's keys), three VALU fewer.
+#ifndef MOX_HASH_FIN1
+#define MOX_HASH_FIN1 1
+#endif
+__device__ __forceinline__ uint32_t hash_fin(uint32_t a) {
   a *= 0x9E3779B1u;
+  if (MOX_HASH_FIN1) return a ^ (a >> 16);
   a ^= a >> 15;
   a *= 0x85EBCA6Bu;
-  a ^= a >> 13;
+  return a ^ (a >> 13);
+}
+__device__ __forceinline__ uint32_t hash32(uint32_t k0, uint32_t k1, uint32_t k2, uint32_t k3) {
+  const uint32_t a = hash_fin(hash_fold(k0, k1, k2, k3));
   // never 0: 0 marks a free slot in the dictionary and k_reduce tag arrays (a
   // key hashing to 0 would spin on a "free" slot); 1 simply shares its hash
   return max(collide32(a, MOX_H32_BITS), 1u);  // collide32: identity except in the collision build
@@ -279,11 +290,7 @@ __device__ __forceinline__ uint32_t hash32_map(uint32_t k0, uint32_t k1, uint32_
 #ifdef MOX_HASH_COLLIDE
   return hash32(k0, k1, k2, k3);
 #else
-  uint32_t a = hash_fold(k0, k1, k2, k3);
-  a *= 0x9E3779B1u;
-  a ^= a >> 15;
-  a *= 0x85EBCA6Bu;
-  return a ^ (a >> 13);
+  return hash_fin(hash_fold(k0, k1, k2, k3));
 #endif
 }
 __device__ __forceinline__ uint32_t key_hash(uint64_t w0, uint64_t w1) {
