@@ -277,6 +277,15 @@ int mox_print_top_words(const mox_table* t, size_t n);
  * mox_fetch_table like a run's.  Duplicate words are summed. */
 int mox_reduce_pairs(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n);
 
+/* ---- test hook (no GPU needed) ---- */
+/* The exchange's per-peer send / receive layout (mox_multi.hip x_layout) for
+ * nranks ranks whose count rows are counts[i][d][0..2] = (short records, long
+ * words, long-word bytes) that rank i sends to rank d, the count all-to-all
+ * modelled as the device-copy transport does it.  out[i][k][d], k = 0..7:
+ * short send offset / length, blob send offset / length, short receive offset /
+ * length, blob receive offset / length of rank i for peer d (bytes). */
+int mox_debug_exchange_layout(int nranks, const uint64_t* counts, uint64_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,16 +10,14 @@ namespace mox {
 constexpr int MAP_THREADS = 1024;           // 16 waves; one persistent workgroup per CU
 constexpr int MAP_WG_PER_CU = 1;
 constexpr int MAP_MIN_WAVES = 1;
-#ifndef MOX_LD_BATCH
-#define MOX_LD_BATCH 1  // k_map loader: poll, write and publish a row group at once (0: row by row)
+// Ablation switches (MOX_DBG env, below) and the tools' variant builds are
+// experiments: several produce wrong counts by design.  They compile only
+// together with MOX_EXPERIMENT_BUILD, which tools/build_variant.sh sets and no
+// product target (Makefile) does.
+#if defined(MOX_ABLATE) && !defined(MOX_EXPERIMENT_BUILD)
+#error "MOX_ABLATE is an experiment build (tools/build_variant.sh): not for the product library"
 #endif
-#ifndef MOX_LD_FENCE
-#define MOX_LD_FENCE 1  // k_map loader: a scheduling fence after each row group's loads (mox_kernels.hip)
-#endif
-#ifndef MOX_MAP_LOADERS
-#define MOX_MAP_LOADERS 1
-#endif
-constexpr int MAP_LOADERS = MOX_MAP_LOADERS;  // loader waves (alternate row groups)
+constexpr int MAP_LOADERS = 1;              // loader waves
 #ifndef MOX_LD_SLEEP
 #define MOX_LD_SLEEP 1  // k_map loader's poll for a free ring slot (s_sleep units of 64 clocks)
 #endif
@@ -57,31 +55,10 @@ constexpr int KSEL_N = 17 * 4;              // k_map key selectors: key length 0
 constexpr int LD_GROUP = MOX_LD_GROUP;      // loader: rows per register group
 constexpr int LD_GROUPS = MOX_LD_GROUPS;    // groups in flight (LD_GROUP x (LD_GROUPS-1) rows outstanding)
 constexpr int MAP_CONSUMERS = MAP_WAVES - MAP_LOADERS;
-// k_map row supply.  0 (default): one loader wave + the LDS ring.  1: every
-// wave loads its own rows, MOX_MAP_AHEAD rows ahead, by LDS-DMA into row
-// buffers of its own (no loader wave, no ring); the wait for a row's DMA
-// counts the wave's cold-record stores issued since (mox_kernels.hip, k_map).
-// It removes the ring's supply floor (427-489 us at C2 -> 242 us one row
-// ahead, 174 us two ahead) but measured 1.5-4 % slower on the whole kernel
-// (DESIGN.md §8, round 5): the consumers, not the supply, bind.
-#ifndef MOX_MAP_SELF
-#define MOX_MAP_SELF 0
-#endif
-constexpr int MAP_ROW_WAVES = MOX_MAP_SELF ? MAP_WAVES : MAP_CONSUMERS;  // waves that process rows
-#ifndef MOX_MAP_AHEAD
-#define MOX_MAP_AHEAD 1  // rows a wave keeps loading ahead of the one it processes (1 or 2; 2 fits with
-                         // -DMOX_DICT_SLOTS=4544 -DMOX_TIMING_ONLY_SMALL_DICT, a timing experiment)
-#endif
-constexpr int MAP_AHEAD = MOX_MAP_AHEAD;
-#ifndef MOX_MAP_PAIR
-#define MOX_MAP_PAIR 0  // 1: a wave processes two consecutive rows at once (do_pair), one pair loaded ahead
-                        // (MOX_MAP_SELF; its LDS needs a dictionary of <= 2,784 slots with the list tails,
-                        // -DMOX_DICT_SLOTS=2784 -DMOX_TIMING_ONLY_SMALL_DICT: a timing experiment)
-#endif
-constexpr int MAP_PAIRW = MOX_MAP_PAIR ? 2 : 1;  // rows per buffer / list unit
-static_assert(!MOX_MAP_PAIR || (MOX_MAP_SELF && MOX_MAP_AHEAD == 1), "row pairs: self-loading, one pair ahead");
-constexpr int MAP_BUFS = MAP_AHEAD + 1;     // row buffers per wave
-static_assert(MAP_AHEAD == 1 || MAP_AHEAD == 2, "k_map rows ahead");
+// (Rows loaded by their own wave by LDS-DMA, with no loader or ring, removed the
+// ring's supply floor but measured 1.5-4 % slower on the whole kernel; two rows
+// per wave tied with the ring at a smaller dictionary: DESIGN.md §8, round 5.)
+constexpr int MAP_ROW_WAVES = MAP_CONSUMERS;  // waves that process rows
 static_assert(TOKMAX - 1 >= PAY / 2, "list[TOKMAX - 1] is the token-loop sink: no row may reach it");
 // A k_map token list: up to TOKMAX entries of a row, then 64 entries of tail
 // (LIST_ODD, written after every row's list) that the token pass reads past
@@ -96,11 +73,10 @@ constexpr int NB = 1 << NB_LOG2;
 constexpr uint64_t COLD_CAP_MAX = (1ull << 32) / (16ull * NB);
 constexpr uint32_t QF_MAX = 4;              // most cold regions per (map workgroup, partition) (k_map without a dictionary)
 // k_map dynamic LDS (carved in this order by k_map): dictionary counts, region
-// counters, misc, key selectors, dictionary keys, then the row supply (per-wave
-// row buffers, or the ring with its ready / free words) and the token lists
+// counters, misc, key selectors, dictionary keys, then the row ring with its
+// ready / free words and the token lists
 constexpr size_t MAP_LDS_BYTES = (size_t)DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 +
-                                 (MOX_MAP_SELF ? (size_t)MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT : (size_t)RING * 8 + (size_t)RING * SLOT) +
-                                 (size_t)MAP_ROW_WAVES * 2 * LIST_N * MAP_PAIRW;
+                                 (size_t)RING * 8 + (size_t)RING * SLOT + (size_t)MAP_ROW_WAVES * 2 * LIST_N;
 static_assert(MAP_LDS_BYTES <= 160 * 1024, "k_map LDS over 160 KiB");
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)
 constexpr int MAX_SAMPLE_PIECES = 1024;
@@ -158,9 +134,7 @@ enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO
                   DBG_PAIR_NOSTORE = 8192u, // no dictionary: pairs formed, their global stores skipped (timing only)
                   DBG_NOPAIR = 16384u,      // no dictionary: every record stored alone, no pair slots (timing A/B)
                   DBG_PAIR_SEQ = 32768u,    // no dictionary: pairs stored at consecutive addresses (timing only: wrong regions)
-                  DBG_S1_SORT2 = 65536u,    // k_reduce_sort1/2 sort every unit's keys twice (timing only, same result)
-                  DBG_COLD_SEQ = 131072u,   // k_map dictionary pass: cold records all into partition 0's region (timing only)
-                  DBG_COLD_NOSTORE = 262144u };  // k_map dictionary pass: region slots reserved, records not stored (timing only)
+                  DBG_S1_SORT2 = 65536u };  // k_reduce_sort1/2 sort every unit's keys twice (timing only, same result)
 // Bounds checks of derived indices (UnitDesc ranges, scatter cursors, table
 // offsets), compiled in only with -DMOX_CHECK (libmox_check.so, `make check`):
 // a failed check counts into ctl->dbg_cnt[0], records the largest site id in
@@ -168,7 +142,9 @@ enum : uint32_t { DBG_NO_TOKENS = 1u, DBG_NO_EMIT = 2u, DBG_NO_DICT = 4u, DBG_NO
 // Production builds evaluate to true and emit nothing.
 enum : uint32_t {
   CHK_SMALL_DESC = 1u, CHK_SMALL_OUT = 2u, CHK_RED_OUT = 3u, CHK_SPLIT_K = 4u, CHK_SPLIT_W = 5u, CHK_UNIT = 6u,
-  CHK_MAT_ROW = 7u, CHK_MAT_BYTES = 8u, CHK_SCATTER = 9u, CHK_RED_IN = 10u, CHK_GATHER = 11u
+  CHK_MAT_ROW = 7u, CHK_MAT_BYTES = 8u, CHK_SCATTER = 9u, CHK_RED_IN = 10u, CHK_GATHER = 11u,
+  CHK_RED_TABLE = 12u,  // k_reduce table: a bucket's taken slots not a prefix, or one key in two slots
+  CHK_RED_NU = 13u      // k_reduce: taken slots != counted new keys
 };
 #ifdef MOX_CHECK
 #define MOX_CHK(w, ok, site) (::mox::chk_record((w).ctl, (ok), (site)))

@@ -363,19 +363,19 @@ struct MapLds {
 // (k_map has no static LDS; checked at entry, Ctl::layout_err).  As constants
 // the compiler folds them into the LDS instructions' 16-bit offset field (from
 // the extern array's symbol it added the base per access, v_add_u32 v, 0, v).
-// The row supply comes first, so every row slot (row pair) is SLOT-aligned and
-// key_load ORs a token's 4-aligned offset into its slot address (v_and_or_b32).
+// The row ring comes first, so every row slot is SLOT-aligned and key_load ORs
+// a token's 4-aligned offset into its slot address (v_and_or_b32).
 constexpr uint32_t L_ROWS = 0;
-constexpr uint32_t L_ROWS_BYTES = MOX_MAP_SELF ? MAP_WAVES * MAP_BUFS * MAP_PAIRW * SLOT : RING * SLOT;
+constexpr uint32_t L_ROWS_BYTES = RING * SLOT;
 constexpr uint32_t L_DCNT = L_ROWS + L_ROWS_BYTES;
 constexpr uint32_t L_BCNT = L_DCNT + DICT_SLOTS * 4;
 constexpr uint32_t L_MISC = L_BCNT + NB * 4;
 constexpr uint32_t L_SELTAB = L_MISC + 16;
 constexpr uint32_t L_DKEY = L_SELTAB + KSEL_N * 16;
-constexpr uint32_t L_RFLAGS = L_DKEY + DICT_SLOTS * 16;  // ring only: ready[RING], free[RING]
-constexpr uint32_t L_LISTS = L_RFLAGS + (MOX_MAP_SELF ? 0u : RING * 8u);
-static_assert(L_LISTS + (size_t)MAP_ROW_WAVES * 2 * LIST_N * MAP_PAIRW == MAP_LDS_BYTES, "k_map LDS layout");
-static_assert(L_ROWS % (SLOT * MAP_PAIRW) == 0 && (SLOT & (SLOT - 1)) == 0, "row slots aligned to their size");
+constexpr uint32_t L_RFLAGS = L_DKEY + DICT_SLOTS * 16;  // ring: ready[RING], free[RING]
+constexpr uint32_t L_LISTS = L_RFLAGS + RING * 8u;
+static_assert(L_LISTS + (size_t)MAP_ROW_WAVES * 2 * LIST_N == MAP_LDS_BYTES, "k_map LDS layout");
+static_assert(L_ROWS % SLOT == 0 && (SLOT & (SLOT - 1)) == 0, "row slots aligned to their size");
 static_assert(L_DCNT % 16 == 0 && L_SELTAB % 16 == 0 && L_DKEY % 16 == 0 && L_LISTS % 16 == 0, "LDS table alignment");
 typedef __attribute__((address_space(3))) uint8_t LdsByte;
 // LDS address of a generic pointer into LDS, and a pointer from an LDS address
@@ -429,7 +429,7 @@ __device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w
   return -1;
 }
 
-__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1, uint32_t* nst = nullptr);
+__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1);
 
 // A short word (lowered length <= 16, no NUL byte) as an exact 16-byte key.
 // Hot words: LDS dictionary count.  Others: appended to this workgroup's
@@ -494,14 +494,11 @@ __device__ __forceinline__ void note_sample(const MapCtx& m, uint32_t b, uint32_
     rare(m).samp[((uint64_t)b * m.rg + blockIdx.x * m.qf + q) * SPLIT_PER_REGION + pos] = h;
 }
 // No dictionary: slot B = the partition bits and the qb bits below them
-// (partition b = B >> qb, region q = B & (qf - 1)).  *nst (when given) counts
-// the pair stores the wave issued (2 per round in which any lane stored a pair;
-// a lower bound: spills and samples are not counted), for k_map's row-DMA wait.
-__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t h, uint4 key, uint32_t* nst) {
+// (partition b = B >> qb, region q = B & (qf - 1)).
+__device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t h, uint4 key) {
   const uint32_t b = B >> m.qb, qr = B & (m.qf - 1);
   bool done = false;
   do {
-    bool st2 = false;
     if (!done) {
       uint4 q;
       const int r = pair_try(m.s.pst, m.s.pend, B, key, &q);
@@ -524,7 +521,6 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
             uint4* o = cold_at(m, b, qr, pos);
             o[0] = q;
             o[1] = key;
-            st2 = true;
           } else {
             cold_spill(m, q);
             cold_spill(m, key);
@@ -533,16 +529,15 @@ __device__ __forceinline__ void cold_pair(const MapCtx& m, uint32_t B, uint32_t 
       }
       done = r != 0;
     }
-    if (nst && __any(st2)) *nst += 2u;
     __builtin_amdgcn_wave_barrier();
   } while (__any(!done));
 }
-__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1, uint32_t* nst) {
+__device__ __forceinline__ void cold_word(const MapCtx& m, uint32_t h, uint64_t w0, uint64_t w1) {
   const uint32_t b = bucket_of(h);
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) { asm volatile("" ::"v"(b)); return; }
   const uint4 key = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
   if (m.dict_n == 0) {
-    if (!MOX_ABL(m.w.dbg, DBG_NOPAIR)) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key, nst); return; }
+    if (!MOX_ABL(m.w.dbg, DBG_NOPAIR)) { cold_pair(m, h >> (32 - NB_LOG2 - m.qb), h, key); return; }
     const uint32_t B = h >> (32 - NB_LOG2 - m.qb), qr = B & (m.qf - 1);
     const uint32_t pos = atomicAdd(&m.s.bcnt[B], 1u);
     if (pos < SPLIT_PER_REGION) note_sample(m, b, qr, pos, max(h, 1u));  // (h: hash32_map)
@@ -768,50 +763,25 @@ struct KeyLd {
   uint32_t E[5];
   uint4 S;  // v_perm selectors: alignment and length mask in one (seltab)
 };
-#ifndef MOX_KEY_UNALIGNED
-#define MOX_KEY_UNALIGNED 0  // 1: one-row keys read at their exact (unaligned) start and masked by AND (no v_perm)
-#endif
-static_assert(!(MOX_KEY_UNALIGNED && MOX_MAP_PAIR), "the row-pair path keeps the v_perm keys");
-// PB: bits of the slot offset in a list entry (10: one row; 11: a row pair,
-// whose two slots are adjacent in LDS), the length field above them
-template <int PB = 10>
+// (Keys read at their exact, unaligned start and masked by AND instead of
+// v_perm measured k_map +13 %: unaligned LDS reads cost far more than the four
+// v_perm they save)
+// List entry: slot offset in bits 0..9, length from bit 10.
 __device__ __forceinline__ void key_load(const MapLds& s, const uint8_t* rowbuf, uint32_t e, KeyLd& r) {
-#if MOX_KEY_UNALIGNED
-  if constexpr (PB == 10) {
-    // the 16 bytes at the token's start (LDS reads take any byte alignment on
-    // gfx950), and the byte mask of its length (seltab[len], 16 B each)
-    typedef uint32_t U32U __attribute__((aligned(1)));
-    const U32U* q = lds_ptr<const U32U>(__builtin_amdgcn_bitop3_b32(e, s.kmask, lds_addr(rowbuf), 0xEA));
-#pragma unroll
-    for (int i = 0; i < 4; i++) r.E[i] = q[i];
-    r.S = *lds_ptr<const uint4>(L_SELTAB + ((e >> 6) & 0x3F0u));
-    return;
-  }
-#endif
-  // rowbuf is a row slot (row pair), aligned to its size (L_ROWS): the 4-aligned
-  // token offset ORs in, (e & mask) | slot in one v_bitop3_b32 (truth table 0xEA)
-  static_assert(((1u << PB) - 1u & ~3u) == (PB == 10 ? 0x3FCu : 0x7FCu), "key offset mask");
-  const uint32_t* q = lds_ptr<const uint32_t>(
-      PB == 10 ? __builtin_amdgcn_bitop3_b32(e, s.kmask, lds_addr(rowbuf), 0xEA) : (lds_addr(rowbuf) | (e & 0x7FCu)));
+  // rowbuf is a row slot, aligned to its size (L_ROWS): the 4-aligned token
+  // offset ORs in, (e & 0x3FC) | slot in one v_bitop3_b32 (truth table 0xEA)
+  const uint32_t* q = lds_ptr<const uint32_t>(__builtin_amdgcn_bitop3_b32(e, s.kmask, lds_addr(rowbuf), 0xEA));
 #pragma unroll
   for (int i = 0; i < 5; i++) r.E[i] = q[i];
   // (entry 4 len + (pos & 3), as a byte offset straight from the list entry:
-  // bits 6.. from len (e >> (PB - 6); nothing above it in a 16-bit entry) and
-  // bits 0..5 from e << 4 (pos & 3 in bits 4..5, zero below): bit i = bit i of
-  // 63 ? (e << 4) : (e >> (PB - 6)), one v_bitop3_b32 with an inline constant
-  // (truth table 0xD8).  An odd entry's offset may pass the table's end: it
-  // reads other LDS, unused.)
-  r.S = *lds_ptr<const uint4>(L_SELTAB + __builtin_amdgcn_bitop3_b32(e >> (PB - 6), e << 4, 63u, 0xD8));
+  // bits 6.. from len (e >> 4; nothing above it in a 16-bit entry) and bits
+  // 0..5 from e << 4 (pos & 3 in bits 4..5, zero below): bit i = bit i of
+  // 63 ? (e << 4) : (e >> 4), one v_bitop3_b32 with an inline constant (truth
+  // table 0xD8).  An odd entry's offset may pass the table's end: it reads
+  // other LDS, unused.)
+  r.S = *lds_ptr<const uint4>(L_SELTAB + __builtin_amdgcn_bitop3_b32(e >> 4, e << 4, 63u, 0xD8));
 }
-__device__ __forceinline__ void key_make(uint32_t e, const KeyLd& r, uint32_t (&K)[4]) {
-  (void)e;
-#if MOX_KEY_UNALIGNED
-  K[0] = r.E[0] & r.S.x;
-  K[1] = r.E[1] & r.S.y;
-  K[2] = r.E[2] & r.S.z;
-  K[3] = r.E[3] & r.S.w;
-  return;
-#endif
+__device__ __forceinline__ void key_make(const KeyLd& r, uint32_t (&K)[4]) {
   // byte 4 d + j of the key = byte S.d[j] of (E[d + 1]:E[d]) (0x0C: zero): one
   // v_perm_b32 per dword aligns and masks at once
   K[0] = __builtin_amdgcn_perm(r.E[1], r.E[0], r.S.x);
@@ -854,21 +824,8 @@ __device__ __forceinline__ void after_fence(uint32_t (&v)[TU]) {
 // builtin keeps the combiner from splitting it into four compares and a
 // boolean tree, and (unlike inline asm, which it replaces) lets the scheduler
 // interleave the chains without a wait state after every step.
-#ifndef MOX_BK_ONCE
-#define MOX_BK_ONCE 1
-#endif
-#ifndef MOX_PROBE_LAZY
-#define MOX_PROBE_LAZY 0  // 1: second dictionary slot read only where the first missed (k_map pass_a)
-#endif
-#ifndef MOX_EQ64
-#define MOX_EQ64 0  // 1: two v_cmp_eq_u64 per key compare (lane masks ANDed on the SALU)
-#endif
+// (Two v_cmp_eq_u64 per compare tied, round 5.)
 __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
-#if MOX_EQ64
-  const uint64_t a0 = ((uint64_t)k.y << 32) | k.x, a1 = ((uint64_t)k.w << 32) | k.z;
-  const uint64_t b0 = ((uint64_t)K[1] << 32) | K[0], b1 = ((uint64_t)K[3] << 32) | K[2];
-  return (a0 == b0) & (a1 == b1);
-#endif
   uint32_t d = k.x ^ K[0];
   d = __builtin_amdgcn_bitop3_b32(k.y, K[1], d, 0xBE);
   d = __builtin_amdgcn_bitop3_b32(k.z, K[2], d, 0xBE);
@@ -882,86 +839,50 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
 // of a phase are issued before the first is used (SCHED_FENCE).  The
 // dictionary arrays are zero when there is no dictionary (a real key is never
 // zero, so nothing hits), but that case takes pass_c.
-// nst counts the cold-store instructions the wave issues (one per batch in
-// which any lane stores a record; spills and samples are extra), for the
-// counted wait on the next row's DMA (k_map, MOX_MAP_SELF).  nvalid counts the
-// entries taken (SALU: the valid masks' bit counts); fewer than the row's
-// total means odd entries for the generic walk (do_row).
-// A one-row list (PB 10) is read past its last entry into the LIST_ODD tail
-// (LIST_N; the batch sizes keep j < total + 64), so the reads need neither a
-// bounds clamp nor an inactive-lane select.
-template <int TU, int PB = 10>
+// nvalid counts the entries taken (SALU: the valid masks' bit counts); fewer
+// than the row's total means odd entries for the generic walk (do_row).
+// The list is read past its last entry into the LIST_ODD tail (LIST_N; the
+// batch sizes keep j < total + 64), so the reads need neither a bounds clamp
+// nor an inactive-lane select.
+template <int TU>
 __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t total, uint32_t& nst, uint32_t& nvalid) {
+                                       uint32_t& nvalid) {
 #ifdef MOX_ISA_MARKS  // (ISA reading aid: comment markers around the token pass)
   asm volatile("; PASS_A begin TU=%0" ::"i"(TU));
 #endif
   const int lane = threadIdx.x & 63;
   uint32_t e[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) {
-    const uint32_t j = j0 + u * 64 + lane;
-    if constexpr (PB == 10) {
-      e[u] = list[j];
-    } else {
-      constexpr uint32_t LMAX = 2 * TOKMAX;  // row-pair list entries (the last is the sink)
-      e[u] = list[j < LMAX ? j : LMAX - 1];
-    }
-  }
+  for (int u = 0; u < TU; u++) e[u] = list[j0 + u * 64 + lane];
   SCHED_FENCE();  // every batch's list read in flight before the first is used
-  if constexpr (PB != 10) {
-#pragma unroll
-    for (int u = 0; u < TU; u++) e[u] = j0 + u * 64 + lane < total ? e[u] : (17u << PB);  // inactive = odd (slot offset 0)
-  }
   KeyLd ld[TU];
 #pragma unroll
-  for (int u = 0; u < TU; u++) key_load<PB>(m.s, rowbuf, e[u], ld[u]);
+  for (int u = 0; u < TU; u++) key_load(m.s, rowbuf, e[u], ld[u]);
   SCHED_FENCE();
   AFTER_FENCE(e);
   uint32_t K[TU][4], h[TU], s1[TU], s2[TU];  // s1, s2: the two slots' key byte offsets (16 s)
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    key_make(e[u], ld[u], K[u]);
+    key_make(ld[u], K[u]);
     h[u] = hash32_map(K[u][0], K[u][1], K[u][2], K[u][3]);
     s1[u] = slot_off16((h[u] & 0xFFFFu) * (uint32_t)DICT_SLOTS);  // 16 dict_s1(h)
     s2[u] = slot_off16((h[u] >> 16) * (uint32_t)DICT_SLOTS);      // 16 dict_s2(h)
   }
+  // (Reading the second slot only where the first missed: fewer LDS bytes,
+  // one more round trip per pass, slower; round 5.)
   uint4 d1[TU], d2[TU];
-#if MOX_PROBE_LAZY
-  // (timing experiment) the second slot read only by the lanes whose key is
-  // not in the first: fewer LDS bytes, one more round trip per pass
-#pragma unroll
-  for (int u = 0; u < TU; u++) d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]);
-  SCHED_FENCE();
-  bool h1[TU];
-#pragma unroll
-  for (int u = 0; u < TU; u++) {
-    h1[u] = key_eq4(d1[u], K[u]);
-    if (e[u] < (17u << PB) && !h1[u]) d2[u] = *lds_ptr<const uint4>(L_DKEY + s2[u]);
-  }
-  SCHED_FENCE();
-#elif defined(MOX_TIMING_ONE_PROBE)  // (timing only, counts wrong: no second slot read)
-#pragma unroll
-  for (int u = 0; u < TU; u++) { d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]); d2[u] = d1[u]; }
-  SCHED_FENCE();
-#else
 #pragma unroll
   for (int u = 0; u < TU; u++) { d1[u] = *lds_ptr<const uint4>(L_DKEY + s1[u]); d2[u] = *lds_ptr<const uint4>(L_DKEY + s2[u]); }
   SCHED_FENCE();
-#endif
   // hits count in LDS; every miss reserves its region slot (the LDS returning
   // atomics of all batches issued together), then the misses are stored
   bool miss[TU];
   uint32_t pos[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    const bool valid = e[u] < (17u << PB);  // LIST_ODD of the format
+    const bool valid = e[u] < LIST_ODD;
     nvalid += (uint32_t)__popcll(__ballot(valid));
-#if MOX_PROBE_LAZY
-    const bool hit1 = h1[u], hit2 = valid && !hit1 && key_eq4(d2[u], K[u]);
-#else
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
-#endif
     miss[u] = valid & !(hit1 | hit2);
     if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
 #if defined(MOX_PATHS) && MOX_PATHS
@@ -973,29 +894,27 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
   }
   if MOX_ABL(m.w.dbg, DBG_NO_COLDSTORE) return;
   // (a dictionary pass: the region counters are at L_BCNT, an immediate offset;
-  // pos and bk are read under miss only.  MOX_BK_ONCE keeps the partition
-  // opaque so that it is computed once (the compiler forms the counter address
-  // from h directly and shifts h again for the store): k_map +1 % with it.)
+  // pos and bk are read under miss only.  The partition is kept opaque so
+  // that it is computed once (the compiler forms the counter address from h
+  // directly and shifts h again for the store): k_map +1 % without it.)
   uint32_t bk[TU];
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     if (miss[u]) {
       bk[u] = bucket_of(h[u]);
-      if (MOX_BK_ONCE) asm("" : "+v"(bk[u]));
+      asm("" : "+v"(bk[u]));
       pos[u] = atomicAdd(lds_ptr<uint32_t>(L_BCNT + 4 * bk[u]), 1u);
     }
   }
   SCHED_FENCE();
 #pragma unroll
   for (int u = 0; u < TU; u++) {
-    nst += __any(miss[u] && pos[u] < m.rc) ? 1u : 0u;
     if (!miss[u]) continue;
     const uint32_t b = bk[u];
     const uint4 key = make_uint4(K[u][0], K[u][1], K[u][2], K[u][3]);
     if (pos[u] < SPLIT_PER_REGION) note_sample(m, b, 0, pos[u], max(h[u], 1u));  // (hash32_map)
     if (pos[u] < m.rc) {
-      if (MOX_ABL(m.w.dbg, DBG_COLD_NOSTORE)) asm volatile("" ::"v"(key.x), "v"(key.w));
-      else *cold_at(m, MOX_ABL(m.w.dbg, DBG_COLD_SEQ) ? 0u : b, 0, pos[u]) = key;
+      *cold_at(m, b, 0, pos[u]) = key;
     } else {
       cold_spill(m, key);
     }
@@ -1010,7 +929,7 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
 // (list read into its LIST_ODD tail as in pass_a; nvalid likewise)
 template <int TU>
 __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, const uint16_t* list, uint32_t j0,
-                                       uint32_t& nst, uint32_t& nvalid) {
+                                       uint32_t& nvalid) {
   const int lane = threadIdx.x & 63;
   uint32_t e[TU];
 #pragma unroll
@@ -1025,64 +944,12 @@ __device__ __forceinline__ void pass_c(const MapCtx& m, const uint8_t* rowbuf, c
   AFTER_FENCE(e);
   uint32_t K[TU][4];
 #pragma unroll
-  for (int u = 0; u < TU; u++) key_make(e[u], ld[u], K[u]);
+  for (int u = 0; u < TU; u++) key_make(ld[u], K[u]);
 #pragma unroll
   for (int u = 0; u < TU; u++) {
     if (e[u] >= LIST_ODD) continue;
     const uint64_t w0 = ((uint64_t)K[u][1] << 32) | K[u][0], w1 = ((uint64_t)K[u][3] << 32) | K[u][2];
-    cold_word(m, hash32_map(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1, &nst);
-  }
-}
-
-// ---- k_map row supply by the row's own wave (MOX_MAP_SELF)
-// LDS-DMA of one row slot: lane i's 16 bytes at gsrc land at LDS byte address
-// lds + 16 i (global_load_lds_dwordx4, nt: read once).  Written as asm so that
-// the compiler neither waits for it nor counts it: its LDS target is read only
-// after the counted wait below.  M0 is restored in the same statement.
-__device__ __forceinline__ void row_dma(const uint8_t* gsrc, uint32_t lds) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds)
-               : "memory");
-}
-// Source byte of lane block p of a row slot, clamped like raw16 to a 16-byte
-// block that overlaps [lo, hi) (bytes outside are fixed up by fix16 after the
-// read); an empty buffer reads its first block (c.base + first is the buffer
-// start rounded down to 16 B, a valid address: make_corpus)
-__device__ __forceinline__ uint64_t dma_src(const Corpus& c, uint64_t p) {
-  const uint64_t first = c.lo & ~15ull, last = (c.hi - 1) & ~15ull;
-  p = p > last ? last : p;
-  p = p < first ? first : p;
-  return c.hi <= c.lo ? first : p;
-}
-#ifndef MOX_MAP_STATIC
-#define MOX_MAP_STATIC 0  // 1: k_map waves take rows wv, wv + 16, ... instead of LDS tickets (MOX_MAP_SELF)
-#endif
-#ifndef MOX_DMA_MARGIN
-#define MOX_DMA_MARGIN 1  // the counted row-DMA wait leaves this many fewer operations outstanding than counted
-#endif
-template <int N>
-__device__ __forceinline__ void vm_wait_n() { asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory"); }
-// Wait until at most n (wave-uniform) of the wave's vector-memory operations
-// are outstanding, rounded down to a step of this ladder (waiting for a few
-// more than needed is safe: they are older)
-__device__ __forceinline__ void vm_wait_le(uint32_t n) {
-  if (n >= 8) {
-    if (n >= 32) vm_wait_n<32>();
-    else if (n >= 16) vm_wait_n<16>();
-    else if (n >= 12) vm_wait_n<12>();
-    else vm_wait_n<8>();
-  } else if (n >= 4) {
-    if (n >= 6) { if (n == 7) vm_wait_n<7>(); else vm_wait_n<6>(); }
-    else if (n == 5) vm_wait_n<5>();
-    else vm_wait_n<4>();
-  } else if (n >= 2) {
-    if (n == 3) vm_wait_n<3>(); else vm_wait_n<2>();
-  } else if (n == 1) {
-    vm_wait_n<1>();
-  } else {
-    vm_wait_n<0>();
+    cold_word(m, hash32_map(K[u][0], K[u][1], K[u][2], K[u][3]), w0, w1);
   }
 }
 
@@ -1119,11 +986,8 @@ struct Cyc {
 //     prefix sum of per-lane start counts from 5 bit-sliced ballots);
 //  2. token phase (lane = token): pass_a over all tokens (both dictionary slots
 //     read at once: an LDS count on a hit, the cold store on a miss).
-// nst: vector-memory stores the row issued (a lower bound, pass_a); vclear:
-// the row waited for every vector-memory operation of the wave (vm_settle on a
-// rare path), so the next row's DMA has landed.
 __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a, unsigned long long& ntok, uint8_t* rowbuf,
-                                       uint16_t* list, struct Cyc* cyc, bool edge, uint32_t& nst, bool& vclear) {
+                                       uint16_t* list, struct Cyc* cyc, bool edge) {
 #ifdef MOX_ISA_MARKS
   asm volatile("; DO_ROW begin");
 #endif
@@ -1191,7 +1055,6 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   } else {
     start = ctx ? 0u : slow_starts(m, p0);
     vm_settle();
-    vclear = true;
   }
 #ifdef MOX_ISA_MARKS
   asm volatile("; MARK BP_START");
@@ -1258,15 +1121,15 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
   uint32_t nvalid = 0;
   if (m.dict_n == 0) {  // no dictionary: no probes (uniform branch)
     for (uint32_t j0 = 0; j0 < total;) {
-      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, nst, nvalid); j0 += 128; }
-      else { pass_c<1>(m, rowbuf, list, j0, nst, nvalid); j0 += 64; }
+      if (total - j0 > 64) { pass_c<2>(m, rowbuf, list, j0, nvalid); j0 += 128; }
+      else { pass_c<1>(m, rowbuf, list, j0, nvalid); j0 += 64; }
     }
   } else {
     for (uint32_t j0 = 0; j0 < total;) {
       const uint32_t rem = total - j0;
-      if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, total, nst, nvalid); j0 += 192; }
-      else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, total, nst, nvalid); j0 += 128; }
-      else { pass_a<1>(m, rowbuf, list, j0, total, nst, nvalid); j0 += 64; }
+      if (rem > 128) { pass_a<3>(m, rowbuf, list, j0, nvalid); j0 += 192; }
+      else if (rem > 64) { pass_a<2>(m, rowbuf, list, j0, nvalid); j0 += 128; }
+      else { pass_a<1>(m, rowbuf, list, j0, nvalid); j0 += 64; }
     }
   }
   // the row has odd entries iff fewer than total were valid (tail entries are
@@ -1279,108 +1142,11 @@ __device__ __forceinline__ void do_row(const MapCtx& m, uint64_t sbase, uint4 a,
       if (e >= LIST_ODD) generic_token(m, sbase + (e & 1023u));
     }
     vm_settle();
-    vclear = true;
   }
   if (cyc) cyc->pa += __builtin_amdgcn_s_memtime() - t1;
   wave_lds_fence();
 }
 
-#if MOX_MAP_PAIR
-// ASCII byte classification of one 16-byte lane block (do_row's common path):
-// whitespace flags of the 16 bytes in bits 0..15, and the control-byte flags
-// (bytes < 33 that are not whitespace, NUL included) as 0x80 per byte
-__device__ __forceinline__ uint32_t classify16(uint4 a, uint32_t& ctl) {
-  const uint32_t ad[4] = {a.x, a.y, a.z, a.w};
-  uint32_t wsd[4];
-  ctl = 0;
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    const uint32_t x = ad[d];
-    const uint32_t lt33 = ~(x + 0x5F5F5F5Fu), ge32 = x + 0x60606060u, ge9 = x + 0x77777777u, ge14 = x + 0x72727272u;
-    wsd[d] = lt33 & (ge32 | (ge9 & ~ge14)) & 0x80808080u;
-    ctl |= lt33 & ~wsd[d];
-  }
-  return gather16(wsd);
-}
-// Two consecutive rows at once (MOX_MAP_PAIR): slots buf (row u) and buf + SLOT
-// (row u + 1), one list of both rows' tokens in 11-bit-offset entries (row
-// u + 1's at slot offset 1024 + ...).  The two rows' byte phases are
-// independent chains the scheduler interleaves; their start counts share one
-// packed wave scan (row u's in the low 16 bits) and one max scan, their list
-// entries one loop; the token pass runs over the joint list (fuller batches).
-// Rows with non-ASCII or control bytes take do_row one at a time.  The caller
-// passes interior rows only (no edge checks) and a pass with a dictionary.
-__device__ __forceinline__ void do_pair(const MapCtx& m, uint64_t sbase, uint4 a0, uint4 a1, unsigned long long& ntok,
-                                        uint8_t* buf, uint16_t* list, struct Cyc* cyc, uint32_t& nst, bool& vclear) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t keep = (uint32_t)(lane - 1) < 62u ? 0xFFFFFFFFu : 0u;
-  bool fall = __any((nonascii16(a0) | nonascii16(a1)) != 0);
-  uint32_t ws0 = 0, ws1 = 0, st0 = 0, st1 = 0;
-  if (!fall) {
-    uint32_t ctl0, ctl1;
-    const uint32_t w0 = classify16(a0, ctl0), w1 = classify16(a1, ctl1);
-    const uint32_t n0 = from_next_lane(w0), n1 = from_next_lane(w1);
-    const uint32_t q0 = from_prev_lane(w0), q1 = from_prev_lane(w1);
-    ws0 = w0 | (n0 << 16);
-    ws1 = w1 | (n1 << 16);
-    st0 = (~ws0) & ((ws0 << 1) | ((q0 >> 15) & 1u)) & 0xFFFFu & keep;
-    st1 = (~ws1) & ((ws1 << 1) | ((q1 >> 15) & 1u)) & 0xFFFFu & keep;
-    fall = __any(((ctl0 | ctl1) & 0x80808080u) != 0);  // control bytes (NUL checks): one row at a time
-  }
-  if (fall) {
-    do_row(m, sbase, a0, ntok, buf, list, cyc, false, nst, vclear);
-    do_row(m, sbase + PAY, a1, ntok, buf + SLOT, list, cyc, false, nst, vclear);
-    return;
-  }
-  const uint32_t c0 = __popc(st0), c1 = __popc(st1);
-  ntok += c0 + c1;
-  const uint32_t incl = wave_incl_scan(c0 | (c1 << 16));  // (a row has at most 496 tokens: no carry)
-  const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  const uint32_t t0 = tot & 0xFFFFu, total = t0 + (tot >> 16);
-  if (total == 0) return;
-  reinterpret_cast<uint4*>(buf)[lane] = lower16(a0);
-  reinterpret_cast<uint4*>(buf + SLOT)[lane] = lower16(a1);
-  uint32_t sm0 = ws0 >> 1, sm1 = ws1 >> 1;
-  sm0 |= sm0 >> 1; sm1 |= sm1 >> 1;
-  sm0 |= sm0 >> 2; sm1 |= sm1 >> 2;
-  sm0 |= sm0 >> 4; sm1 |= sm1 >> 4;
-  sm0 |= sm0 >> 8; sm1 |= sm1 >> 8;
-  const bool any_odd = ((st0 & ~sm0) | (st1 & ~sm1)) != 0;
-  const uint32_t trips = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max(max(c0, c1)), 63);
-  uint16_t* const sink = list + (2 * TOKMAX - 1);
-  uint16_t* const mine0 = list + ((incl & 0xFFFFu) - c0);
-  uint16_t* const mine1 = list + (t0 + (incl >> 16) - c1);
-  const uint32_t lb0 = (uint32_t)(lane * 16), lb1 = lb0 + SLOT;
-  for (uint32_t it = 0; it < trips; it++) {
-    const uint32_t p0 = ffbl(st0), p1 = ffbl(st1);
-    st0 &= st0 - 1;
-    st1 &= st1 - 1;
-    const uint32_t l0 = ffbl(ws0 >> (p0 & 31u)), l1 = ffbl(ws1 >> (p1 & 31u));
-    *(it < c0 ? mine0 + it : sink) = (uint16_t)(lb0 + p0 + (l0 << 11));
-    *(it < c1 ? mine1 + it : sink) = (uint16_t)(lb1 + p1 + (l1 << 11));
-  }
-  wave_lds_fence();
-  if (__any(any_odd)) {  // rare: tokens over 16 bytes
-    for (uint32_t j = lane; j < total; j += 64) {
-      const uint32_t e = list[j];
-      if (e >= (17u << 11)) {
-        const uint32_t pos = e & 2047u;
-        generic_token(m, pos < SLOT ? sbase + pos : sbase + PAY + (pos - SLOT));
-      }
-    }
-    vm_settle();
-    vclear = true;
-  }
-  uint32_t nv_unused = 0;  // (the pair path finds its odd entries from the smeared masks)
-  for (uint32_t j0 = 0; j0 < total;) {
-    const uint32_t rem = total - j0;
-    if (rem > 128) { pass_a<3, 11>(m, buf, list, j0, total, nst, nv_unused); j0 += 192; }
-    else if (rem > 64) { pass_a<2, 11>(m, buf, list, j0, total, nst, nv_unused); j0 += 128; }
-    else { pass_a<1, 11>(m, buf, list, j0, total, nst, nv_unused); j0 += 64; }
-  }
-  wave_lds_fence();
-}
-#endif
 
 // Map kernel.  One persistent 1024-thread workgroup per CU owns a contiguous
 // range of rows (992 payload bytes each).
@@ -1416,24 +1182,17 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.s.misc = lds_ptr<uint32_t>(L_MISC);  // [0] spills [1] ticket
   m.s.seltab = lds_ptr<uint4>(L_SELTAB);
   m.s.dkey = lds_ptr<uint4>(L_DKEY);
-  if (MOX_KEY_UNALIGNED) asm("v_mov_b32 %0, 0x3ff" : "=v"(m.s.kmask));
-  else asm("v_mov_b32 %0, 0x3fc" : "=v"(m.s.kmask));
+  asm("v_mov_b32 %0, 0x3fc" : "=v"(m.s.kmask));
   m.keep = (uint32_t)((threadIdx.x & 63) - 1) < 62u ? 0xFFFFFFFFu : 0u;
   asm volatile("" : "+v"(m.keep));
-#if MOX_MAP_SELF
-  uint8_t* rowbufs = lds_ptr<uint8_t>(L_ROWS);  // MAP_AHEAD + 1 row (pair) buffers per wave
-#else
   uint32_t* sready = lds_ptr<uint32_t>(L_RFLAGS);         // row ticket + 1 once loaded
   uint32_t* sfree = lds_ptr<uint32_t>(L_RFLAGS + RING * 4);  // row ticket + 1 once consumed
   uint8_t* ring = lds_ptr<uint8_t>(L_ROWS);
-#endif
   uint16_t* lists = lds_ptr<uint16_t>(L_LISTS);
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
-#ifndef MOX_TIMING_ONLY_SMALL_DICT  // (timing experiments with a smaller dictionary: dictionary passes only)
   static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
   static_assert(NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
-#endif
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
@@ -1455,19 +1214,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     m.s.bcnt[i] = resume ? cold_n_at(w, m.rg, blockIdx.x * m.qf + q, b) : 0u;
   }
   if (tid < 4) m.s.misc[tid] = (resume && tid == 0) ? w.spill_n[blockIdx.x] : 0u;
-#if !MOX_MAP_SELF
   if (tid < RING) { sready[tid] = 0; sfree[tid] = 0; }
-#endif
-  if (MOX_KEY_UNALIGNED && tid < 17) {  // byte masks of a len-byte key
-    uint32_t mk[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++) {
-      mk[d] = 0;
-#pragma unroll
-      for (int j = 0; j < 4; j++) mk[d] |= (4 * d + j < tid ? 0xFFu : 0u) << (8 * j);
-    }
-    m.s.seltab[tid] = make_uint4(mk[0], mk[1], mk[2], mk[3]);
-  } else if (!MOX_KEY_UNALIGNED && tid < KSEL_N) {  // key byte 4 d + j = window byte sh + 4 d + j, or 0 past len (v_perm selector 0x0C)
+  if (tid < KSEL_N) {  // key byte 4 d + j = window byte sh + 4 d + j, or 0 past len (v_perm selector 0x0C)
     const uint32_t len = (uint32_t)tid >> 2, sh = (uint32_t)tid & 3u;
     uint32_t sel[4];
 #pragma unroll
@@ -1487,181 +1235,6 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   const uint64_t rb = blockIdx.x * per + (blockIdx.x < rem ? blockIdx.x : rem);
   const uint32_t n = (uint32_t)(per + (blockIdx.x < rem ? 1 : 0));
 
-#if MOX_MAP_SELF
-  {
-    // ---------------- every wave: rows by ticket, each loaded by its own wave
-    // one row ahead.  At the start of a row the wave issues the LDS-DMA of its
-    // next row into its other buffer and takes the ticket of the row after
-    // that; the current row's DMA (issued one row earlier) is then waited for
-    // by a counted vmcnt: younger than it are only the previous row's cold
-    // stores (counted by the token passes, a lower bound) and the next row's
-    // DMA, so the wait never drains the stores the wave just issued.  A row
-    // thus has a whole row's processing time to arrive, and there is no loader
-    // wave, ring, or ready / free hand-off.
-#ifdef MOX_MAP_ACTIVE  // (timing experiment: only this many waves take rows)
-    if (wv < MOX_MAP_ACTIVE) {
-#else
-    {
-#endif
-    uint16_t* list = lists + wv * (MAP_PAIRW * LIST_N);
-    uint32_t e_lo = rb < 2 ? (uint32_t)(2 - rb) : 0u;  // edge rows: see the consumers of the ring build below
-    const uint32_t e_hi = __builtin_amdgcn_readfirstlane(nrows >= rb + 3 ? (uint32_t)min<uint64_t>(nrows - 3 - rb, n) : 0u);
-    if (c.own_hi > base0 && nrows * PAY < c.own_hi - base0) e_lo = n;
-    uint8_t* mybuf = rowbufs + wv * (MAP_BUFS * MAP_PAIRW * SLOT);
-    const uint32_t lds0 = __builtin_amdgcn_readfirstlane(
-        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)mybuf);
-#ifdef MOX_STAMP
-    Cyc cyc{0, 0, 0, 0, 0, 0};
-    Cyc* cp = &cyc;
-#else
-    Cyc* cp = nullptr;
-#endif
-    // tickets: lane 0's LDS atomic, read (readfirstlane) one row later, so the
-    // atomic's round trip is not waited for where it is issued
-#if MOX_MAP_STATIC
-    // static rows: wave wv takes rows wv, wv + 16, ... of the workgroup's range
-    uint32_t tk = __builtin_amdgcn_readfirstlane(wv);
-    auto ticket = [&]() -> uint32_t { const uint32_t u = tk; tk += MAP_WAVES; return u; };
-#else
-    auto ticket = [&]() -> uint32_t {
-      uint32_t u = 0;
-      if (lane == 0) u = lds_fetch_add1(L_MISC + 4, 1u);  // m.s.misc[1]
-      return u;
-    };
-#endif
-    // row u's slot, lane block: interior rows from one loop-invariant per-lane
-    // base; edge rows clamped like raw16 (their out-of-range bytes are fixed up
-    // after the read)
-    const uint8_t* lbase = c.base + (base0 + rb * PAY - 16 + 16 * (uint64_t)lane);
-    auto dma = [&](uint32_t u, uint32_t bi) {
-      const uint8_t* src;
-      if (u < e_lo || u >= e_hi) src = c.base + dma_src(c, base0 + (rb + u) * PAY - 16 + 16 * (uint64_t)lane);
-      else src = lbase + (uint64_t)u * PAY;
-      row_dma(src, lds0 + bi * SLOT);
-    };
-#if MOX_MAP_PAIR
-    // row pairs: ticket q = rows 2q, 2q + 1 (adjacent slots of a pair buffer),
-    // the next pair loaded one pair ahead (two DMAs)
-    const uint32_t np = (n + 1) / 2;
-    auto dma_pair = [&](uint32_t q, uint32_t bi) -> uint32_t {
-      dma(2 * q, bi * 2);
-      if (2 * q + 1 < n) { dma(2 * q + 1, bi * 2 + 1); return 2u; }
-      return 1u;
-    };
-    uint32_t cur = __builtin_amdgcn_readfirstlane(ticket());
-    if (cur < np) (void)dma_pair(cur, 0);
-    uint32_t nxt_v = ticket();
-    uint32_t nst = 0;
-    bool vclear = false;
-    uint32_t bi = 0;
-    for (; cur < np;) {
-      const uint32_t nxt = __builtin_amdgcn_readfirstlane(nxt_v);
-      const uint32_t ahead = nxt < np ? dma_pair(nxt, bi ^ 1u) : 0u;
-      const uint32_t nn_v = ticket();
-      const uint32_t young = nst + ahead;
-      if (!vclear) vm_wait_le(__builtin_amdgcn_readfirstlane(young > MOX_DMA_MARGIN ? young - MOX_DMA_MARGIN : 0u));
-      nst = 0;
-      vclear = false;
-      uint8_t* sl = mybuf + bi * (2 * SLOT);
-      const uint32_t u0 = 2 * cur;
-      const uint64_t sbase = base0 + (rb + u0) * PAY - 16;
-      uint4 a0 = reinterpret_cast<const uint4*>(sl)[lane];
-      const bool two = u0 + 1 < n;
-      uint4 a1 = two ? reinterpret_cast<const uint4*>(sl + SLOT)[lane] : make_uint4(0, 0, 0, 0);
-      const bool edge0 = u0 < e_lo || u0 >= e_hi, edge1 = u0 + 1 < e_lo || u0 + 1 >= e_hi;
-      if (two && !edge0 && !edge1 && m.dict_n) {
-        do_pair(m, sbase, a0, a1, ntok, sl, list, nullptr, nst, vclear);
-      } else {
-        if (edge0 && (sbase < c.lo || sbase + SLOT > c.hi)) a0 = fix16(c, sbase + 16 * (uint64_t)lane, a0);
-        do_row(m, sbase, a0, ntok, sl, list, nullptr, edge0, nst, vclear);
-        if (two) {
-          const uint64_t sb1 = sbase + PAY;
-          if (edge1 && (sb1 < c.lo || sb1 + SLOT > c.hi)) a1 = fix16(c, sb1 + 16 * (uint64_t)lane, a1);
-          do_row(m, sb1, a1, ntok, sl + SLOT, list, nullptr, edge1, nst, vclear);
-        }
-      }
-      cur = nxt;
-      nxt_v = nn_v;
-      bi ^= 1u;
-    }
-#else
-    // rows in flight: the wave's next MAP_AHEAD rows (tickets taken in order),
-    // row k in buffer k mod MAP_BUFS.  Younger than row k's DMA are the stores
-    // of the MAP_AHEAD rows before it and the DMAs issued since (one per row).
-    uint32_t cur = __builtin_amdgcn_readfirstlane(ticket());
-    if (cur < n) dma(cur, 0);
-#if MOX_MAP_AHEAD == 2
-    uint32_t nx1 = __builtin_amdgcn_readfirstlane(ticket());
-    uint32_t dm1 = 0;      // the DMA of nx1 issued (at the row before)
-    if (nx1 < n) { dma(nx1, 1); dm1 = 1; }
-    uint32_t nst1 = 0;     // stores of the row before the previous one
-    bool vclear1 = false;
-#endif
-    uint32_t nxt_v = ticket();
-    uint32_t nst = 0;      // cold-store instructions of the previous row (issued after cur's DMA)
-    bool vclear = false;   // the previous row drained the wave's vector memory
-    uint32_t bi = 0;       // cur's buffer
-    for (uint32_t k = 0; cur < n; k++) {
-      const uint64_t tw = cp ? __builtin_amdgcn_s_memtime() : 0;
-      const uint32_t nxt = __builtin_amdgcn_readfirstlane(nxt_v);
-      const uint32_t bnext = bi + MAP_AHEAD < MAP_BUFS ? bi + MAP_AHEAD : bi + MAP_AHEAD - MAP_BUFS;
-      uint32_t ahead = 0;
-      if (nxt < n) { dma(nxt, bnext); ahead = 1; }
-      const uint32_t nn_v = ticket();
-      // cur's DMA has landed once at most (younger operations counted - margin)
-      // are outstanding; MOX_DMA_MARGIN fewer than counted: a safety margin of
-      // the oldest stores
-#if MOX_MAP_AHEAD == 2
-      const uint32_t young = nst1 + dm1 + nst + ahead;
-      const bool clear = vclear || vclear1;
-#else
-      const uint32_t young = nst + ahead;
-      const bool clear = vclear;
-#endif
-      const uint64_t tv = cp ? __builtin_amdgcn_s_memtime() : 0;
-#ifndef MOX_DMA_NOWAIT  // (timing experiment only: the row is read without waiting for its DMA)
-      if (!clear) vm_wait_le(__builtin_amdgcn_readfirstlane(young > MOX_DMA_MARGIN ? young - MOX_DMA_MARGIN : 0u));
-#else
-      (void)clear;
-      (void)young;
-#endif
-      if (cp) cp->pb += __builtin_amdgcn_s_memtime() - tv;  // (stamp builds: the counted wait alone)
-#if MOX_MAP_AHEAD == 2
-      nst1 = nst;
-      vclear1 = vclear;
-      dm1 = ahead;
-#endif
-      nst = 0;
-      vclear = false;
-      uint8_t* sl = mybuf + bi * SLOT;
-      const uint64_t sbase = base0 + (rb + cur) * PAY - 16;
-      uint4 a = reinterpret_cast<const uint4*>(sl)[lane];
-      const bool edge = cur < e_lo || cur >= e_hi;
-      if (edge && (sbase < c.lo || sbase + SLOT > c.hi)) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
-      if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
-      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge, nst, vclear);
-      else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
-#if MOX_MAP_AHEAD == 2
-      cur = nx1;
-      nx1 = nxt;
-#else
-      cur = nxt;
-#endif
-      nxt_v = nn_v;
-      bi = bi + 1 < MAP_BUFS ? bi + 1 : 0u;
-    }
-#endif
-    vm_wait_n<0>();  // (every DMA issued was waited for above; nothing may land in LDS after the loop)
-    }
-#ifdef MOX_STAMP
-    if (lane == 0 && w.stamps) {
-      unsigned long long* o = w.stamps + 8 * 4096 + ((uint64_t)blockIdx.x * MAP_WAVES + wv) * 8;
-      o[0] = cyc.wait; o[1] = cyc.byte; o[2] = cyc.pa; o[3] = cyc.pb; o[4] = cyc.miss; o[5] = cyc.rows;
-      o[6] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-  }
-#else
   if (wv < MAP_LOADERS) {
     // ---------------- loaders: loader wv owns row groups wv, wv + MAP_LOADERS, ...
     uint4 buf[LD_GROUPS][LD_GROUP];
@@ -1673,7 +1246,6 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       }
     };
     auto retire = [&](const uint4 (&b)[LD_GROUP], uint32_t t0) {
-#if MOX_LD_BATCH
       // the whole group at once: ONE poll of its slots' free words (lane i
       // reads row t0 + i's), the rows' ds_writes back to back, then ONE store
       // publishing every row (after the data: one wave, LDS executes in
@@ -1703,29 +1275,12 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane < LD_GROUP && t0 + lane < n)
         __hip_atomic_store(&sready[(t0 + lane) % RING], t0 + lane + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-      // row by row: each row goes into its ring slot and is published as soon
-      // as that slot is free (a whole-group wait held back the group's first
-      // rows behind its slowest slot: k_map -0.9 % over three A/B pairs)
-#pragma unroll
-      for (int i = 0; i < LD_GROUP; i++) {
-        const uint32_t t = t0 + i;
-        if (t >= n) continue;
-        if (t >= RING)
-          while (__hip_atomic_load(&sfree[t % RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != t - RING + 1)
-            __builtin_amdgcn_s_sleep(MOX_LD_SLEEP);
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        reinterpret_cast<uint4*>(ring + (t % RING) * SLOT)[lane] = b[i];
-        __atomic_signal_fence(__ATOMIC_SEQ_CST);
-        if (lane == 0) __hip_atomic_store(&sready[t % RING], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-#endif
     };
     __builtin_amdgcn_s_setprio(3);  // the loader feeds 15 consumers: never let it lose issue arbitration
     constexpr uint32_t STRIDE = MAP_LOADERS * LD_GROUP;  // rows between this loader's consecutive groups
     const uint32_t first = wv * LD_GROUP;
 #pragma unroll
-    // Groups are issued in order and each issue is fenced (MOX_LD_FENCE): the
+    // Groups are issued in order and each issue is fenced: the
     // retire of the oldest group then waits for that group's loads only
     // (s_waitcnt vmcnt counts loads in issue order).  Unfenced, the scheduler
     // issued the first group's loads last, so retiring it waited for every
@@ -1733,15 +1288,15 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     // alone took 661 us of k_map's ~990 at C2 (tools/r04_ladder.sh).
     for (int g = 0; g < LD_GROUPS - 1; g++) {
       issue(buf[g], first + g * STRIDE);
-      if (MOX_LD_FENCE) SCHED_FENCE();
+      SCHED_FENCE();
     }
     for (uint32_t t0 = first; t0 < n; t0 += LD_GROUPS * STRIDE) {
 #pragma unroll
       for (int g = 0; g < LD_GROUPS; g++) {
         issue(buf[(g + LD_GROUPS - 1) % LD_GROUPS], t0 + (g + LD_GROUPS - 1) * STRIDE);
-        if (MOX_LD_FENCE) SCHED_FENCE();
+        SCHED_FENCE();
         retire(buf[g], t0 + g * STRIDE);
-        if (MOX_LD_FENCE) SCHED_FENCE();
+        SCHED_FENCE();
       }
     }
   } else {
@@ -1779,9 +1334,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
       const bool edge = u < e_lo || u >= e_hi;
       if (edge && (sbase < c.lo || sbase + SLOT > c.hi)) a = fix16(c, sbase + 16 * (uint64_t)lane, a);
       if (cp) { const uint64_t t0 = __builtin_amdgcn_s_memtime(); cp->wait += t0 - tw; cp->byte -= t0; cp->rows++; }
-      uint32_t nst = 0;
-      bool vclear = false;
-      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge, nst, vclear);
+      if (!MOX_ABL(w.dbg, DBG_NO_ROW)) do_row(m, sbase, a, ntok, sl, list, cp, edge);
       else asm volatile("" ::"v"(a.x), "v"(a.y), "v"(a.z), "v"(a.w));
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
       if (lane == 0) __hip_atomic_store(&sfree[slot], u + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1794,7 +1347,6 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
     }
 #endif
   }
-#endif
   __syncthreads();
   if (m.dict_n == 0) {  // records still parked in pair slots: written as singles
     for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {
@@ -2702,21 +2254,6 @@ __device__ __forceinline__ int red_try(const RedLds& s, uint32_t h, uint4 k, uin
 #endif
 }
 
-// Fast path for a key sitting in its home bucket's first slot: tag, key and
-// count read in one LDS round trip, 28 bytes.
-#ifndef MOX_RED_HOME
-#define MOX_RED_HOME 0
-#endif
-__device__ __forceinline__ bool red_home(const RedLds& s, uint32_t h, uint4 k, uint64_t c) {
-  const uint32_t sl = 4 * red_bucket(h);
-  const uint32_t t = reinterpret_cast<const uint32_t*>(s.tag4)[sl];
-  const uint4 kk = s.key[sl];
-  const unsigned long long cv = __hip_atomic_load(&s.cnt[sl], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (t != h || cv == 0 || !key_eq16(kk, k)) return false;
-  atomicAdd(&s.cnt[sl], (unsigned long long)c);
-  return true;
-}
-
 // Table order of short words: (h32, hash32b, key).  Every reduce kernel uses
 // it (k_reduce, k_reduce_small, k_reduce_sort1), so the order does not depend
 // on which kernel a key's unit went to, nor on whether its partition was split.
@@ -3480,11 +3017,6 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
           RED_MARK(1);
           if (!MOX_ABL(w.dbg, DBG_RED_NOINSERT)) {
-            if (MOX_RED_HOME) {
-#pragma unroll
-              for (int u2 = 0; u2 < RED_UNROLL; u2++)
-                if (todo[u2]) todo[u2] = !red_home(s, h[u2], cur[u2], 1);
-            }
             uint32_t nnew = 0;
 #pragma unroll
             for (int u2 = 0; u2 < RED_UNROLL; u2++) {
@@ -3584,7 +3116,31 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
           }
         }
       }
+      // The chunks' new-key counts went out as inline-asm LDS adds, which the
+      // compiler's wait-count tracking does not see: drain the DS queue
+      // explicitly, so the barrier's release cannot be dropped as "nothing
+      // pending" and misc[0] is settled when it is read below.
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __syncthreads();
+#ifdef MOX_CHECK
+      {  // table invariants red_try relies on: every bucket's taken slots are a
+         // prefix, and no key sits in two slots of its two buckets
+        bool ok = true;
+        for (int bk = tid; bk < RED_BUCKETS; bk += RED_THREADS) {
+          for (int i = 0; i < 4; i++) {
+            const uint32_t t = tags[4 * bk + i];
+            if (t == 0) {
+              for (int j = i + 1; j < 4; j++) ok = ok && tags[4 * bk + j] == 0;
+              continue;
+            }
+            const int lim = bk + 1 < RED_BUCKETS ? 8 : 4;
+            for (int j = i + 1; j < lim; j++)
+              if (tags[4 * bk + j] == t && key_eq16(s.key[4 * bk + j], s.key[4 * bk + i])) ok = false;
+          }
+        }
+        (void)MOX_CHK(w, ok, CHK_RED_TABLE);
+      }
+#endif
 #if MOX_RED_LAZYCAP
       if (s.misc[0] > (uint32_t)RED_CAP) {  // (uniform: every thread reads the settled count)
         __syncthreads();
@@ -3612,7 +3168,6 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
       // deterministic order (key_less): bucket sort by the hash bits below the
       // unit and sub-pass bits, then a key_less insertion sort inside each bin
       if (stamp) w.stamps[b * 8 + 2] = __builtin_amdgcn_s_memrealtime();  // all waves done inserting
-      const uint32_t nu = s.misc[0];
       const uint32_t bsh = shift0 + kk;
       for (int i = tid; i < RED_SORTB; i += RED_THREADS) { s.bin[i] = 0; s.fill[i] = 0; }
       __syncthreads();
@@ -3631,6 +3186,10 @@ extern "C" __global__ __launch_bounds__(RED_THREADS, 8) void k_reduce(Work w) { 
         if (tid == 0) s.bin[RED_SORTB] = (uint16_t)tot;
       }
       __syncthreads();
+      // distinct keys = taken slots (the tag count of the bin scan above), not
+      // misc[0]: no wave may disagree on it (check builds: the two agree)
+      const uint32_t nu = s.bin[RED_SORTB];
+      (void)MOX_CHK(w, nu == s.misc[0], CHK_RED_NU);
       for (int i = tid; i < RED_SLOTS; i += RED_THREADS)
         if (tags[i]) {
           const uint32_t bn = red_bin(tags[i], bsh);

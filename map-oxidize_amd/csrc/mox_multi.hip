@@ -265,15 +265,15 @@ int x_split(mox_engine* e, const uint64_t* all, size_t m) {
   return MOX_OK;
 }
 
-// Phase 2: layout from the host count rows (h_xcnt[0, P) = what this rank
-// sends to each peer, h_xcnt[MAX_RANKS + s] = what peer s sends here), then
-// the pack kernels into x_send_short / x_send_blob.
-int x_pack(mox_engine* e) {
-  HIPCHK(hipSetDevice(e->device));
-  XPlan& x = *e->xp;
+// Send / receive layout of one rank from its count rows (h_send[d] = what it
+// sends to peer d, h_recv[s] = what peer s sends to it): per-peer byte offsets
+// and lengths of both payloads, packed in peer order.  Pure host arithmetic;
+// rank i's s_*_len[p] equals rank p's r_*_len[i] whenever h_recv is the
+// transpose of the ranks' h_send rows (count_transpose, the transports), so
+// both sides of every pair skip or post the same send / receive
+// (tests/test_exchange_plan.py).
+void x_layout(XPlan& x, const XCnt* h_send, const XCnt* h_recv) {
   const int P = x.P;
-  const XCnt* h_send = e->h_xcnt;
-  const XCnt* h_recv = e->h_xcnt + MAX_RANKS;
   x.ns = x.sb = x.rs = x.rb = x.r_long = 0;
   x.sdir = XDir{};
   x.rdir = XDir{};
@@ -299,6 +299,23 @@ int x_pack(mox_engine* e) {
   x.sdir.blob[P] = x.sb;
   x.rdir.blob[P] = x.rb;
   x.rdir.hpre[P] = x.r_long;
+}
+
+// The count all-to-all of the device-copy transport (and its model in the
+// test hook): member i's receive row s = member s's send row i.
+void count_transpose(int P, XCnt* const* send_rows, XCnt* const* recv_rows) {
+  for (int i = 0; i < P; i++)
+    for (int s = 0; s < P; s++) recv_rows[i][s] = send_rows[s][i];
+}
+
+// Phase 2: layout from the host count rows (h_xcnt[0, P) = what this rank
+// sends to each peer, h_xcnt[MAX_RANKS + s] = what peer s sends here), then
+// the pack kernels into x_send_short / x_send_blob.
+int x_pack(mox_engine* e) {
+  HIPCHK(hipSetDevice(e->device));
+  XPlan& x = *e->xp;
+  const int P = x.P;
+  x_layout(x, e->h_xcnt, e->h_xcnt + MAX_RANKS);
   int rc;
   if ((rc = grow_dev(e->x_send_short, x.ns * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_send_blob, x.sb + 64)) ||
       (rc = grow_dev(e->x_recv_short, x.rs * sizeof(WRec) + 64)) || (rc = grow_dev(e->x_recv_blob, x.rb + 64)))
@@ -596,8 +613,12 @@ int group_counts(Group& G) {
     HIPCHK(hipMemcpyAsync(e->h_xcnt, e->d_xcnt, P * sizeof(XCnt), hipMemcpyDeviceToHost, e->stream));
   }
   if (int rc = sync_members(G)) return rc;
-  for (int i = 0; i < P; i++)
-    for (int s = 0; s < P; s++) G.m[i]->h_xcnt[MAX_RANKS + s] = G.m[s]->h_xcnt[i];
+  std::vector<XCnt*> snd(P), rcv(P);
+  for (int i = 0; i < P; i++) {
+    snd[i] = G.m[i]->h_xcnt;
+    rcv[i] = G.m[i]->h_xcnt + MAX_RANKS;
+  }
+  count_transpose(P, snd.data(), rcv.data());
   return MOX_OK;
 }
 
@@ -1106,6 +1127,33 @@ int mox_gather_host(mox_engine* e, int nranks, int rank, int root, mox_alltoallv
 int mox_reduce_pairs(mox_engine* e, const uint8_t* bytes, const uint64_t* offs, const uint64_t* counts, uint64_t n) {
   if (!e || (n && (!bytes || !offs || !counts))) return fail(MOX_EINVAL, "NULL argument");
   return reduce_pairs_impl(e, bytes, offs, counts, n);
+}
+
+int mox_debug_exchange_layout(int nranks, const uint64_t* counts, uint64_t* out) {
+  if (!counts || !out) return fail(MOX_EINVAL, "NULL argument");
+  if (nranks < 1 || nranks > MAX_RANKS) return fail(MOX_EINVAL, "bad rank count %d", nranks);
+  const int P = nranks;
+  std::vector<XCnt> rows(2 * (size_t)P * P);
+  std::vector<XCnt*> snd(P), rcv(P);
+  for (int i = 0; i < P; i++) {
+    snd[i] = rows.data() + (size_t)i * P;
+    rcv[i] = rows.data() + (size_t)(P + i) * P;
+    for (int d = 0; d < P; d++) {
+      const uint64_t* c = counts + ((size_t)i * P + d) * 3;
+      snd[i][d] = XCnt{c[0], c[1], c[2], 0};
+    }
+  }
+  count_transpose(P, snd.data(), rcv.data());
+  for (int i = 0; i < P; i++) {
+    XPlan x;
+    x.P = P;
+    x_layout(x, snd[i], rcv[i]);
+    const uint64_t* cols[8] = {x.s_short_off, x.s_short_len, x.s_blob_off, x.s_blob_len,
+                               x.r_short_off, x.r_short_len, x.r_blob_off, x.r_blob_len};
+    for (int k = 0; k < 8; k++)
+      for (int d = 0; d < P; d++) out[((size_t)i * 8 + k) * P + d] = cols[k][d];
+  }
+  return MOX_OK;
 }
 
 }  // extern "C"

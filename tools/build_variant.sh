@@ -7,7 +7,7 @@
 # commit's, exported with tools/export_src.sh).
 set -e
 NAME=$1; shift
-FLAGS="$*"
+FLAGS="-DMOX_EXPERIMENT_BUILD $*"  # experiment builds only (mox_internal.h: ablation switches)
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/build/var_$NAME
 mkdir -p $OUT
