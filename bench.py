@@ -190,6 +190,32 @@ def roofline_fields(per_rank, map_avg, workload, traffic_json):
     return r
 
 
+def same_work_n1(eng, shard, per_rank, steps, warmup, n, value_n):
+    """The N = 1 figure of an N > 1 line on the same per-GPU work (weak-scaling
+    denominator): ONE GPU alone on the shard of rank / member 0 -- a synchronous
+    pass plus the device bytewise sort of its table per step, the N > 1 step's
+    local work without the exchange and the gather -- timed after the N > 1
+    steps in the same run.  ``eng`` is a single-GPU engine with the sort flag."""
+    d, blen, ob, oe, end = shard
+    for _ in range(warmup):
+        eng.run_range(d, blen, ob, oe, end)
+        eng.sort_result()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        eng.run_range(d, blen, ob, oe, end)
+        eng.sort_result()
+    eng.synchronize()
+    el = time.perf_counter() - t0
+    v1 = per_rank / (el / steps) / 1e9
+    return {"value": round(v1, 3), "unit": "GB/s", "ms_per_step": round(el / steps * 1e3, 4),
+            "scaling_efficiency": round(value_n / (n * v1), 4),
+            "note": "one GPU alone on shard 0 of this run (%d MiB): synchronous pass + device bytewise sort of its "
+                    "table per step (the N > 1 step's per-GPU work without exchange and gather), %d untimed + %d "
+                    "timed steps after the N > 1 steps; scaling_efficiency = value / (n_gpus x this)"
+                    % (per_rank >> 20, warmup, steps)}
+
+
 def main_group(a):
     """--gpus N > 1 without torchrun: one process, one engine group over N GPUs.
     A timed step is one mox_run_shards call with MOX_F_SORT_BYTES: local passes,
@@ -241,6 +267,11 @@ def main_group(a):
     progress("sorted-result steps")
     elapsed, rows = timed(base_flags | mox.MOX_F_SORT_BYTES)  # the value: sorted result inside the step
     last = rows[-1]
+    progress("same-work N = 1 steps (member 0's shard alone)")
+    e1 = mox.Engine(device=devices[0] if devices else 0, flags=base_flags | mox.MOX_F_TIMING_MAP | mox.MOX_F_SORT_BYTES,
+                    sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
+    n1 = same_work_n1(e1, shards[0], per_rank, a.steps, a.warmup, n, total / (elapsed / a.steps) / 1e9)
+    e1.close()
     t = g.fetch()  # bytewise order (sorted on GPU 0 by the last timed step)
     counts, offs, raw = t.arrays()
     table_n, table_bytes, table_tokens = t.n, int(offs[-1]) if t.n else 0, t.tokens
@@ -300,6 +331,7 @@ def main_group(a):
                                "order": "bytewise (sorted exchange: each member sorts its byte range on its GPU "
                                         "inside the timed step; sort_bytes = the slowest member's sort)"},
         },
+        "same_work_n1": n1,
         "check_sum_counts_eq_tokens": ok,
         "cpu_baseline": None,
     }
@@ -416,6 +448,18 @@ def main():
         if dist:
             dist.barrier()
         el_hash = time.perf_counter() - t1
+    n1 = None
+    if world > 1 and gather:
+        # the same-work N = 1 figure: rank 0 alone on its shard while the others wait
+        if dist:
+            dist.barrier()
+        if rank == 0:
+            progress("same-work N = 1 steps (rank 0's shard alone)")
+            eng.set_flags(base_flags | mox.MOX_F_TIMING_MAP | mox.MOX_F_SORT_BYTES)
+            n1 = (hi - lo, own_b, own_e, at_end)
+            n1 = same_work_n1(eng, (d_buf,) + n1, per_rank, a.steps, a.warmup, world, 0.0)
+        if dist:
+            dist.barrier()
     sorted_result = None
     if world == 1:
         # like-for-like with the N > 1 line (whose step ends in the bytewise
@@ -496,6 +540,8 @@ def main():
         ms_step = elapsed / a.steps * 1e3
         gbs = total / (elapsed / a.steps) / 1e9
         map_avg = statistics.mean(map_ms)
+        if n1:  # the efficiency against the max-over-ranks time (known only now)
+            n1["scaling_efficiency"] = round(gbs / (world * n1["value"]), 4)
         # algorithmic bytes per step = input read once + the output
         # table written once (word bytes + a u64 count per distinct word)
         b_alg = total + (table_bytes + 8 * table_n if (world == 1 or gather) else 0)
@@ -534,6 +580,7 @@ def main():
                                            "reduce_units", "split_partitions")},
             "multi_gpu": xinfo,
             "sorted_result": sorted_result,
+            "same_work_n1": n1,
             "check_sum_counts_eq_tokens": ok,
             "cpu_baseline": None,
         }

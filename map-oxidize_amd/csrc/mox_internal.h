@@ -28,13 +28,27 @@ constexpr int MAP_LOADERS = 1;              // loader waves
 #define MOX_RING 32
 #endif
 constexpr int RING = MOX_RING;              // k_map row ring slots (LDS)
-#ifndef MOX_DICT_SLOTS
-#define MOX_DICT_SLOTS 5120
-#endif
 // LDS hot dictionary: single-word slots, two choices per word (dict_s1 / dict_s2,
-// mox_kernels.hip); k_dict_pick picks up to DICT_MAX_WORDS candidates
+// mox_kernels.hip); k_dict_pick picks up to DICT_MAX_WORDS candidates.
+// MOX_DICT12: a slot is one 16-byte LDS word, the lowered key's first 12 bytes
+// and the workgroup's u32 count of the word (words of at most 12 bytes: 99.5 %
+// of the hot words), instead of a 16-byte key plus a count in a separate array
+// (20 bytes): a third more words in the same LDS, at the same VALU cost per
+// probe (the count address is the hit slot's plus 12).
+#ifndef MOX_DICT12
+#define MOX_DICT12 0
+#endif
+constexpr bool DICT12 = MOX_DICT12 != 0;
+#ifndef MOX_DICT_SLOTS
+#define MOX_DICT_SLOTS (MOX_DICT12 ? 6752 : 5120)
+#endif
 constexpr int DICT_SLOTS = MOX_DICT_SLOTS;
-constexpr int DICT_MAX_WORDS = DICT_SLOTS < 4096 ? DICT_SLOTS : 4096;
+#ifndef MOX_DICT_MAX_WORDS
+#define MOX_DICT_MAX_WORDS (MOX_DICT12 ? 5120 : 4096)
+#endif
+constexpr int DICT_MAX_WORDS = DICT_SLOTS < MOX_DICT_MAX_WORDS ? DICT_SLOTS : MOX_DICT_MAX_WORDS;
+constexpr uint32_t DICT_KEY_BYTES = DICT12 ? 12u : 16u;  // longest dictionary word
+constexpr size_t DICT_CNT_BYTES = DICT12 ? 0 : (size_t)DICT_SLOTS * 4;  // k_map's separate count array
 static_assert(DICT_SLOTS % 32 == 0 && DICT_SLOTS <= 65536 && DICT_MAX_WORDS <= DICT_SLOTS, "dictionary geometry");
 constexpr int MAX_MAP_GRID = 1024;          // map workgroups
 constexpr int MAP_WAVES = MAP_THREADS / 64;
@@ -75,7 +89,7 @@ constexpr uint32_t QF_MAX = 4;              // most cold regions per (map workgr
 // k_map dynamic LDS (carved in this order by k_map): dictionary counts, region
 // counters, misc, key selectors, dictionary keys, then the row ring with its
 // ready / free words and the token lists
-constexpr size_t MAP_LDS_BYTES = (size_t)DICT_SLOTS * (16 + 4) + NB * 4 + 16 + KSEL_N * 16 +
+constexpr size_t MAP_LDS_BYTES = (size_t)DICT_SLOTS * 16 + DICT_CNT_BYTES + NB * 4 + 16 + KSEL_N * 16 +
                                  (size_t)RING * 8 + (size_t)RING * SLOT + (size_t)MAP_ROW_WAVES * 2 * LIST_N;
 static_assert(MAP_LDS_BYTES <= 160 * 1024, "k_map LDS over 160 KiB");
 constexpr int GC_SLOTS = 65536;             // global dictionary candidate table (k_sample -> k_dict_*)

@@ -348,9 +348,9 @@ __device__ __forceinline__ uint32_t slot_off16(uint32_t p) {
 // and the pair goes out as one aligned 32-byte sector.
 constexpr uint32_t PS_EMPTY = 0u, PS_BUSY = 1u, PS_FULL = 2u;
 struct MapLds {
-  uint4* dkey;      // DICT_SLOTS 16-byte keys (zero = empty: a real key is never zero)
-  uint32_t* dcnt;   // DICT_SLOTS
-  uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's space)
+  uint4* dkey;      // DICT_SLOTS 16-byte keys (zero = empty: a real key is never zero); DICT12: 12-byte key + count
+  uint32_t* dcnt;   // DICT_SLOTS counts (DICT12: unused, the count is dkey[s].w)
+  uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's / dkey's space)
   uint32_t* misc;   // [0] spills [1] row ticket
   uint4* seltab;    // [KSEL_N]: v_perm selectors of a len-byte key at byte offset sh (entry 4 len + sh)
   uint32_t kmask;   // 0x3FC in a VGPR (key_load's v_bitop3_b32 takes no literal)
@@ -368,7 +368,7 @@ struct MapLds {
 constexpr uint32_t L_ROWS = 0;
 constexpr uint32_t L_ROWS_BYTES = RING * SLOT;
 constexpr uint32_t L_DCNT = L_ROWS + L_ROWS_BYTES;
-constexpr uint32_t L_BCNT = L_DCNT + DICT_SLOTS * 4;
+constexpr uint32_t L_BCNT = L_DCNT + (uint32_t)DICT_CNT_BYTES;
 constexpr uint32_t L_MISC = L_BCNT + NB * 4;
 constexpr uint32_t L_SELTAB = L_MISC + 16;
 constexpr uint32_t L_DKEY = L_SELTAB + KSEL_N * 16;
@@ -419,7 +419,12 @@ __device__ __forceinline__ KWork rare_ptr(const MapCtx& m) {
 #define rare(m) (*rare_ptr(m))
 
 __device__ __forceinline__ bool key_eq(uint4 k, uint64_t w0, uint64_t w1) {
+  if (DICT12) return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && (w1 >> 32) == 0;
   return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && k.w == (uint32_t)(w1 >> 32);
+}
+// The LDS count of dictionary slot s (DICT12: the slot's fourth dword).
+__device__ __forceinline__ uint32_t* dict_cnt(const MapLds& s, uint32_t slot) {
+  return DICT12 ? &s.dkey[slot].w : &s.dcnt[slot];
 }
 // Exact dictionary lookup: the key's two slots.
 __device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w0, uint64_t w1) {
@@ -440,7 +445,7 @@ __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_
   if (m.dict_n && !MOX_ABL(m.w.dbg, DBG_NO_DICT)) {
     const int slot = dict_find(m.s, h, w0, w1);
     if (slot >= 0) {
-      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
+      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(dict_cnt(m.s, slot), 1u);
       return;
     }
   }
@@ -829,7 +834,9 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
   uint32_t d = k.x ^ K[0];
   d = __builtin_amdgcn_bitop3_b32(k.y, K[1], d, 0xBE);
   d = __builtin_amdgcn_bitop3_b32(k.z, K[2], d, 0xBE);
-  d = __builtin_amdgcn_bitop3_b32(k.w, K[3], d, 0xBE);
+  // DICT12: the slot's fourth dword is its count; a token longer than 12
+  // bytes (K[3] != 0) matches no slot
+  d = DICT12 ? (d | K[3]) : __builtin_amdgcn_bitop3_b32(k.w, K[3], d, 0xBE);
   return d == 0;
 }
 
@@ -884,11 +891,15 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     nvalid += (uint32_t)__popcll(__ballot(valid));
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
     miss[u] = valid & !(hit1 | hit2);
-    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
+    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) {
+      if (DICT12) atomicAdd(lds_ptr<uint32_t>(L_DKEY + 12u + (hit1 ? s1[u] : s2[u])), 1u);
+      else atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
+    }
 #if defined(MOX_PATHS) && MOX_PATHS
     if (miss[u]) {
-      if ((d1[u].x | d1[u].y | d1[u].z | d1[u].w) && hash32(d1[u].x, d1[u].y, d1[u].z, d1[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
-      if ((d2[u].x | d2[u].y | d2[u].z | d2[u].w) && hash32(d2[u].x, d2[u].y, d2[u].z, d2[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
+      const uint32_t w1 = DICT12 ? 0u : d1[u].w, w2 = DICT12 ? 0u : d2[u].w;
+      if ((d1[u].x | d1[u].y | d1[u].z | w1) && hash32(d1[u].x, d1[u].y, d1[u].z, w1) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
+      if ((d2[u].x | d2[u].y | d2[u].z | w2) && hash32(d2[u].x, d2[u].y, d2[u].z, w2) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
     }
 #endif
   }
@@ -1191,8 +1202,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint16_t* lists = lds_ptr<uint16_t>(L_LISTS);
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
-  static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
-  static_assert(NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
+  static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 + (DICT12 ? NB * QF_MAX * 4 : 0) <= DICT_SLOTS * 16, "pair slots inside dkey");
+  static_assert(DICT12 || NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
@@ -1201,12 +1212,12 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.rg = w.map_grid * m.qf;
   m.rc = w.cold_cap / m.qf;
   m.wcold = w.cold + (uint64_t)blockIdx.x * m.qf * NB * m.rc;
-  if (!m.dict_n) m.s.bcnt = m.s.dcnt;  // NB x qf region counters
+  if (!m.dict_n) m.s.bcnt = DICT12 ? m.s.pst + NB * QF_MAX : m.s.dcnt;  // NB x qf region counters
   // without a dictionary the key array is zero (no real key is zero, so nothing
   // would hit; that case takes pass_c, and the pair slots live there)
   for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
-    m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);
-    m.s.dcnt[i] = 0;
+    m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);  // (DICT12: the image's count dword is 0)
+    if (!DICT12) m.s.dcnt[i] = 0;
   }
   __syncthreads();  // (no dictionary: the region counters live in dcnt's space)
   for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {
@@ -1362,7 +1373,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   }
   if (m.dict_n) {
     for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
-      const uint32_t cnt = m.s.dcnt[i];
+      const uint32_t cnt = *dict_cnt(m.s, i);
       if (cnt) atomicAdd(&w.dict_tot[i], (unsigned long long)cnt);
     }
   }
@@ -1587,6 +1598,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_hist(Work w) {
   __syncthreads();
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < GC_SLOTS; i += gridDim.x * 1024) {
     const uint64_t n = w.cand[i].count;
+    if (DICT12 && ((w.cand[i].w1 & ~(1ull << 63)) >> 32) != 0) continue;  // over 12 bytes: never picked (k_dict_pick)
     if (n) atomicAdd(&h[n > 255 ? 255 : n], 1u);
   }
   __syncthreads();
@@ -1645,7 +1657,9 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
   const uint32_t t = T, t1 = T - 1;
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const WRec r = w.cand[i];
-  const bool real = r.w0 != 0 && r.w1 != 0;
+  // (DICT12: words over 12 bytes never enter the dictionary: w1's high half is
+  // zero below the claim marker bit)
+  const bool real = r.w0 != 0 && r.w1 != 0 && (!DICT12 || ((r.w1 & ~(1ull << 63)) >> 32) == 0);
   const bool pick = real && r.count >= t;
   const bool fill = real && t1 >= 2 && t1 < 255 && r.count == t1;
   const uint64_t bm = __ballot(pick), bf = __ballot(fill);
