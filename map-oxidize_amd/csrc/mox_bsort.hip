@@ -52,7 +52,6 @@ constexpr int OS_TILE = OS_THREADS * OS_ITEMS;   // 4,096 records per tile (16 K
 constexpr int OS_WG_PER_CU = OS_ITEMS <= 8 ? 4 : 2;
 constexpr int OS_WAVES = OS_THREADS / 64;
 constexpr int OS_DIGITS = 12;                    // key bytes 0..7 (0 = aux), run bytes 0..3
-constexpr int SCAN_T = 1024, SCAN_PER = 8, SCAN_TILE = SCAN_T * SCAN_PER;
 // look-back status word of (tile, digit): flag in bits 63..62, count below
 constexpr uint64_t ST_AGG = 1ull << 62, ST_INC = 2ull << 62, ST_VAL = (1ull << 62) - 1;
 constexpr uint32_t OS_SPIN_MAX = 1u << 22;       // a look-back that waits longer reports a failure (never expected)
@@ -64,13 +63,22 @@ __device__ __forceinline__ uint32_t digit_of(const BRec& r, int d) {
   return (r.run >> (8 * (d - 8))) & 0xFFu;
 }
 
-// Window bytes [WIN level, WIN level + WIN) of word i and its length class.
+// Window bytes [WIN level, WIN level + WIN) of word i and its length class:
+// two aligned 8-byte loads and a funnel shift (the table's byte buffers carry
+// 64 bytes of slack past their end: grow_dev callers), not one load per byte.
 __device__ __forceinline__ uint64_t window(const uint64_t* offs, const uint8_t* bytes, uint64_t i, uint32_t level) {
   const uint64_t o = offs[i], len = offs[i + 1] - o, a = (uint64_t)WIN * level;
   const uint64_t have = len > a ? len - a : 0;
   const uint32_t nb = have < WIN ? (uint32_t)have : WIN;
   uint64_t k = 0;
-  for (uint32_t j = 0; j < nb; j++) k |= (uint64_t)bytes[o + a + j] << (8 * (7 - j));
+  if (nb) {
+    const uint64_t p = o + a, base = p & ~7ull;
+    const uint32_t sh = (uint32_t)(p & 7u);
+    const uint64_t* q = reinterpret_cast<const uint64_t*>(bytes + base);
+    const uint64_t lo = q[0], hi = sh + nb > 8 ? q[1] : 0ull;
+    const uint64_t le = sh ? (lo >> (8 * sh)) | (hi << (64 - 8 * sh)) : lo;  // bytes p .. p + 7, little-endian
+    k = __builtin_bswap64(le & ((1ull << (8 * nb)) - 1ull));                   // nb <= 7: byte j at bits 63 - 8 j
+  }
   return k | (have > WIN ? AUX_MORE : (uint32_t)have);
 }
 
@@ -266,64 +274,123 @@ extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass
   }
 }
 
-// Exclusive scan of u64 (three kernels: tile sums, scan of the tile sums in
-// one workgroup, tile scans with their offsets).  In place.
-__device__ __forceinline__ uint64_t wg_exscan(uint64_t x, uint64_t* ws, uint64_t& tot) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+// Exclusive scan of u64 in place, without any wait on another workgroup (a
+// decoupled look-back over tiles measured 27-50 us per scan of 1.4 M values:
+// every status read crosses the XCDs' L2s).  k_scan_tsum: tile sums (coalesced
+// reads, SC1_TILE values per tile); [k_scan_top: exclusive scan of the tile
+// sums in one workgroup, only for more than SC1_TOP tiles]; k_scan_tile: a
+// tile's prefix (the sum of the tile sums before it, reduced by the workgroup
+// itself, or the scanned sum), its values scanned through LDS (padded: a
+// thread's 16 consecutive values in distinct banks), written back coalesced;
+// the last tile writes the total.
+constexpr int SC1_T = 256, SC1_PER = 16, SC1_TILE = SC1_T * SC1_PER;
+constexpr int SC1_PAD = SC1_PER + 1;   // LDS row of a thread: 16 values + 1 pad
+constexpr uint64_t SC1_TOP = 4096;     // tile sums a workgroup reduces itself (16 per thread)
+__device__ __forceinline__ uint64_t wave_exscan64(uint64_t x, uint64_t& wave_tot) {
+  const int lane = threadIdx.x & 63;
   uint64_t inc = x;
   for (int o = 1; o < 64; o <<= 1) {
     const uint64_t y = __shfl_up(inc, o);
     if (lane >= o) inc += y;
   }
-  if (lane == 63) ws[wv] = inc;
-  __syncthreads();
-  uint64_t pre = 0, t = 0;
-  for (int k = 0; k < nw; k++) { if (k < wv) pre += ws[k]; t += ws[k]; }
-  __syncthreads();
-  tot = t;
-  return pre + inc - x;
+  wave_tot = __shfl(inc, 63);
+  return inc - x;
 }
-extern "C" __global__ __launch_bounds__(SCAN_T) void k_scan_sums(const uint64_t* a, uint64_t n, uint64_t* sums) {
-  __shared__ uint64_t ws[SCAN_T / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_TILE;
-  uint64_t s = 0;
-  for (int j = 0; j < SCAN_PER; j++) {
-    const uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + j;
-    if (i < n) s += a[i];
+// block sum of x (SC1_T threads), every thread gets it
+__device__ __forceinline__ uint64_t block_sum64(uint64_t x, uint64_t* ws) {
+  uint64_t wt;
+  (void)wave_exscan64(x, wt);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = wt;
+  __syncthreads();
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 0; k < SC1_T / 64; k++) t += ws[k];
+  return t;
+}
+extern "C" __global__ __launch_bounds__(SC1_T) void k_scan_tsum(const uint64_t* a, uint64_t n, uint64_t* sums) {
+  __shared__ uint64_t ws[SC1_T / 64];
+  const uint64_t t0 = (uint64_t)blockIdx.x * SC1_TILE;
+  uint64_t x = 0;
+#pragma unroll
+  for (int k = 0; k < SC1_PER; k++) {
+    const uint64_t i = t0 + (uint64_t)k * SC1_T + threadIdx.x;
+    x += i < n ? a[i] : 0ull;
   }
-  uint64_t tot;
-  (void)wg_exscan(s, ws, tot);
+  const uint64_t tot = block_sum64(x, ws);
   if (threadIdx.x == 0) sums[blockIdx.x] = tot;
 }
-extern "C" __global__ __launch_bounds__(SCAN_T) void k_scan_top(uint64_t* sums, uint64_t nt, uint64_t* total) {
-  __shared__ uint64_t ws[SCAN_T / 64];
+extern "C" __global__ __launch_bounds__(1024) void k_scan_top(uint64_t* sums, uint64_t nt) {
+  __shared__ uint64_t ws[16];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint64_t carry = 0;
-  for (uint64_t c = 0; c < nt; c += SCAN_T) {
+  for (uint64_t c = 0; c < nt; c += 1024) {
     const uint64_t i = c + threadIdx.x;
-    const uint64_t x = i < nt ? sums[i] : 0;
-    uint64_t tot;
-    const uint64_t ex = wg_exscan(x, ws, tot);
-    if (i < nt) sums[i] = carry + ex;
+    const uint64_t x = i < nt ? sums[i] : 0ull;
+    uint64_t wt;
+    const uint64_t ex = wave_exscan64(x, wt);
+    if (lane == 0) ws[wv] = wt;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int k = 0; k < 16; k++) { if (k < wv) pre += ws[k]; tot += ws[k]; }
+    if (i < nt) sums[i] = carry + pre + ex;
     carry += tot;
+    __syncthreads();
   }
-  if (threadIdx.x == 0 && total) *total = carry;
 }
-extern "C" __global__ __launch_bounds__(SCAN_T) void k_scan_fin(uint64_t* a, uint64_t n, const uint64_t* sums) {
-  __shared__ uint64_t ws[SCAN_T / 64];
-  const uint64_t b0 = (uint64_t)blockIdx.x * SCAN_TILE;
-  uint64_t v[SCAN_PER], s = 0;
-  for (int j = 0; j < SCAN_PER; j++) {
-    const uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + j;
-    v[j] = i < n ? a[i] : 0;
-    s += v[j];
+extern "C" __global__ __launch_bounds__(SC1_T) void k_scan_tile(uint64_t* a, uint64_t n, const uint64_t* sums, int scanned,
+                                                                uint64_t* total) {
+  __shared__ uint64_t v[SC1_T * SC1_PAD];
+  __shared__ uint64_t ws[SC1_T / 64];
+  const int t = threadIdx.x, wv = t >> 6;
+  const uint64_t tile = blockIdx.x, t0 = tile * SC1_TILE;
+  // coalesced: value t0 + k 256 + t goes to LDS row (k 256 + t) / 16
+#pragma unroll
+  for (int k = 0; k < SC1_PER; k++) {
+    const uint32_t e = (uint32_t)(k * SC1_T + t);
+    const uint64_t i = t0 + e;
+    v[(e >> 4) * SC1_PAD + (e & 15u)] = i < n ? a[i] : 0ull;
   }
-  uint64_t tot;
-  uint64_t ex = wg_exscan(s, ws, tot) + sums[blockIdx.x];
-  for (int j = 0; j < SCAN_PER; j++) {
-    const uint64_t i = b0 + (uint64_t)threadIdx.x * SCAN_PER + j;
-    if (i < n) a[i] = ex;
-    ex += v[j];
+  uint64_t pre;
+  if (scanned) {
+    pre = sums[tile];
+  } else {  // the sums of the tiles before this one (at most SC1_TOP)
+    uint64_t x = 0;
+    for (uint64_t k = t; k < tile; k += SC1_T) x += sums[k];
+    pre = block_sum64(x, ws);  // (its barriers also publish v)
   }
+  __syncthreads();
+  uint64_t x[SC1_PER], sum = 0;
+#pragma unroll
+  for (int j = 0; j < SC1_PER; j++) {
+    x[j] = v[t * SC1_PAD + j];
+    sum += x[j];
+  }
+  uint64_t wtot;
+  const uint64_t wex = wave_exscan64(sum, wtot);
+  __syncthreads();  // (ws reused)
+  if ((t & 63) == 0) ws[wv] = wtot;
+  __syncthreads();
+  uint64_t wpre = 0, agg = 0;
+#pragma unroll
+  for (int k = 0; k < SC1_T / 64; k++) {
+    if (k < wv) wpre += ws[k];
+    agg += ws[k];
+  }
+  uint64_t run = pre + wpre + wex;
+#pragma unroll
+  for (int j = 0; j < SC1_PER; j++) {
+    v[t * SC1_PAD + j] = run;
+    run += x[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < SC1_PER; k++) {
+    const uint32_t e = (uint32_t)(k * SC1_T + t);
+    const uint64_t i = t0 + e;
+    if (i < n) a[i] = v[(e >> 4) * SC1_PAD + (e & 15u)];
+  }
+  if (t == 0 && t0 + SC1_TILE >= n && total) *total = pre + agg;  // the last tile
 }
 
 // Tie runs after a level: sorted records j - 1 and j are tied when they carry
@@ -344,10 +411,23 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_ties(const BRec* r, uint6
 // After the exclusive scan of fl: every record in a run goes to the subset at
 // its compact index with its next window and the run id base + (heads up to
 // and including its run's), and its sorted position.  The subset is in sorted
-// position order, so each run is a contiguous segment of it.
-extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r, uint64_t n, const uint64_t* fx, uint64_t m,
-                                                                   uint32_t run_base, const uint64_t* offs, const uint8_t* bytes,
+// position order, so each run is a contiguous segment of it.  The subset size
+// m and the run count come from the scan's total (*tot: m | runs << 32) and
+// the level's first run id from *rb_in, all on the device (no host round trip
+// per level); block 0 publishes the next level's first run id and resets the
+// long-run list for k_bs_segsort.
+extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r, uint64_t n, const uint64_t* fx, const uint64_t* tot,
+                                                                   const uint32_t* rb_in, uint32_t* rb_out, unsigned int* nlrun,
+                                                                   unsigned int* err, const uint64_t* offs, const uint8_t* bytes,
                                                                    uint32_t level, BRec* sub, uint64_t* pos) {
+  const uint64_t m = tot[0] & 0xFFFFFFFFull, runs = tot[0] >> 32;
+  const uint32_t run_base = *rb_in;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if ((uint64_t)run_base + runs >= (1ull << 32)) atomicOr(err, 2u);  // too many tie runs (the host fails the sort)
+    *rb_out = (uint32_t)(run_base + runs);
+    *nlrun = 0;
+  }
+  if (m == 0) return;
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
     const uint64_t f = fx[j], c = f & 0xFFFFFFFFull, c1 = j + 1 < n ? (fx[j + 1] & 0xFFFFFFFFull) : m;
     if (c1 == c) continue;  // not in a run
@@ -361,50 +441,59 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r
     pos[c] = j;
   }
 }
-// The subset's runs sorted by key, each by one thread in LDS (insertion sort):
-// a workgroup loads SEG_CH subset records (plus SEG_MAX after them) and sorts
-// the runs whose head lies in its SEG_CH.  A run longer than SEG_MAX is listed
-// (lrun: its first record and length) for k_bs_longsort; one longer than
-// RUN_LMAX, or one running past the loaded window, sets *longrun, and the host
-// then radix-sorts the whole subset instead.  Typical runs are a long word's
-// punctuation variants: a few records each.
+// The subset's runs sorted by key in LDS: a workgroup loads SEG_CH subset
+// records (plus SEG_MAX after them) and sorts the runs whose head lies in its
+// SEG_CH.  Every record of such a run ranks itself against the run (records
+// with a smaller key, or an equal key at a smaller position: a stable order)
+// and is written to its run start + rank: the work of a run of L records is
+// spread over its L threads, L compares each (one thread per run doing an
+// insertion sort left the other threads idle and ran O(L^2) dependent steps:
+// ~35 us per level at C2).  A run longer than SEG_MAX is listed (lrun: its first
+// record and length) for k_bs_longsort by its head; one longer than RUN_LMAX,
+// or one running past the loaded window beyond the list, sets *longrun, and
+// the host then radix-sorts the whole subset instead.  Typical runs are a long
+// word's punctuation variants: a few records each.
 constexpr int SEG_CH = 2048, SEG_MAX = 64, RUN_LMAX = 4096;
-extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, uint64_t m, unsigned int* longrun, uint2* lrun,
+extern "C" __global__ __launch_bounds__(256) void k_bs_segsort(BRec* S, const uint64_t* tot, unsigned int* longrun, uint2* lrun,
                                                                unsigned int* nlrun, unsigned int lrun_cap) {
   __shared__ BRec ls[SEG_CH + SEG_MAX];
   const int t = threadIdx.x;
+  const uint64_t m = tot[0] & 0xFFFFFFFFull;  // the subset size (k_bs_gather_ties)
   for (uint64_t c0 = (uint64_t)blockIdx.x * SEG_CH; c0 < m; c0 += (uint64_t)gridDim.x * SEG_CH) {
     const uint32_t nl = (uint32_t)(m - c0 < (uint64_t)(SEG_CH + SEG_MAX) ? m - c0 : (uint64_t)(SEG_CH + SEG_MAX));
     for (uint32_t i = t; i < nl; i += 256) ls[i] = S[c0 + i];
     const uint32_t prev_run = c0 > 0 ? S[c0 - 1].run : 0xFFFFFFFFu;
     __syncthreads();
     const uint32_t nh = nl < (uint32_t)SEG_CH ? nl : (uint32_t)SEG_CH;
-    for (uint32_t p = t; p < nh; p += 256) {
+    for (uint32_t p = t; p < nl; p += 256) {
       const uint32_t run = ls[p].run;
-      if ((p == 0 ? prev_run : ls[p - 1].run) == run) continue;  // not a run head
-      uint32_t e = p;
-      while (e + 1 < nl && ls[e + 1].run == run) e++;
-      if (e + 1 == nl && c0 + nl < m && S[c0 + nl].run == run) {  // runs on past the window: count it out
-        uint64_t f = c0 + nl;
-        while (f < m && f - (c0 + p) <= (uint64_t)RUN_LMAX && S[f].run == run) f++;
-        const uint64_t len = f - (c0 + p);
+      // head of p's run inside the window (at most SEG_MAX back for a run this
+      // workgroup sorts); a head before the window belongs to the previous chunk
+      uint32_t h = p;
+      while (h > 0 && p - h <= (uint32_t)SEG_MAX && ls[h - 1].run == run) h--;
+      if (p - h > (uint32_t)SEG_MAX) continue;  // a run past SEG_MAX: listed by its head
+      if (h == 0 && prev_run == run) continue;   // the previous chunk's run
+      if (h >= nh) continue;                     // the next chunk's run
+      uint32_t e = p;  // last record of the run inside the window
+      while (e + 1 < nl && e - h < (uint32_t)SEG_MAX && ls[e + 1].run == run) e++;
+      const bool cut = (e + 1 == nl && c0 + nl < m && S[c0 + nl].run == run) || (e - h >= (uint32_t)SEG_MAX && e + 1 < nl && ls[e + 1].run == run);
+      if (cut || e - h + 1 > (uint32_t)SEG_MAX) {  // longer than SEG_MAX (or past the window): its head lists it
+        if (p != h) continue;
+        uint64_t f = c0 + e + 1;
+        while (f < m && f - (c0 + h) <= (uint64_t)RUN_LMAX && S[f].run == run) f++;
+        const uint64_t len = f - (c0 + h);
         if (len > (uint64_t)RUN_LMAX) { atomicOr(longrun, 1u); continue; }
         const unsigned int q = atomicAdd(nlrun, 1u);
-        if (q < lrun_cap) lrun[q] = make_uint2((uint32_t)(c0 + p), (uint32_t)len); else atomicOr(longrun, 1u);
+        if (q < lrun_cap) lrun[q] = make_uint2((uint32_t)(c0 + h), (uint32_t)len); else atomicOr(longrun, 1u);
         continue;
       }
-      if (e - p + 1 > (uint32_t)SEG_MAX) {  // k_bs_longsort
-        const unsigned int q = atomicAdd(nlrun, 1u);
-        if (q < lrun_cap) lrun[q] = make_uint2((uint32_t)(c0 + p), e - p + 1); else atomicOr(longrun, 1u);
-        continue;
+      const uint64_t key = ls[p].key;
+      uint32_t rank = 0;
+      for (uint32_t k = h; k <= e; k++) {
+        const uint64_t kk = ls[k].key;
+        rank += (kk < key || (kk == key && k < p)) ? 1u : 0u;
       }
-      for (uint32_t k = p + 1; k <= e; k++) {
-        const BRec x = ls[k];
-        uint32_t q = k;
-        while (q > p && ls[q - 1].key > x.key) { ls[q] = ls[q - 1]; q--; }
-        ls[q] = x;
-      }
-      for (uint32_t k = p; k <= e; k++) S[c0 + k] = ls[k];
+      S[c0 + h + rank] = ls[p];
     }
     __syncthreads();  // ls is reloaded for the next chunk
   }
@@ -444,7 +533,8 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_longsort(BRec* S, const u
     __syncthreads();
   }
 }
-extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub, uint64_t m, const uint64_t* pos, BRec* r) {
+extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub, const uint64_t* tot, const uint64_t* pos, BRec* r) {
+  const uint64_t m = tot[0] & 0xFFFFFFFFull;
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += (uint64_t)gridDim.x * blockDim.x) r[pos[c]] = sub[c];
 }
 // Output table in sorted order: counts and lengths, then (after the length
@@ -533,17 +623,21 @@ namespace {
 
 int grid_for(uint64_t n) { return (int)std::min<uint64_t>(4096, std::max<uint64_t>(1, (n + 255) / 256)); }
 
-// Exclusive scan of a[0, n) in place on the engine stream; *d_total (device) =
-// the sum.  sums: scratch of (n + SCAN_TILE - 1) / SCAN_TILE words.
+// Exclusive scan of a[0, n) in place on the engine stream (k_scan_tsum,
+// [k_scan_top,] k_scan_tile); *d_total (device) = the sum.  sums: scratch of
+// scan_sum_words(n) words.
+uint64_t scan_sum_words(uint64_t n) { return (n + SC1_TILE - 1) / SC1_TILE + 8; }
 int scan_u64(mox_engine* e, uint64_t* a, uint64_t n, uint64_t* d_total, uint64_t* sums) {
-  const uint64_t nt = (n + SCAN_TILE - 1) / SCAN_TILE;
   if (n == 0) {
     HIPCHK(hipMemsetAsync(d_total, 0, 8, e->stream));
     return MOX_OK;
   }
-  hipLaunchKernelGGL(k_scan_sums, dim3((uint32_t)nt), dim3(SCAN_T), 0, e->stream, (const uint64_t*)a, n, sums);
-  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(SCAN_T), 0, e->stream, sums, nt, d_total);
-  hipLaunchKernelGGL(k_scan_fin, dim3((uint32_t)nt), dim3(SCAN_T), 0, e->stream, a, n, (const uint64_t*)sums);
+  const uint64_t nt = (n + SC1_TILE - 1) / SC1_TILE;
+  if (nt > 0x7FFFFFFFull) return fail(MOX_EINVAL, "scan: too many tiles");
+  hipLaunchKernelGGL(k_scan_tsum, dim3((uint32_t)nt), dim3(SC1_T), 0, e->stream, (const uint64_t*)a, n, sums);
+  const int scanned = nt > SC1_TOP ? 1 : 0;
+  if (scanned) hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(1024), 0, e->stream, sums, nt);
+  hipLaunchKernelGGL(k_scan_tile, dim3((uint32_t)nt), dim3(SC1_T), 0, e->stream, a, n, (const uint64_t*)sums, scanned, d_total);
   HIPCHK(hipGetLastError());
   return MOX_OK;
 }
@@ -601,7 +695,9 @@ void bsort_free(mox_engine* e) {
 // sorted copy lives in s_counts / s_offs / s_bytes and becomes the result.
 // Scratch (s_tmp) is engine-owned and reused across calls: about 88 bytes per
 // word plus the look-back status (6 bytes per word).
-int bsort_table(mox_engine* e) {
+// One attempt; returns -1 (nothing changed in e->res) when an eager level met
+// a tie run the unchecked mode cannot sort: the caller runs it again checked.
+int bsort_once(mox_engine* e, bool checked) {
   HIPCHK(hipSetDevice(e->device));
   auto& r = e->res;
   const uint64_t n = r.n, nb = r.nb;
@@ -617,7 +713,7 @@ int bsort_table(mox_engine* e) {
   hipStream_t st = e->stream;
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   // scratch: records A, B, subset S, payload | run flags, positions | status | gh, gs | scan sums | totals, err
-  const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8 * ((n + SCAN_TILE - 1) / SCAN_TILE + 16);
+  const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8ull * scan_sum_words(n);
   const unsigned int lrun_cap = (unsigned int)std::min<uint64_t>(1u << 20, n / 4 + 16);  // k_bs_longsort's run list
   const uint64_t need = 4 * rec + 2 * u64n + 8ull * lrun_cap + TICK_BYTES + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
   int rc;
@@ -652,41 +748,63 @@ int bsort_table(mox_engine* e) {
   BRec* R = s.a;                 // sorted (A or B)
   BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner
   // levels 1, 2, ...: runs of words sharing every compared byte, re-sorted on
-  // the next window (by run: short runs in LDS by k_bs_segsort; a subset with
-  // a longer run by the radix passes, run id as the most significant digits)
-  uint32_t run_base = 1;
-  unsigned int* longrun = s.err + 1;  // [0] fall back [1] listed long runs
+  // the next window (by run: short runs in LDS by k_bs_segsort, runs of up to
+  // RUN_LMAX by k_bs_longsort).  The first EAGER_LEVELS levels (words up to 21
+  // bytes) run with no host round trip: their kernels take the subset size and
+  // run ids from the device.  Then one read-back: the subset size of the next
+  // level and the flags.  Further levels (longer words tied on 21 bytes) read
+  // their subset size back one level at a time.  A run past RUN_LMAX (or past
+  // the long-run list) makes the whole sort run again in the checked mode, where
+  // every level reads back and such a subset is radix-sorted with the run id as
+  // the most significant digits (never seen on the benchmark corpora).
+  constexpr uint32_t EAGER_LEVELS = 2;
+  unsigned int* longrun = s.err + 1;  // [0] a run past RUN_LMAX or the list  [1] listed long runs
+  uint64_t* lvt = total;                                // lvt[level % 4]: the level's scan total (m | runs << 32)
+  uint32_t* rbs = (uint32_t*)(total + 4);               // rbs[level % 4]: the level's first run id
+  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)rbs, 1u, 1, st));  // level 0's run ids end at 1
+  uint32_t run_base = 1;  // checked mode only
   for (uint32_t level = 1;; level++) {
+    uint64_t* lt = lvt + (level & 3);
     hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin);
-    if ((rc = scan_u64(e, fin, n, total, ssum))) return rc;
-    HIPCHK(hipMemcpyAsync(h_tot, total, 8, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    if ((uint32_t)h_tot[2]) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
-    const uint64_t m = h_tot[0] & 0xFFFFFFFFull, runs = h_tot[0] >> 32;
-    if (m == 0) break;
-    if ((uint64_t)run_base + runs >= (1ull << 32)) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
-    hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin, m,
-                       run_base, r.offs, r.bytes, level, S, pos);
-    HIPCHK(hipMemsetAsync(longrun, 0, 8, st));  // [0] fall back to the radix [1] listed long runs
-    hipLaunchKernelGGL(k_bs_segsort, dim3((uint32_t)std::min<uint64_t>(4096, (m + SEG_CH - 1) / SEG_CH)), dim3(256), 0, st, S, m,
-                       longrun, lrun, longrun + 1, lrun_cap);
+    if ((rc = scan_u64(e, fin, n, lt, ssum))) return rc;
+    uint64_t m = n, runs = 0;
+    if (checked || level > EAGER_LEVELS) {
+      HIPCHK(hipMemcpyAsync(h_tot, lt, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 8, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      const uint32_t fl0 = (uint32_t)h_tot[2], fl1 = (uint32_t)(h_tot[2] >> 32);
+      if (fl0 & 1u) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
+      if (fl0 & 2u) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
+      if (fl1 && !checked) return -1;  // a long run in an eager level: run again, checked
+      m = h_tot[0] & 0xFFFFFFFFull;
+      runs = h_tot[0] >> 32;
+      if (m == 0) break;
+    }
+    hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin,
+                       (const uint64_t*)lt, (const uint32_t*)(rbs + ((level - 1) & 3)), rbs + (level & 3), longrun + 1, s.err,
+                       r.offs, r.bytes, level, S, pos);
+    hipLaunchKernelGGL(k_bs_segsort, dim3((uint32_t)std::min<uint64_t>(4096, (m + SEG_CH - 1) / SEG_CH)), dim3(256), 0, st, S,
+                       (const uint64_t*)lt, longrun, lrun, longrun + 1, lrun_cap);
     hipLaunchKernelGGL(k_bs_longsort, dim3(1024), dim3(256), 0, st, S, (const uint2*)lrun, (const unsigned int*)(longrun + 1),
                        lrun_cap);
-    HIPCHK(hipMemcpyAsync(h_tot + 3, longrun, 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
     BRec* sorted = S;
-    if ((uint32_t)h_tot[3]) {  // a run longer than SEG_MAX: the radix passes over the whole subset
-      s.a = S;
-      s.b = S2;
-      const uint64_t top = (uint64_t)run_base + runs;  // run ids < top: bytes of run id to sort on
-      const int nrb = top < (1ull << 8) ? 1 : top < (1ull << 16) ? 2 : top < (1ull << 24) ? 3 : 4;
-      if ((rc = radix_sort(e, s, m, 8 + nrb))) return rc;
-      sorted = s.a;
+    if (checked) {
+      HIPCHK(hipMemcpyAsync(h_tot + 3, longrun, 4, hipMemcpyDeviceToHost, st));
+      HIPCHK(hipStreamSynchronize(st));
+      if ((uint32_t)h_tot[3]) {  // a run past RUN_LMAX: the radix passes over the whole subset
+        HIPCHK(hipMemsetAsync(longrun, 0, 4, st));
+        s.a = S;
+        s.b = S2;
+        const uint64_t top = (uint64_t)run_base + runs;  // run ids < top: bytes of run id to sort on
+        const int nrb = top < (1ull << 8) ? 1 : top < (1ull << 16) ? 2 : top < (1ull << 24) ? 3 : 4;
+        if ((rc = radix_sort(e, s, m, 8 + nrb))) return rc;
+        sorted = s.a;
+      }
+      run_base += (uint32_t)runs;
     }
-    hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)sorted, m, (const uint64_t*)pos, R);
+    hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)sorted, (const uint64_t*)lt,
+                       (const uint64_t*)pos, R);
     HIPCHK(hipGetLastError());
-    run_base += (uint32_t)runs;
   }
   // the sorted table: counts and lengths, offsets by a scan, bytes
   uint64_t* oc = (uint64_t*)e->s_counts.p;
@@ -696,14 +814,21 @@ int bsort_table(mox_engine* e) {
   hipLaunchKernelGGL(k_bs_out2, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, r.bytes,
                      (const uint64_t*)oo, (uint8_t*)e->s_bytes.p);
   HIPCHK(hipGetLastError());
+  // complete: the callers time the sort on the host clock (ms_sort), so the
+  // output kernels above must be inside it
+  HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
+  HIPCHK(hipStreamSynchronize(st));
+  if ((uint32_t)h_tot[2] & 1u) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
   r.counts = oc;
   r.offs = oo;
   r.bytes = (const uint8_t*)e->s_bytes.p;
   r.sorted = true;
-  // complete: the callers time the sort on the host clock (ms_sort), so the
-  // output kernels above must be inside it
-  HIPCHK(hipStreamSynchronize(st));
   return MOX_OK;
+}
+
+int bsort_table(mox_engine* e) {
+  const int rc = bsort_once(e, getenv("MOX_BSORT_CHECKED") != nullptr);
+  return rc == -1 ? bsort_once(e, true) : rc;
 }
 
 }  // namespace mox_host

@@ -1050,7 +1050,9 @@ void mox_engine_destroy(mox_engine* e) {
   dfree(e->d_xcur);
   dfree(e->d_xs);
   dfree(e->d_xr);
-  if (e->h_xs) (void)hipHostFree(e->h_xs);
+  dfree(e->d_xsp);
+  if (e->h_xflag) (void)hipHostFree(e->h_xflag);
+  if (e->ev_xs) (void)hipEventDestroy(e->ev_xs);
   if (e->h_xcnt) (void)hipHostFree(e->h_xcnt);
   if (e->h_ctl_x) (void)hipHostFree(e->h_ctl_x);
   if (e->h_ctl) (void)hipHostFree(e->h_ctl);

@@ -55,6 +55,7 @@ __global__ void k_xcount(Work w, uint32_t P, XCnt* xcnt);
 __global__ void k_xpack_short(Work w, WRec* out);
 __global__ void k_xpack_long(Work w, XDir dir, unsigned long long* cur, uint8_t* blob);
 __global__ void k_xsample(Work w, uint64_t* out);
+__global__ void k_xsplit(const uint64_t* blocks, uint32_t P, uint64_t* sp, uint32_t* flag);
 __global__ void k_xcount_r(Work w, XSplit x, XCnt* xcnt);
 __global__ void k_xpack_r(Work w, XSplit x, XDir dir, unsigned long long* cur, WRec* out, uint8_t* blob);
 __global__ void k_xingest(Work w, XDir dir, uint64_t n_short);
@@ -180,9 +181,11 @@ struct mox_engine {
   XCnt* d_xcnt = nullptr;                 // [0, MAX_RANKS) sent, [MAX_RANKS, 2 MAX_RANKS) received
   XCnt* h_xcnt = nullptr;                 // pinned mirror
   unsigned long long* d_xcur = nullptr;   // 3 MAX_RANKS pack cursors
-  uint64_t* d_xs = nullptr;               // sorted exchange: MAX_RANKS x XS_SAMPLES sampled prefixes sent (one copy per peer)
+  uint64_t* d_xs = nullptr;               // sorted exchange: MAX_RANKS x XS_BLOCK sample blocks sent (one copy per peer)
   uint64_t* d_xr = nullptr;               // ... and received
-  uint64_t* h_xs = nullptr;               // pinned: every rank's samples
+  uint64_t* d_xsp = nullptr;              // MAX_RANKS splitters (k_xsplit), then the skew flag word
+  uint32_t* h_xflag = nullptr;            // pinned copy of the skew flag
+  hipEvent_t ev_xs = nullptr;             // engine group, copy transport: this member's sample block is written
   DevBuf x_send_short, x_send_blob, x_recv_short, x_recv_blob;  // device
   DevBuf hx_send, hx_recv;                // pinned host staging (host transport)
   Ctl* h_ctl_x = nullptr;                 // pinned control block of an exchange pass

@@ -30,25 +30,15 @@ constexpr int MAP_LOADERS = 1;              // loader waves
 constexpr int RING = MOX_RING;              // k_map row ring slots (LDS)
 // LDS hot dictionary: single-word slots, two choices per word (dict_s1 / dict_s2,
 // mox_kernels.hip); k_dict_pick picks up to DICT_MAX_WORDS candidates.
-// MOX_DICT12: a slot is one 16-byte LDS word, the lowered key's first 12 bytes
-// and the workgroup's u32 count of the word (words of at most 12 bytes: 99.5 %
-// of the hot words), instead of a 16-byte key plus a count in a separate array
-// (20 bytes): a third more words in the same LDS, at the same VALU cost per
-// probe (the count address is the hit slot's plus 12).
-#ifndef MOX_DICT12
-#define MOX_DICT12 0
-#endif
-constexpr bool DICT12 = MOX_DICT12 != 0;
+// (12-byte keys with the count inside the 16-byte slot held 4,620 words
+// instead of 3,660 and cut the C2 cold records 5 %, but k_map got 15-24 us
+// slower than k_reduce gained: profiles/r06/dict12_ab.txt, not kept.)
 #ifndef MOX_DICT_SLOTS
-#define MOX_DICT_SLOTS (MOX_DICT12 ? 6752 : 5120)
+#define MOX_DICT_SLOTS 5120
 #endif
 constexpr int DICT_SLOTS = MOX_DICT_SLOTS;
-#ifndef MOX_DICT_MAX_WORDS
-#define MOX_DICT_MAX_WORDS (MOX_DICT12 ? 5120 : 4096)
-#endif
-constexpr int DICT_MAX_WORDS = DICT_SLOTS < MOX_DICT_MAX_WORDS ? DICT_SLOTS : MOX_DICT_MAX_WORDS;
-constexpr uint32_t DICT_KEY_BYTES = DICT12 ? 12u : 16u;  // longest dictionary word
-constexpr size_t DICT_CNT_BYTES = DICT12 ? 0 : (size_t)DICT_SLOTS * 4;  // k_map's separate count array
+constexpr int DICT_MAX_WORDS = DICT_SLOTS < 4096 ? DICT_SLOTS : 4096;
+constexpr size_t DICT_CNT_BYTES = (size_t)DICT_SLOTS * 4;  // k_map's count array
 static_assert(DICT_SLOTS % 32 == 0 && DICT_SLOTS <= 65536 && DICT_MAX_WORDS <= DICT_SLOTS, "dictionary geometry");
 constexpr int MAX_MAP_GRID = 1024;          // map workgroups
 constexpr int MAP_WAVES = MAP_THREADS / 64;
@@ -339,18 +329,29 @@ struct XDir {
 // padded): bytewise order never decreases that prefix, so owners never decrease
 // along the sorted table.  The splitters are quantiles of sampled prefixes of
 // every rank's local table (the same on every rank).
+// The splitters are weighted quantiles of sampled prefixes of every rank's
+// local table (the same on every rank), chosen on the device (k_xsplit).  A
+// rank's sample block: XS_SAMPLES prefixes sorted ascending, then its table
+// size (the samples' weight) at XS_SAMPLES; XS_BLOCK words per block.
 constexpr uint32_t XS_SAMPLES = 1024;               // sampled prefixes per rank
+constexpr uint32_t XS_BLOCK = XS_SAMPLES + 8;       // block words: samples, table size, pad
 constexpr uint64_t XS_NONE = ~0ull;                 // sample of an empty table (no UTF-8 word starts with 0xFF)
+constexpr uint32_t XS_LDS = 16384;                  // samples k_xsplit holds (more ranks: every k-th sample)
+// Skew: one prefix value holding more than XS_SKEW_NUM / XS_SKEW_DEN of a fair
+// share (1 / P of the words) would load its rank past that: the exchange then
+// falls back to hash owners and the gathered table is sorted at the root.
+constexpr uint32_t XS_SKEW_NUM = 3, XS_SKEW_DEN = 2;
 struct XSplit {
   uint32_t P;
-  uint64_t sp[MAX_RANKS];       // sp[0 .. P-2]: ascending splitters
+  const uint64_t* sp;           // device: sp[0 .. P-2] ascending splitters (k_xsplit)
   uint64_t soff[MAX_RANKS];     // first record of destination d in the short send buffer
 };
-__host__ __device__ __forceinline__ uint32_t range_owner(const XSplit& x, uint64_t pre) {
-  uint32_t lo = 0, hi = x.P - 1;  // owner = number of splitters <= pre, in [0, P - 1]
+// owner = number of splitters <= pre, in [0, P - 1] (sp: P - 1 ascending values)
+__host__ __device__ __forceinline__ uint32_t range_owner(const uint64_t* sp, uint32_t P, uint64_t pre) {
+  uint32_t lo = 0, hi = P - 1;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (x.sp[mid] <= pre) lo = mid + 1; else hi = mid;
+    if (sp[mid] <= pre) lo = mid + 1; else hi = mid;
   }
   return lo;
 }

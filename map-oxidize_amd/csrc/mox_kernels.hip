@@ -348,9 +348,9 @@ __device__ __forceinline__ uint32_t slot_off16(uint32_t p) {
 // and the pair goes out as one aligned 32-byte sector.
 constexpr uint32_t PS_EMPTY = 0u, PS_BUSY = 1u, PS_FULL = 2u;
 struct MapLds {
-  uint4* dkey;      // DICT_SLOTS 16-byte keys (zero = empty: a real key is never zero); DICT12: 12-byte key + count
-  uint32_t* dcnt;   // DICT_SLOTS counts (DICT12: unused, the count is dkey[s].w)
-  uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's / dkey's space)
+  uint4* dkey;      // DICT_SLOTS 16-byte keys (zero = empty: a real key is never zero)
+  uint32_t* dcnt;   // DICT_SLOTS
+  uint32_t* bcnt;   // NB x qf: cold records this workgroup wrote per region (no dictionary: inside dcnt's space)
   uint32_t* misc;   // [0] spills [1] row ticket
   uint4* seltab;    // [KSEL_N]: v_perm selectors of a len-byte key at byte offset sh (entry 4 len + sh)
   uint32_t kmask;   // 0x3FC in a VGPR (key_load's v_bitop3_b32 takes no literal)
@@ -419,12 +419,7 @@ __device__ __forceinline__ KWork rare_ptr(const MapCtx& m) {
 #define rare(m) (*rare_ptr(m))
 
 __device__ __forceinline__ bool key_eq(uint4 k, uint64_t w0, uint64_t w1) {
-  if (DICT12) return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && (w1 >> 32) == 0;
   return k.x == (uint32_t)w0 && k.y == (uint32_t)(w0 >> 32) && k.z == (uint32_t)w1 && k.w == (uint32_t)(w1 >> 32);
-}
-// The LDS count of dictionary slot s (DICT12: the slot's fourth dword).
-__device__ __forceinline__ uint32_t* dict_cnt(const MapLds& s, uint32_t slot) {
-  return DICT12 ? &s.dkey[slot].w : &s.dcnt[slot];
 }
 // Exact dictionary lookup: the key's two slots.
 __device__ __forceinline__ int dict_find(const MapLds& s, uint32_t h, uint64_t w0, uint64_t w1) {
@@ -445,7 +440,7 @@ __device__ __forceinline__ void short_word(const MapCtx& m, uint64_t w0, uint64_
   if (m.dict_n && !MOX_ABL(m.w.dbg, DBG_NO_DICT)) {
     const int slot = dict_find(m.s, h, w0, w1);
     if (slot >= 0) {
-      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(dict_cnt(m.s, slot), 1u);
+      if (!MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(&m.s.dcnt[slot], 1u);
       return;
     }
   }
@@ -834,9 +829,7 @@ __device__ __forceinline__ bool key_eq4(uint4 k, const uint32_t (&K)[4]) {
   uint32_t d = k.x ^ K[0];
   d = __builtin_amdgcn_bitop3_b32(k.y, K[1], d, 0xBE);
   d = __builtin_amdgcn_bitop3_b32(k.z, K[2], d, 0xBE);
-  // DICT12: the slot's fourth dword is its count; a token longer than 12
-  // bytes (K[3] != 0) matches no slot
-  d = DICT12 ? (d | K[3]) : __builtin_amdgcn_bitop3_b32(k.w, K[3], d, 0xBE);
+  d = __builtin_amdgcn_bitop3_b32(k.w, K[3], d, 0xBE);
   return d == 0;
 }
 
@@ -891,15 +884,11 @@ __device__ __forceinline__ void pass_a(const MapCtx& m, const uint8_t* rowbuf, c
     nvalid += (uint32_t)__popcll(__ballot(valid));
     const bool hit1 = key_eq4(d1[u], K[u]), hit2 = key_eq4(d2[u], K[u]);
     miss[u] = valid & !(hit1 | hit2);
-    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) {
-      if (DICT12) atomicAdd(lds_ptr<uint32_t>(L_DKEY + 12u + (hit1 ? s1[u] : s2[u])), 1u);
-      else atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
-    }
+    if (valid & (hit1 | hit2) && !MOX_ABL(m.w.dbg, DBG_NO_DICTADD)) atomicAdd(lds_ptr<uint32_t>(L_DCNT + ((hit1 ? s1[u] : s2[u]) >> 2)), 1u);
 #if defined(MOX_PATHS) && MOX_PATHS
     if (miss[u]) {
-      const uint32_t w1 = DICT12 ? 0u : d1[u].w, w2 = DICT12 ? 0u : d2[u].w;
-      if ((d1[u].x | d1[u].y | d1[u].z | w1) && hash32(d1[u].x, d1[u].y, d1[u].z, w1) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
-      if ((d2[u].x | d2[u].y | d2[u].z | w2) && hash32(d2[u].x, d2[u].y, d2[u].z, w2) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
+      if ((d1[u].x | d1[u].y | d1[u].z | d1[u].w) && hash32(d1[u].x, d1[u].y, d1[u].z, d1[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
+      if ((d2[u].x | d2[u].y | d2[u].z | d2[u].w) && hash32(d2[u].x, d2[u].y, d2[u].z, d2[u].w) == h[u]) MOX_PATH(rare(m).ctl, PATH_DICT_SAMEHASH);
     }
 #endif
   }
@@ -1202,8 +1191,8 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   uint16_t* lists = lds_ptr<uint16_t>(L_LISTS);
   m.s.pend = m.s.dkey;                                        // no dictionary only: dkey is all zero
   m.s.pst = reinterpret_cast<uint32_t*>(m.s.dkey + NB * QF_MAX);  // = PS_EMPTY
-  static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 + (DICT12 ? NB * QF_MAX * 4 : 0) <= DICT_SLOTS * 16, "pair slots inside dkey");
-  static_assert(DICT12 || NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
+  static_assert(NB * QF_MAX * 16 + NB * QF_MAX * 4 <= DICT_SLOTS * 16, "pair slots inside dkey");
+  static_assert(NB * QF_MAX <= DICT_SLOTS, "region counters inside dcnt");
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   m.dict_n = w.dict_hist[DH_N];
   if (MOX_ABL(w.dbg, DBG_NO_DICT)) m.dict_n = 0;
@@ -1212,12 +1201,12 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   m.rg = w.map_grid * m.qf;
   m.rc = w.cold_cap / m.qf;
   m.wcold = w.cold + (uint64_t)blockIdx.x * m.qf * NB * m.rc;
-  if (!m.dict_n) m.s.bcnt = DICT12 ? m.s.pst + NB * QF_MAX : m.s.dcnt;  // NB x qf region counters
+  if (!m.dict_n) m.s.bcnt = m.s.dcnt;  // NB x qf region counters
   // without a dictionary the key array is zero (no real key is zero, so nothing
   // would hit; that case takes pass_c, and the pair slots live there)
   for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
-    m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);  // (DICT12: the image's count dword is 0)
-    if (!DICT12) m.s.dcnt[i] = 0;
+    m.s.dkey[i] = m.dict_n ? w.dict_key[i] : make_uint4(0, 0, 0, 0);
+    m.s.dcnt[i] = 0;
   }
   __syncthreads();  // (no dictionary: the region counters live in dcnt's space)
   for (uint32_t i = tid; i < NB * m.qf; i += MAP_THREADS) {
@@ -1373,7 +1362,7 @@ extern "C" __global__ __launch_bounds__(MAP_THREADS, MAP_MIN_WAVES) void k_map(C
   }
   if (m.dict_n) {
     for (int i = tid; i < DICT_SLOTS; i += MAP_THREADS) {
-      const uint32_t cnt = *dict_cnt(m.s, i);
+      const uint32_t cnt = m.s.dcnt[i];
       if (cnt) atomicAdd(&w.dict_tot[i], (unsigned long long)cnt);
     }
   }
@@ -1598,7 +1587,6 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_hist(Work w) {
   __syncthreads();
   for (uint32_t i = blockIdx.x * 1024 + threadIdx.x; i < GC_SLOTS; i += gridDim.x * 1024) {
     const uint64_t n = w.cand[i].count;
-    if (DICT12 && ((w.cand[i].w1 & ~(1ull << 63)) >> 32) != 0) continue;  // over 12 bytes: never picked (k_dict_pick)
     if (n) atomicAdd(&h[n > 255 ? 255 : n], 1u);
   }
   __syncthreads();
@@ -1657,9 +1645,7 @@ extern "C" __global__ __launch_bounds__(1024) void k_dict_pick(Work w, uint32_t 
   const uint32_t t = T, t1 = T - 1;
   const uint32_t i = blockIdx.x * 1024 + threadIdx.x;
   const WRec r = w.cand[i];
-  // (DICT12: words over 12 bytes never enter the dictionary: w1's high half is
-  // zero below the claim marker bit)
-  const bool real = r.w0 != 0 && r.w1 != 0 && (!DICT12 || ((r.w1 & ~(1ull << 63)) >> 32) == 0);
+  const bool real = r.w0 != 0 && r.w1 != 0;
   const bool pick = real && r.count >= t;
   const bool fill = real && t1 >= 2 && t1 < 255 && r.count == t1;
   const uint64_t bm = __ballot(pick), bf = __ballot(fill);
@@ -4229,13 +4215,82 @@ __device__ __forceinline__ uint64_t row_prefix(const Work& w, uint64_t i) {
   for (uint32_t j = 0; j < 8 && j < len; j++) k |= (uint64_t)w.t_bytes[o + j] << (56 - 8 * j);
   return k;
 }
-// XS_SAMPLES prefixes of this rank's local table, evenly over its rows (the
-// table is in hash order, so they are a uniform sample of its distinct words);
-// XS_NONE for an empty table.
-extern "C" __global__ void k_xsample(Work w, uint64_t* out) {
+// This rank's sample block (XS_BLOCK words at out): XS_SAMPLES prefixes of its
+// local table, evenly over its rows (the table is in hash order, so they are a
+// uniform sample of its distinct words; XS_NONE for an empty table), sorted
+// ascending by a bitonic sort in LDS, then the table size (their weight).
+// One workgroup of XS_SAMPLES threads.
+extern "C" __global__ __launch_bounds__(XS_SAMPLES) void k_xsample(Work w, uint64_t* out) {
+  __shared__ uint64_t v[XS_SAMPLES];
+  const uint32_t t = threadIdx.x;
   const uint64_t n = w.ctl->n_total;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < XS_SAMPLES; j += gridDim.x * blockDim.x)
-    out[j] = n ? row_prefix(w, (uint64_t)j * n / XS_SAMPLES) : XS_NONE;
+  v[t] = n ? row_prefix(w, (uint64_t)t * n / XS_SAMPLES) : XS_NONE;
+  __syncthreads();
+  for (uint32_t k = 2; k <= XS_SAMPLES; k <<= 1)
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      const uint32_t l = t ^ j;
+      uint64_t a = 0, b = 0;
+      const bool act = l > t;
+      if (act) { a = v[t]; b = v[l]; }
+      __syncthreads();
+      if (act && ((a > b) == ((t & k) == 0))) { v[t] = b; v[l] = a; }
+      __syncthreads();
+    }
+  out[t] = v[t];
+  if (t < XS_BLOCK - XS_SAMPLES) out[XS_SAMPLES + t] = t == 0 ? n : 0ull;
+}
+
+// Splitters of the sorted exchange from every rank's sample block (blocks:
+// P x XS_BLOCK words, the same on every rank), on the device: no host round
+// trip between the sample all-to-all and the counts.  Rank q's samples weigh
+// n_q (its table size) each, so a rank with more words takes more of the
+// ranges (equal weights let a small shard's samples set half the splitters).
+// A value v's weighted rank interval is (lo(v), hi(v)] with lo = sum_q n_q
+// #(samples of q < v) and hi with <=; splitter k (1 <= k < P) is the value whose
+// interval holds t_k = k W / P, W = sum_q n_q S (S samples per rank): every
+// candidate sample checks every k, and equal values write the same splitter.
+// With more than XS_LDS samples in all, every (S_all / S)-th sample of each
+// (sorted) block is used.  flag = 1 when one value's interval is wider than
+// XS_SKEW_NUM / XS_SKEW_DEN fair shares (skewed prefixes: the host falls back
+// to hash owners).  One workgroup of 1024 threads.
+extern "C" __global__ __launch_bounds__(1024) void k_xsplit(const uint64_t* blocks, uint32_t P, uint64_t* sp, uint32_t* flag) {
+  __shared__ uint64_t v[XS_LDS];
+  __shared__ uint64_t wq[MAX_RANKS];
+  const uint32_t t = threadIdx.x;
+  const uint32_t S = XS_SAMPLES * P <= XS_LDS ? XS_SAMPLES : XS_LDS / P;  // samples per rank used (a power of two)
+  const uint32_t stride = XS_SAMPLES / S;
+  if (t < P) wq[t] = blocks[(uint64_t)t * XS_BLOCK + XS_SAMPLES];
+  if (t + 1 < P) sp[t] = 0;
+  if (t == 0) *flag = 0;
+  for (uint32_t i = t; i < S * P; i += 1024) {
+    const uint32_t q = i / S, j = i % S;
+    v[i] = blocks[(uint64_t)q * XS_BLOCK + (uint64_t)j * stride];
+  }
+  __syncthreads();
+  uint64_t W = 0;
+  for (uint32_t q = 0; q < P; q++) W += wq[q] * S;
+  if (W == 0) return;
+  for (uint32_t i = t; i < S * P; i += 1024) {
+    const uint64_t x = v[i];
+    if (x == XS_NONE) continue;  // an empty table's samples (weight 0)
+    uint64_t lo = 0, hi = 0;
+    for (uint32_t q = 0; q < P; q++) {
+      if (!wq[q]) continue;
+      const uint64_t* b = v + (uint64_t)q * S;
+      uint32_t a = 0, z = S;  // lower bound: first sample >= x
+      while (a < z) { const uint32_t m = (a + z) >> 1; if (b[m] < x) a = m + 1; else z = m; }
+      uint32_t a2 = a, z2 = S;  // upper bound: first sample > x
+      while (a2 < z2) { const uint32_t m = (a2 + z2) >> 1; if (b[m] <= x) a2 = m + 1; else z2 = m; }
+      lo += wq[q] * a;
+      hi += wq[q] * a2;
+    }
+    for (uint32_t k = 1; k < P; k++) {
+      const uint64_t tk = (uint64_t)k * W / P;  // (W <= 2^48: table rows < 2^32, S <= 2^10, P <= 2^6)
+      if (lo < tk && tk <= hi) sp[k - 1] = x;
+    }
+    // skew: this value alone is more than XS_SKEW_NUM / XS_SKEW_DEN of W / P
+    if (P > 1 && (hi - lo) * P * XS_SKEW_DEN > W * XS_SKEW_NUM) *flag = 1;
+  }
 }
 // Rows of the local table per block: a contiguous chunk each
 constexpr uint32_t XR_THREADS = 256;
@@ -4250,14 +4305,16 @@ __device__ __forceinline__ void xr_chunk(uint64_t n, uint64_t& r0, uint64_t& r1)
 // global atomic per (workgroup, destination) for the short words.
 extern "C" __global__ __launch_bounds__(XR_THREADS) void k_xcount_r(Work w, XSplit x, XCnt* xcnt) {
   __shared__ uint32_t lc[MAX_RANKS];
+  __shared__ uint64_t sp[MAX_RANKS];
   const uint32_t t = threadIdx.x;
   if (t < MAX_RANKS) lc[t] = 0;
+  if (t + 1 < x.P) sp[t] = x.sp[t];
   __syncthreads();
   const uint64_t ns = w.ctl->n_short, n = w.ctl->n_total;
   uint64_t r0, r1;
   xr_chunk(n, r0, r1);
   for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) {
-    const uint32_t d = range_owner(x, row_prefix(w, i));
+    const uint32_t d = range_owner(sp, x.P, row_prefix(w, i));
     if (i < ns) {
       atomicAdd(&lc[d], 1u);
     } else {
@@ -4279,13 +4336,15 @@ extern "C" __global__ __launch_bounds__(XR_THREADS) void k_xpack_r(Work w, XSpli
                                                                  WRec* out, uint8_t* blob) {
   __shared__ uint32_t lc[MAX_RANKS];
   __shared__ unsigned long long lb[MAX_RANKS];
+  __shared__ uint64_t sp[MAX_RANKS];
   const uint32_t t = threadIdx.x, P = x.P;
   if (t < MAX_RANKS) lc[t] = 0;
+  if (t + 1 < P) sp[t] = x.sp[t];
   __syncthreads();
   const uint64_t ns = w.ctl->n_short, n = w.ctl->n_total;
   uint64_t r0, r1;
   xr_chunk(ns, r0, r1);  // short rows: counted, then written at the reserved ranges
-  for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) atomicAdd(&lc[range_owner(x, row_prefix(w, i))], 1u);
+  for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) atomicAdd(&lc[range_owner(sp, P, row_prefix(w, i))], 1u);
   __syncthreads();
   if (t < P) {
     lb[t] = lc[t] ? x.soff[t] + atomicAdd(&cur[t], (unsigned long long)lc[t]) : 0ull;
@@ -4300,14 +4359,14 @@ extern "C" __global__ __launch_bounds__(XR_THREADS) void k_xpack_r(Work w, XSpli
       if (j < 8) k0 |= b << (8 * j); else k1 |= b << (8 * (j - 8));
     }
     const uint64_t pre = __builtin_bswap64(k0);
-    const uint32_t d = range_owner(x, pre);
+    const uint32_t d = range_owner(sp, P, pre);
     const uint32_t r = atomicAdd(&lc[d], 1u);
     out[lb[d] + r] = WRec{k0, k1, w.t_counts[i]};
   }
   // long words (rare): one global atomic per word and cursor
   for (uint64_t i = ns + (uint64_t)blockIdx.x * XR_THREADS + t; i < n; i += (uint64_t)gridDim.x * XR_THREADS) {
     const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;
-    const uint32_t d = range_owner(x, row_prefix(w, i));
+    const uint32_t d = range_owner(sp, P, row_prefix(w, i));
     uint64_t h = FNV0;
     for (uint64_t j = 0; j < len; j++) h = fnv_step(h, w.t_bytes[o + j]);
     h = fnv_finish(h);

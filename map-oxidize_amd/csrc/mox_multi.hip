@@ -216,9 +216,10 @@ int x_alloc(mox_engine* e) {
 }
 
 // Phase 1: k_xcount into the device send rows d_xcnt[0, P).  Sorted exchange
-// (MOX_F_SORT_BYTES): k_xsample instead, into d_xs (one copy per peer); the
-// caller moves every rank's samples to every rank and calls x_split, which
-// picks the splitters and runs k_xcount_r.
+// (MOX_F_SORT_BYTES): k_xsample instead, this rank's sorted sample block into
+// d_xs (one copy per peer); the caller moves every rank's block to every rank
+// (d_xr) and calls x_split, which picks the splitters on the device and runs
+// k_xcount_r.
 int x_begin(mox_engine* e, int P) {
   if (int rc = drain_async(e)) return rc;
   if (!e->have_result || !e->res.pass) return fail(MOX_ESTATE, "no local result: mox_run_range first");
@@ -233,12 +234,15 @@ int x_begin(mox_engine* e, int P) {
   HIPCHK(hipMemsetAsync(e->d_xcnt, 0, P * sizeof(XCnt), e->stream));
   if (x.ranged) {
     int rc;
-    constexpr size_t SB = (size_t)MAX_RANKS * XS_SAMPLES * 8;
-    if (!e->d_xs && ((rc = dalloc(e, (void**)&e->d_xs, SB)) || (rc = dalloc(e, (void**)&e->d_xr, SB)))) return rc;
-    if (!e->h_xs) HIPCHK(hipHostMalloc((void**)&e->h_xs, SB, hipHostMallocDefault));
-    hipLaunchKernelGGL(k_xsample, dim3(4), dim3(256), 0, e->stream, e->w, e->d_xs);
+    constexpr size_t SB = (size_t)MAX_RANKS * XS_BLOCK * 8;
+    if (!e->d_xs && ((rc = dalloc(e, (void**)&e->d_xs, SB)) || (rc = dalloc(e, (void**)&e->d_xr, SB)) ||
+                     (rc = dalloc(e, (void**)&e->d_xsp, MAX_RANKS * 8 + 64))))
+      return rc;
+    if (!e->h_xflag) HIPCHK(hipHostMalloc((void**)&e->h_xflag, 64, hipHostMallocDefault));
+    if (!e->ev_xs) HIPCHK(hipEventCreateWithFlags(&e->ev_xs, hipEventDisableTiming));
+    hipLaunchKernelGGL(k_xsample, dim3(1), dim3(XS_SAMPLES), 0, e->stream, e->w, e->d_xs);
     for (int d = 1; d < P; d++)
-      HIPCHK(hipMemcpyAsync(e->d_xs + (size_t)d * XS_SAMPLES, e->d_xs, XS_SAMPLES * 8, hipMemcpyDeviceToDevice, e->stream));
+      HIPCHK(hipMemcpyAsync(e->d_xs + (size_t)d * XS_BLOCK, e->d_xs, XS_BLOCK * 8, hipMemcpyDeviceToDevice, e->stream));
   } else {
     hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, e->stream, e->w, (uint32_t)P, e->d_xcnt);
   }
@@ -246,21 +250,34 @@ int x_begin(mox_engine* e, int P) {
   return MOX_OK;
 }
 
-// Sorted exchange: splitters from every rank's samples (all[0, m), the same
-// on every rank, so every rank picks the same ones): P - 1 quantiles of the
-// valid samples; then the per-destination counts by range owner (k_xcount_r).
-int x_split(mox_engine* e, const uint64_t* all, size_t m) {
+// Sorted exchange, after every rank's sample block is in d_xr (the same on
+// every rank, so every rank picks the same splitters): the weighted splitters
+// on the device (k_xsplit), the per-destination counts by range owner
+// (k_xcount_r), and the skew flag copied to the host behind them (read after
+// the counts all-to-all's synchronisation: no round trip of its own).
+int x_split(mox_engine* e) {
   HIPCHK(hipSetDevice(e->device));
   XPlan& x = *e->xp;
-  std::vector<uint64_t> v;
-  v.reserve(m);
-  for (size_t i = 0; i < m; i++)
-    if (all[i] != XS_NONE) v.push_back(all[i]);
-  std::sort(v.begin(), v.end());
+  uint32_t* d_flag = reinterpret_cast<uint32_t*>(e->d_xsp + MAX_RANKS);
+  hipLaunchKernelGGL(k_xsplit, dim3(1), dim3(1024), 0, e->stream, (const uint64_t*)e->d_xr, (uint32_t)x.P, e->d_xsp, d_flag);
   x.split = XSplit{};
   x.split.P = (uint32_t)x.P;
-  for (int i = 0; i + 1 < x.P; i++) x.split.sp[i] = v.empty() ? 0 : v[(size_t)(i + 1) * v.size() / x.P];
+  x.split.sp = e->d_xsp;
   hipLaunchKernelGGL(k_xcount_r, dim3(1024), dim3(256), 0, e->stream, e->w, x.split, e->d_xcnt);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(e->h_xflag, d_flag, 4, hipMemcpyDeviceToHost, e->stream));
+  return MOX_OK;
+}
+
+// Skewed prefixes (k_xsplit's flag: one 8-byte prefix holds several ranks'
+// shares): this exchange falls back to hash owners (the gathered table is then
+// sorted at the root, as an unsorted one is).  Every rank reads the same flag.
+int x_unrange(mox_engine* e) {
+  HIPCHK(hipSetDevice(e->device));
+  XPlan& x = *e->xp;
+  x.ranged = false;
+  HIPCHK(hipMemsetAsync(e->d_xcnt, 0, x.P * sizeof(XCnt), e->stream));
+  hipLaunchKernelGGL(k_xcount, dim3(64), dim3(256), 0, e->stream, e->w, (uint32_t)x.P, e->d_xcnt);
   HIPCHK(hipGetLastError());
   return MOX_OK;
 }
@@ -346,8 +363,8 @@ int x_reduce(mox_engine* e) {
   HIPCHK(hipSetDevice(e->device));
   const XPlan& x = *e->xp;
   if (int rc = reduce_received(e, x.rs, x.rb, x.r_long, x.rdir, x.local, x.t0)) return rc;
-  e->stats.x_bytes_sent = x.ns * sizeof(WRec) + x.sb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_SAMPLES * 8 : 0);
-  e->stats.x_bytes_recv = x.rs * sizeof(WRec) + x.rb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_SAMPLES * 8 : 0);
+  e->stats.x_bytes_sent = x.ns * sizeof(WRec) + x.sb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_BLOCK * 8 : 0);
+  e->stats.x_bytes_recv = x.rs * sizeof(WRec) + x.rb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_BLOCK * 8 : 0);
   e->res.exchanged = true;
   if (x.ranged) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -362,18 +379,20 @@ int exchange_impl(mox_engine* e, int P, int me, Transport& T) {
   (void)me;
   int rc;
   if ((rc = x_begin(e, P))) return rc;
-  if (e->xp->ranged) {  // every rank's samples to every rank
+  if (e->xp->ranged) {  // every rank's sample block to every rank, then the splitters on the device
     uint64_t off[MAX_RANKS], len[MAX_RANKS];
     for (int d = 0; d < P; d++) {
-      off[d] = (uint64_t)d * XS_SAMPLES * 8;
-      len[d] = XS_SAMPLES * 8;
+      off[d] = (uint64_t)d * XS_BLOCK * 8;
+      len[d] = XS_BLOCK * 8;
     }
     if ((rc = T.alltoallv((const uint8_t*)e->d_xs, off, len, (uint8_t*)e->d_xr, off, len))) return rc;
-    HIPCHK(hipMemcpyAsync(e->h_xs, e->d_xr, (size_t)P * XS_SAMPLES * 8, hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(hipStreamSynchronize(e->stream));
-    if ((rc = x_split(e, e->h_xs, (size_t)P * XS_SAMPLES))) return rc;
+    if ((rc = x_split(e))) return rc;
   }
   if ((rc = T.counts(e->d_xcnt, e->d_xcnt + MAX_RANKS, e->h_xcnt, e->h_xcnt + MAX_RANKS))) return rc;
+  if (e->xp->ranged && *e->h_xflag) {  // skewed prefixes: hash owners (the same decision on every rank)
+    if ((rc = x_unrange(e))) return rc;
+    if ((rc = T.counts(e->d_xcnt, e->d_xcnt + MAX_RANKS, e->h_xcnt, e->h_xcnt + MAX_RANKS))) return rc;
+  }
   if ((rc = x_pack(e))) return rc;
   const XPlan& x = *e->xp;
   if ((rc = T.alltoallv_pair((const uint8_t*)e->x_send_short.p, x.s_short_off, x.s_short_len, (uint8_t*)e->x_recv_short.p,
@@ -622,6 +641,41 @@ int group_counts(Group& G) {
   return MOX_OK;
 }
 
+// Sorted exchange, the whole group: member i's sample block (d_xs) into every
+// member's d_xr block i, device to device with no host synchronisation (RCCL
+// send / recv in one group, or peer copies ordered after the sender's
+// k_xsample by an event).
+int group_samples(Group& G) {
+  const int P = G.n;
+  constexpr size_t BB = XS_BLOCK * 8;
+  if (G.xport == MOX_XPORT_RCCL) {
+    RCCLCHK(ncclGroupStart());
+    for (int i = 0; i < P; i++) {
+      mox_engine* e = G.m[i];
+      for (int p = 0; p < P; p++) {
+        RCCLCHK(ncclSend(e->d_xs + (size_t)p * XS_BLOCK, BB, ncclUint8, p, G.comms[i], e->stream));
+        RCCLCHK(ncclRecv(e->d_xr + (size_t)p * XS_BLOCK, BB, ncclUint8, p, G.comms[i], e->stream));
+      }
+    }
+    RCCLCHK(ncclGroupEnd());
+    return MOX_OK;
+  }
+  for (int i = 0; i < P; i++) {
+    HIPCHK(hipSetDevice(G.m[i]->device));
+    HIPCHK(hipEventRecord(G.m[i]->ev_xs, G.m[i]->stream));
+  }
+  for (int j = 0; j < P; j++) {
+    mox_engine* r = G.m[j];
+    HIPCHK(hipSetDevice(r->device));
+    for (int i = 0; i < P; i++) {
+      const mox_engine* snd = G.m[i];
+      HIPCHK(hipStreamWaitEvent(r->stream, snd->ev_xs, 0));
+      HIPCHK(hipMemcpyPeerAsync(r->d_xr + (size_t)i * XS_BLOCK, r->device, snd->d_xs, snd->device, BB, r->stream));
+    }
+  }
+  return MOX_OK;
+}
+
 // Phase 2' of the exchange for the whole group: both payloads.
 int group_payloads(Group& G) {
   const int P = G.n;
@@ -680,18 +734,17 @@ int group_exchange(Group& G) {
   const int P = G.n;
   for (int i = 0; i < P; i++)
     if (int rc = x_begin(G.m[i], P)) return rc;
-  if (G.m[0]->xp->ranged) {  // sorted exchange: every member's samples, read by the host, give every member's splitters
-    std::vector<uint64_t> all((size_t)P * XS_SAMPLES);
-    for (int i = 0; i < P; i++) {
-      HIPCHK(hipSetDevice(G.m[i]->device));
-      HIPCHK(hipMemcpyAsync(G.m[i]->h_xs, G.m[i]->d_xs, XS_SAMPLES * 8, hipMemcpyDeviceToHost, G.m[i]->stream));
-    }
-    if (int rc = sync_members(G)) return rc;
-    for (int i = 0; i < P; i++) std::memcpy(all.data() + (size_t)i * XS_SAMPLES, G.m[i]->h_xs, XS_SAMPLES * 8);
+  if (G.m[0]->xp->ranged) {  // sorted exchange: every member's sample block to every member, splitters on each GPU
+    if (int rc = group_samples(G)) return rc;
     for (int i = 0; i < P; i++)
-      if (int rc = x_split(G.m[i], all.data(), all.size())) return rc;
+      if (int rc = x_split(G.m[i])) return rc;
   }
   if (int rc = group_counts(G)) return rc;
+  if (G.m[0]->xp->ranged && *G.m[0]->h_xflag) {  // skewed prefixes: hash owners on every member
+    for (int i = 0; i < P; i++)
+      if (int rc = x_unrange(G.m[i])) return rc;
+    if (int rc = group_counts(G)) return rc;
+  }
   for (int i = 0; i < P; i++)
     if (int rc = x_pack(G.m[i])) return rc;
   if (int rc = group_payloads(G)) return rc;

@@ -343,3 +343,43 @@ def test_sorted_exchange_c3_path_world8():
     want, wtok = coracle.count(data, nthreads=16)
     assert out[0][1] == wtok
     assert out[0][0] == want
+
+
+def test_sorted_exchange_weights_ranks_by_table_size():
+    """Splitters weighted by every rank's table size (k_xsplit): rank 0's shard
+    holds ~all distinct words (random tokens), the other ranks' shards a few
+    hundred repeated words.  With equal sample weights two thirds of the
+    samples would come from the small tables and most of rank 0's words would
+    land on one rank; weighted, the ranks' final tables stay near an even
+    share -- and the gathered table is still the oracle's sorted list."""
+    world = 3
+    third = 4 << 20
+    h = corpus.fill(corpus.HICARD, 71, 0, third).tobytes()
+    few = b" ".join(b"w%03d" % (i % 300) for i in range(third // 5))[:third]
+    data = h + b" " + few + b" " + few
+    want, wtok = coracle.count(data)
+    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, table_order=True)
+    sizes = [len(items) for items, _ in out]
+    assert [x for items, _ in out for x in items] == want  # still sorted ranges in rank order
+    assert max(sizes) <= 2.2 * (sum(sizes) / world), sizes
+    out = run_ranks(data, world, gather_root=0, flags=mox.MOX_F_SORT_BYTES, table_order=True)
+    assert out[0] == (want, wtok)
+
+
+def test_sorted_exchange_skewed_prefixes_fall_back():
+    """words that share their first 8 bytes (URL-like) cannot be
+    split by 8-byte prefix splitters: one rank would receive and sort nearly the
+    whole table.  k_xsplit flags the skew and every rank falls back to hash
+    owners (the ranks' tables are then in engine order), and the gathered,
+    fetched table is still the oracle's sorted list."""
+    world = 3
+    rng = __import__("random").Random(5)
+    words = [b"https://www.example.org/" + bytes(rng.choice(b"abcdefghij") for _ in range(rng.randint(3, 9)))
+             for _ in range(150000)]  # ~78 % of the distinct words share "https://"
+    data = b" ".join(words) + b" " + corpus.fill(corpus.ZIPF, 72, 0, 1 << 20).tobytes()
+    want, wtok = coracle.count(data)
+    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, table_order=True)
+    assert sorted(x for items, _ in out for x in items) == want
+    assert any([w for w, _ in items] != sorted(w for w, _ in items) for items, _ in out)  # hash owners: engine order
+    out = run_ranks(data, world, gather_root=0, flags=mox.MOX_F_SORT_BYTES)
+    assert out[0] == (want, wtok)

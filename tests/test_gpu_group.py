@@ -176,11 +176,39 @@ def tricky_words(rng):
     return sorted(words)
 
 
-def test_device_sort_tie_levels():
+@pytest.mark.parametrize("checked", [False, True])
+def test_device_sort_tie_levels(monkeypatch, checked):
     """mox_reduce_pairs table (words taken verbatim) sorted on the GPU: the
-    order equals Python's bytes order, through several 16-byte tie levels."""
+    order equals Python's bytes order, through several 16-byte tie levels --
+    with the first tie levels run without a host round trip (default) and with
+    every level read back (MOX_BSORT_CHECKED, the mode a run past RUN_LMAX falls
+    back to)."""
+    if checked:
+        monkeypatch.setenv("MOX_BSORT_CHECKED", "1")
     rng = random.Random(99)
     words = tricky_words(rng)
+    shuffled = words[:]
+    rng.shuffle(shuffled)
+    e = mox.Engine(device=0, flags=mox.MOX_F_SORT_BYTES)
+    try:
+        t = e.reduce_pairs(shuffled, list(range(1, len(shuffled) + 1)))
+        got = list(t.items())
+        t.close()
+    finally:
+        e.close()
+    assert [w for w, _ in got] == words
+    cnt = dict(zip(shuffled, range(1, len(shuffled) + 1)))
+    assert all(cnt[w] == c for w, c in got)
+
+
+def test_device_sort_run_past_the_segment_sort():
+    """6,000 words sharing a 20-byte prefix: one tie run longer than k_bs_segsort
+    / k_bs_longsort take (RUN_LMAX), met in a level that runs without a host
+    round trip; the sort runs again in the checked mode (radix passes over the
+    subset) and the order still equals Python's bytes order."""
+    rng = random.Random(7)
+    words = sorted({b"x" * 20 + bytes(rng.choice(b"abcdefgh") for _ in range(rng.randint(1, 12))) for _ in range(9000)})
+    assert len(words) > 4096
     shuffled = words[:]
     rng.shuffle(shuffled)
     e = mox.Engine(device=0, flags=mox.MOX_F_SORT_BYTES)

@@ -16,6 +16,9 @@
 #   ab       interleaved per-kernel A/B of build variants: AB_VARS="v1 v2 v1 v2"
 #            AB_KERNELS="k_map" [AB_DBG="0"] [AB_ARGS="--workload C4 ..."]
 #   abe      interleaved end-to-end bench A/B of variants: AB_VARS, AB_ARGS
+#   sort     the device bytewise sort's GPU tests (group, exchange)
+#   xsort    the exchange and engine-group GPU tests (not slow)
+#   c2       the C2 bench line without the CPU baseline (value, k_map, sorted-result line)
 #   varpar   a build variant (VAR=name: build/var_name) through the parity subset and the
 #            full-size C2 async parity test
 #   pmc      k_map FETCH/WRITE traffic at C2 and SQ counters of k_map
@@ -81,6 +84,18 @@ abe)
     rc=$?; [ $rc -eq 0 ] || { tail -3 $f.err; step "abe $spec" $rc; }
     python3 -c "import json,sys;d=json.loads(open('$f.json').read().strip().splitlines()[-1]);print('$spec', d['value'], d['roofline']['avg_launch_ms'], d['stats']['cold_records'], d['stats']['dict_words'])"
   done
+  ;;
+sort)
+  # the device bytewise sort: its own tests, the sorted exchange, the group's sorted table
+  pyt sort.log 600 tests/test_gpu_group.py tests/test_gpu_exchange.py -m "gpu and not slow" -k "sort"
+  ;;
+xsort)
+  # the exchange and engine-group tests (sorted exchange, device splitters, device sort)
+  pyt xsort.log 900 tests/test_gpu_exchange.py tests/test_gpu_group.py -m "gpu and not slow"
+  ;;
+c2)
+  timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err; step "bench C2" $?
+  python3 -c "import json;d=json.loads(open('$O/bench_c2.json').read().strip().splitlines()[-1]);print(d['value'], d['roofline']['avg_launch_ms'], d['sorted_result'])"
   ;;
 varpar)
   # a build variant (build/var_$VAR) through the parity subset and the full-size
