@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MOX_ABI_VERSION 3
+#define MOX_ABI_VERSION 4
 
 /* status codes */
 #define MOX_OK 0
@@ -157,6 +157,9 @@ typedef struct mox_stats {
   double ms_local;         /* engine group: local passes of all members (wall time) */
   uint32_t n_gpus;         /* engine group size (1 for a single-GPU engine) */
   uint32_t async_dropped;  /* overflowed async passes superseded by a later queued pass (never re-run) */
+  uint32_t x_ranged;       /* the last exchange owned words by byte range (MOX_F_SORT_BYTES); 0: by hash
+                              (no sort flag, or skewed 8-byte prefixes fell back to hash owners) */
+  uint32_t x_pad;
 } mox_stats;
 
 const char* mox_last_error(void);

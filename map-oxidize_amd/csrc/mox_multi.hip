@@ -366,6 +366,7 @@ int x_reduce(mox_engine* e) {
   e->stats.x_bytes_sent = x.ns * sizeof(WRec) + x.sb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_BLOCK * 8 : 0);
   e->stats.x_bytes_recv = x.rs * sizeof(WRec) + x.rb + x.P * sizeof(XCnt) + (x.ranged ? x.P * XS_BLOCK * 8 : 0);
   e->res.exchanged = true;
+  e->stats.x_ranged = x.ranged ? 1u : 0u;
   if (x.ranged) {
     const auto t0 = std::chrono::steady_clock::now();
     const int rc = bsort_table(e);

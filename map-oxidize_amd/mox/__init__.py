@@ -120,6 +120,8 @@ class Stats(ctypes.Structure):
         ("ms_local", ctypes.c_double),
         ("n_gpus", ctypes.c_uint32),
         ("async_dropped", ctypes.c_uint32),
+        ("x_ranged", ctypes.c_uint32),
+        ("x_pad", ctypes.c_uint32),
     ]
 
     def as_dict(self):

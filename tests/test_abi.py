@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert mox.lib().mox_abi_version() == 3
+    assert mox.lib().mox_abi_version() == 4
 
 
 def test_no_cpu_fallback_without_gpu():

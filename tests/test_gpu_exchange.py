@@ -358,9 +358,11 @@ def test_sorted_exchange_weights_ranks_by_table_size():
     few = b" ".join(b"w%03d" % (i % 300) for i in range(third // 5))[:third]
     data = h + b" " + few + b" " + few
     want, wtok = coracle.count(data)
-    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, table_order=True)
+    stats = []
+    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, table_order=True, stats=stats)
     sizes = [len(items) for items, _ in out]
     assert [x for items, _ in out for x in items] == want  # still sorted ranges in rank order
+    assert all(st["x_ranged"] == 1 for st in stats)  # the sorted exchange ran (no skew fallback)
     assert max(sizes) <= 2.2 * (sum(sizes) / world), sizes
     out = run_ranks(data, world, gather_root=0, flags=mox.MOX_F_SORT_BYTES, table_order=True)
     assert out[0] == (want, wtok)
@@ -378,8 +380,9 @@ def test_sorted_exchange_skewed_prefixes_fall_back():
              for _ in range(150000)]  # ~78 % of the distinct words share "https://"
     data = b" ".join(words) + b" " + corpus.fill(corpus.ZIPF, 72, 0, 1 << 20).tobytes()
     want, wtok = coracle.count(data)
-    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, table_order=True)
+    stats = []
+    out = run_ranks(data, world, flags=mox.MOX_F_SORT_BYTES, stats=stats)
     assert sorted(x for items, _ in out for x in items) == want
-    assert any([w for w, _ in items] != sorted(w for w, _ in items) for items, _ in out)  # hash owners: engine order
+    assert len(stats) == world and all(st["x_ranged"] == 0 for st in stats)  # hash owners on every rank
     out = run_ranks(data, world, gather_root=0, flags=mox.MOX_F_SORT_BYTES)
     assert out[0] == (want, wtok)

@@ -18,6 +18,7 @@
 #   abe      interleaved end-to-end bench A/B of variants: AB_VARS, AB_ARGS
 #   sort     the device bytewise sort's GPU tests (group, exchange)
 #   xsort    the exchange and engine-group GPU tests (not slow)
+#   overlap  tools/overlap_probe.py: one engine's async C2 passes vs two engines' at once
 #   c2       the C2 bench line without the CPU baseline (value, k_map, sorted-result line)
 #   varpar   a build variant (VAR=name: build/var_name) through the parity subset and the
 #            full-size C2 async parity test
@@ -92,6 +93,10 @@ sort)
 xsort)
   # the exchange and engine-group tests (sorted exchange, device splitters, device sort)
   pyt xsort.log 900 tests/test_gpu_exchange.py tests/test_gpu_group.py -m "gpu and not slow"
+  ;;
+overlap)
+  timeout -k 10 400 python -u tools/overlap_probe.py 30 20 > $O/overlap.txt 2>&1; step "overlap probe" $?
+  cat $O/overlap.txt
   ;;
 c2)
   timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err; step "bench C2" $?
