@@ -80,6 +80,8 @@ def parse():
     ap.add_argument("--xport", default="rccl", choices=["rccl", "host"],
                     help="exchange transport for N > 1 (host: gloo-staged, for ranks sharing one GPU)")
     ap.add_argument("--device", type=int, default=-1, help="override the GPU (default LOCAL_RANK)")
+    ap.add_argument("--no-map-events", action="store_true",
+                    help="diagnostics: no HIP events around k_map in the timed steps (no roofline.achieved)")
     ap.add_argument("--traffic-json", default=None,  # profiles/pmc_k_map.json (C2) or pmc_k_map_<workload>.json
                     help="PMC summary of the map kernel (tools/pmc_traffic.py) to report as roofline.traffic")
     return ap.parse_args()
@@ -365,7 +367,8 @@ def main():
     base_flags = mox.MOX_F_NO_DICT if a.no_dict else 0
     # timed steps: HIP events around k_map only (each event record idles the
     # stream ~5.6 us); one diagnostic step after the timed region has them all
-    eng = mox.Engine(device=local if a.device < 0 else a.device, flags=base_flags | mox.MOX_F_TIMING_MAP,
+    map_flag = 0 if a.no_map_events else mox.MOX_F_TIMING_MAP
+    eng = mox.Engine(device=local if a.device < 0 else a.device, flags=base_flags | map_flag,
                      sample_pieces=a.sample_pieces, reserve_bytes=per_rank)
     progress("%s: generating %d MiB of corpus" % (a.workload, (hi - lo) >> 20))
     host = corpus.fill(kind, seed, lo, hi - lo)
@@ -423,14 +426,14 @@ def main():
     t0 = time.perf_counter()
     for i in range(a.steps):
         step()
-        if not use_async or i > 0:  # async: the call completed the previous pass
+        if (not use_async or i > 0) and map_flag:  # async: the call completed the previous pass
             map_ms.append(eng.ms_map())
         if world > 1:
             st = eng.stats()
             xms.append(st["ms_exchange"])
             gms.append(st["ms_gather"])
     eng.synchronize()
-    if use_async:
+    if use_async and map_flag:
         map_ms.append(eng.ms_map())  # the last pass, completed by synchronize
     if dist:
         dist.barrier()
@@ -539,7 +542,7 @@ def main():
     if rank == 0:
         ms_step = elapsed / a.steps * 1e3
         gbs = total / (elapsed / a.steps) / 1e9
-        map_avg = statistics.mean(map_ms)
+        map_avg = statistics.mean(map_ms) if map_ms else float("nan")
         if n1:  # the efficiency against the max-over-ranks time (known only now)
             n1["scaling_efficiency"] = round(gbs / (world * n1["value"]), 4)
         # algorithmic bytes per step = input read once + the output

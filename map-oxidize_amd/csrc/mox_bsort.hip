@@ -97,21 +97,26 @@ __device__ __forceinline__ void wave_lds_fence() {
 
 // Word i's count, byte offset and length, gathered once by the output kernels
 // through the sorted records' idx (one 16-byte read instead of three 8-byte
-// ones; table bytes < 4 GiB).
+// ones): offset in the low 40 bits of ol (table bytes < 1 TiB), length in the
+// high 24 (words < 16 MiB; a table with a longer word is sorted on the host).
 struct BPay {
   uint64_t count;
-  uint32_t off, len;
+  uint64_t ol;
 };
+constexpr uint64_t PAY_OFF_BITS = 40, PAY_LEN_MAX = (1ull << 24) - 1;
+__device__ __forceinline__ uint64_t pay_off(const BPay& p) { return p.ol & ((1ull << PAY_OFF_BITS) - 1); }
+__device__ __forceinline__ uint64_t pay_len(const BPay& p) { return p.ol >> PAY_OFF_BITS; }
 extern "C" __global__ __launch_bounds__(256) void k_bs_init(const uint64_t* offs, const uint8_t* bytes, const uint64_t* counts,
-                                                            uint64_t n, BRec* out, BPay* pay) {
+                                                            uint64_t n, BRec* out, BPay* pay, unsigned int* err) {
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
     BRec r;
     r.key = window(offs, bytes, i, 0);
     r.run = 0;
     r.idx = (uint32_t)i;
     out[i] = r;
-    const uint64_t o = offs[i];
-    pay[i] = BPay{counts[i], (uint32_t)o, (uint32_t)(offs[i + 1] - o)};
+    const uint64_t o = offs[i], len = offs[i + 1] - o;
+    if (len > PAY_LEN_MAX) atomicOr(err, 4u);  // (the host sorts such a table)
+    pay[i] = BPay{counts[i], o | (len << PAY_OFF_BITS)};
   }
 }
 
@@ -544,7 +549,7 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_out1(const BRec* r, uint6
   for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (uint64_t)gridDim.x * blockDim.x) {
     const BPay p = pay[r[j].idx];
     ocounts[j] = p.count;
-    olen[j] = p.len;
+    olen[j] = pay_len(p);
   }
 }
 // The words' bytes at their sorted offsets: block b writes the bytes of sorted
@@ -575,8 +580,8 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_out2(const BRec* r, uint6
         len = aux;
       } else {
         const BPay p = pay[rec.idx];
-        src = p.off;
-        len = p.len;
+        src = pay_off(p);
+        len = pay_len(p);
       }
     }
     if (B1 - gbase <= (uint64_t)OUT_STAGE) {
@@ -694,7 +699,11 @@ void bsort_free(mox_engine* e) {
 // The engine's result table (e->res) in bytewise order, on its GPU: the
 // sorted copy lives in s_counts / s_offs / s_bytes and becomes the result.
 // Scratch (s_tmp) is engine-owned and reused across calls: about 88 bytes per
-// word plus the look-back status (6 bytes per word).
+// word plus the look-back status (6 bytes per word).  When it does not fit next
+// to the engine's pass buffers (C4 at 16 GiB: 1.37e9 words, ~120 GB), the six
+// big record arrays borrow the pass scratch that is dead once a table is built
+// (cold regions, split buffers, reduce outputs, weighted records; the table
+// itself is never borrowed) and only the rest is allocated.
 // One attempt; returns -1 (nothing changed in e->res) when an eager level met
 // a tie run the unchecked mode cannot sort: the caller runs it again checked.
 int bsort_once(mox_engine* e, bool checked) {
@@ -708,26 +717,58 @@ int bsort_once(mox_engine* e, bool checked) {
   if (const char* cap = getenv("MOX_BSORT_MAX_WORDS"))
     if (n > strtoull(cap, nullptr, 10))
       return fail(MOX_ENOMEM, "bytewise sort: %llu words, MOX_BSORT_MAX_WORDS=%s", (unsigned long long)n, cap);
-  // (32-bit word offsets in the payload: a bigger table is sorted on the host, as on MOX_ENOMEM)
-  if (nb >= (1ull << 32)) return fail(MOX_ENOMEM, "bytewise sort: %llu table bytes (device sort: < 4 GiB)", (unsigned long long)nb);
+  // (40-bit word offsets in the payload: a bigger table is sorted on the host, as on MOX_ENOMEM)
+  if (nb >> PAY_OFF_BITS) return fail(MOX_ENOMEM, "bytewise sort: %llu table bytes (device sort: < 1 TiB)", (unsigned long long)nb);
   hipStream_t st = e->stream;
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   // scratch: records A, B, subset S, payload | run flags, positions | status | gh, gs | scan sums | totals, err
   const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8ull * scan_sum_words(n);
   const unsigned int lrun_cap = (unsigned int)std::min<uint64_t>(1u << 20, n / 4 + 16);  // k_bs_longsort's run list
-  const uint64_t need = 4 * rec + 2 * u64n + 8ull * lrun_cap + TICK_BYTES + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
+  const uint64_t small = 8ull * lrun_cap + TICK_BYTES + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
+  const uint64_t big[6] = {rec, rec, rec, rec, u64n, u64n};  // A, B, S, pay, fin, pos
+  uint8_t* bp[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int rc;
-  if ((rc = grow_dev(e->s_tmp, need)) || (rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) ||
-      (rc = grow_dev(e->s_bytes, nb + 64)))
+  if ((rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) || (rc = grow_dev(e->s_bytes, nb + 64)))
     return rc;
+  uint64_t need = small;
+  for (uint64_t b : big) need += b;
+  rc = grow_dev(e->s_tmp, need);
+  if (rc == MOX_ENOMEM) {
+    (void)hipGetLastError();  // the failed hipMalloc's error is not a later launch's
+    const Work& w = e->w;  // (the table is in t_*, or in the gather / sort buffers: never in these)
+    struct Slab { uint8_t* p; uint64_t left; };
+    Slab slab[] = {{(uint8_t*)w.cold, w.cold ? (uint64_t)w.map_grid * NB * w.cold_cap * 16 : 0},
+                   {(uint8_t*)w.uk, w.uk ? w.uniq_cap * 16 : 0},
+                   {(uint8_t*)w.split_k, w.split_k ? w.split_k_cap * 16 : 0},
+                   {(uint8_t*)w.uc, w.uc ? w.uniq_cap * 8 : 0},
+                   {(uint8_t*)w.w, w.w ? w.w_cap * sizeof(WRec) : 0},
+                   {(uint8_t*)w.w_sorted, w.w_sorted ? w.w_cap * sizeof(WRec) : 0},
+                   {(uint8_t*)w.ui, w.ui ? w.uniq_cap * 4 : 0}};
+    need = small;
+    for (int k = 0; k < 6; k++) {
+      for (auto& sl : slab)
+        if (sl.p && sl.left >= big[k]) {
+          bp[k] = sl.p;
+          const uint64_t used = (big[k] + 255) & ~255ull;
+          sl.p += used;
+          sl.left = sl.left > used ? sl.left - used : 0;
+          break;
+        }
+      if (!bp[k]) need += big[k];
+    }
+    rc = grow_dev(e->s_tmp, need);
+  }
+  if (rc) return rc;
   if (!e->h_bsort) HIPCHK(hipHostMalloc((void**)&e->h_bsort, OS_DIGITS * 256 * 8 + 64, hipHostMallocDefault));
   uint8_t* q = (uint8_t*)e->s_tmp.p;
-  BRec* A = (BRec*)q; q += rec;
-  BRec* B = (BRec*)q; q += rec;
-  BRec* S = (BRec*)q; q += rec;
-  BPay* pay = (BPay*)q; q += rec;
-  uint64_t* fin = (uint64_t*)q; q += u64n;
-  uint64_t* pos = (uint64_t*)q; q += u64n;
+  for (int k = 0; k < 6; k++)
+    if (!bp[k]) { bp[k] = q; q += big[k]; }
+  BRec* A = (BRec*)bp[0];
+  BRec* B = (BRec*)bp[1];
+  BRec* S = (BRec*)bp[2];
+  BPay* pay = (BPay*)bp[3];
+  uint64_t* fin = (uint64_t*)bp[4];
+  uint64_t* pos = (uint64_t*)bp[5];
   uint2* lrun = (uint2*)q; q += 8ull * lrun_cap;
   BSort s;
   s.tick = (unsigned int*)q; q += TICK_BYTES;
@@ -741,7 +782,7 @@ int bsort_once(mox_engine* e, bool checked) {
   uint64_t* h_tot = (uint64_t*)(e->h_bsort + OS_DIGITS * 256);
   HIPCHK(hipMemsetAsync(s.err, 0, 12, st));  // [0] look-back timeout [1] radix fallback [2] long runs (k_bs_segsort)
   // level 0: every word by its first 7 bytes and length class
-  hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, r.counts, n, A, pay);
+  hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, r.counts, n, A, pay, s.err);
   s.a = A;
   s.b = B;
   if ((rc = radix_sort(e, s, n, 8))) return rc;
@@ -775,6 +816,7 @@ int bsort_once(mox_engine* e, bool checked) {
       const uint32_t fl0 = (uint32_t)h_tot[2], fl1 = (uint32_t)(h_tot[2] >> 32);
       if (fl0 & 1u) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
       if (fl0 & 2u) return fail(MOX_EINVAL, "bytewise sort: too many tie runs");
+      if (fl0 & 4u) return fail(MOX_ENOMEM, "bytewise sort: a word of 16 MiB or more (sorted on the host)");
       if (fl1 && !checked) return -1;  // a long run in an eager level: run again, checked
       m = h_tot[0] & 0xFFFFFFFFull;
       runs = h_tot[0] >> 32;
@@ -819,6 +861,7 @@ int bsort_once(mox_engine* e, bool checked) {
   HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
   HIPCHK(hipStreamSynchronize(st));
   if ((uint32_t)h_tot[2] & 1u) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
+  if ((uint32_t)h_tot[2] & 4u) return fail(MOX_ENOMEM, "bytewise sort: a word of 16 MiB or more (sorted on the host)");
   r.counts = oc;
   r.offs = oo;
   r.bytes = (const uint8_t*)e->s_bytes.p;

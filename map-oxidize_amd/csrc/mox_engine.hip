@@ -110,7 +110,8 @@ int realloc_sized(mox_engine* e, const Caps& c) {
       {(void**)&n.ltab, n.long_cap * sizeof(LSlot)}, {(void**)&n.lpos, (n.long_cap + 1) * 8},
       {(void**)&n.uk, n.uniq_cap * 16}, {(void**)&n.uc, n.uniq_cap * 8}, {(void**)&n.ui, n.uniq_cap * 4},
       {(void**)&n.t_counts, n.table_cap * 8}, {(void**)&n.t_offs, (n.table_cap + 1) * 8},
-      {(void**)&n.t_bytes, n.bytes_cap}, {(void**)&n.split_k, n.split_k_cap * 16},
+      {(void**)&n.t_bytes, n.bytes_cap + 64}, {(void**)&n.split_k, n.split_k_cap * 16},  // (t_bytes: 64 B of slack for
+                                                                                          // aligned 8-byte reads past a word)
       {(void**)&n.split_w, n.split_w_cap * sizeof(WRec)}};
   for (auto& a : plan) *a.p = nullptr;
   for (auto& a : plan) {

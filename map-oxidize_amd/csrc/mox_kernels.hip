@@ -4208,12 +4208,24 @@ extern "C" __global__ void k_xingest(Work w, XDir dir, uint64_t n_short) {
 }
 
 // ---- sorted exchange (byte-range ownership; XSplit, mox_internal.h)
+// Bytes [o, o + 16) of the table as two little-endian words, from aligned
+// 8-byte loads and a funnel shift (t_bytes has 64 bytes of slack past its
+// end: realloc_sized), instead of one load per byte.
+__device__ __forceinline__ void table_bytes16(const Work& w, uint64_t o, uint64_t& k0, uint64_t& k1) {
+  const uint64_t* q = reinterpret_cast<const uint64_t*>(w.t_bytes + (o & ~7ull));
+  const uint32_t sh = (uint32_t)(o & 7u) * 8u;
+  const uint64_t a = q[0], b = q[1], c = q[2];
+  k0 = sh ? (a >> sh) | (b << (64 - sh)) : a;
+  k1 = sh ? (b >> sh) | (c << (64 - sh)) : b;
+}
+__device__ __forceinline__ uint64_t mask_bytes(uint64_t x, uint64_t n) { return n >= 8 ? x : x & ((1ull << (8 * n)) - 1ull); }
 // The first 8 bytes of table row i, big-endian, zero padded.
 __device__ __forceinline__ uint64_t row_prefix(const Work& w, uint64_t i) {
   const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;
-  uint64_t k = 0;
-  for (uint32_t j = 0; j < 8 && j < len; j++) k |= (uint64_t)w.t_bytes[o + j] << (56 - 8 * j);
-  return k;
+  uint64_t k0, k1;
+  table_bytes16(w, o, k0, k1);
+  (void)k1;
+  return __builtin_bswap64(mask_bytes(k0, len));
 }
 // This rank's sample block (XS_BLOCK words at out): XS_SAMPLES prefixes of its
 // local table, evenly over its rows (the table is in hash order, so they are a
@@ -4352,12 +4364,11 @@ extern "C" __global__ __launch_bounds__(XR_THREADS) void k_xpack_r(Work w, XSpli
   }
   __syncthreads();
   for (uint64_t i = r0 + t; i < r1; i += XR_THREADS) {
-    const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;
-    uint64_t k0 = 0, k1 = 0;
-    for (uint32_t j = 0; j < len; j++) {  // a short word: at most 16 bytes
-      const uint64_t b = w.t_bytes[o + j];
-      if (j < 8) k0 |= b << (8 * j); else k1 |= b << (8 * (j - 8));
-    }
+    const uint64_t o = w.t_offs[i], len = w.t_offs[i + 1] - o;  // a short word: at most 16 bytes
+    uint64_t k0, k1;
+    table_bytes16(w, o, k0, k1);
+    k0 = mask_bytes(k0, len);
+    k1 = len > 8 ? mask_bytes(k1, len - 8) : 0ull;
     const uint64_t pre = __builtin_bswap64(k0);
     const uint32_t d = range_owner(sp, P, pre);
     const uint32_t r = atomicAdd(&lc[d], 1u);

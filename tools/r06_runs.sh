@@ -18,6 +18,7 @@
 #   abe      interleaved end-to-end bench A/B of variants: AB_VARS, AB_ARGS
 #   sort     the device bytewise sort's GPU tests (group, exchange)
 #   xsort    the exchange and engine-group GPU tests (not slow)
+#   evab     bench line with / without the k_map timing events (interleaved)
 #   overlap  tools/overlap_probe.py: one engine's async C2 passes vs two engines' at once
 #   c2       the C2 bench line without the CPU baseline (value, k_map, sorted-result line)
 #   varpar   a build variant (VAR=name: build/var_name) through the parity subset and the
@@ -93,6 +94,17 @@ sort)
 xsort)
   # the exchange and engine-group tests (sorted exchange, device splitters, device sort)
   pyt xsort.log 900 tests/test_gpu_exchange.py tests/test_gpu_group.py -m "gpu and not slow"
+  ;;
+evab)
+  # the k_map timing events' cost: the default bench line against the same
+  # steps without events around k_map, interleaved
+  for k in 1 2; do
+    for v in ev noev; do
+      f=$O/evab_${k}_$v.json; x=""; [ $v = noev ] && x="--no-map-events"
+      timeout -k 10 300 python -u bench.py --no-cpu-baseline $x > $f 2> $O/evab_${k}_$v.err; step "evab $k $v" $?
+      python3 -c "import json;d=json.loads(open('$f').read().strip().splitlines()[-1]);print('$v', d['value'], d['ms_per_step'])"
+    done
+  done
   ;;
 overlap)
   timeout -k 10 400 python -u tools/overlap_probe.py 30 20 > $O/overlap.txt 2>&1; step "overlap probe" $?
