@@ -81,6 +81,45 @@ def test_c4_full_16gib_digest():
     assert got == want
 
 
+def test_c4_full_16gib_device_sorted():
+    """The device bytewise sort on C4's 16 GiB table (1.37e9 words, 14.8 GB of
+    word bytes: past the 4 GiB the sort took before round 6; its record arrays
+    borrow the pass's dead scratch): mox_sort_result must sort it on the GPU
+    (it raises rather than falling back), and the fetched table is the oracle's
+    (order-independent digest) in bytewise order -- checked on 400 sampled
+    windows of 2,000 consecutive rows, every adjacent pair strictly ascending."""
+    cfg = corpus.CONFIGS["C4"]
+    data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
+    e = mox.Engine(device=0, reserve_bytes=data.nbytes, flags=mox.MOX_F_SORT_BYTES)
+    d = e.alloc(data.nbytes)
+    try:
+        e.h2d(d, data)
+        e.run_device(d, data.nbytes)
+        e.sort_result()  # on the GPU, or MoxError
+        st = e.stats()
+        t = e.fetch()
+        counts, offs, raw = t.arrays()
+        tokens = t.tokens
+        t.close()
+    finally:
+        e.free(d)
+        e.close()
+    assert st["ms_sort"] > 0
+    assert int(counts.sum()) == tokens and counts.size > 1_000_000_000
+    rng = np.random.default_rng(6)
+    n = counts.size
+    for s0 in rng.integers(0, n - 2001, size=400):
+        ws = [raw[offs[i]:offs[i + 1]] for i in range(int(s0), int(s0) + 2001)]
+        assert all(a < b for a, b in zip(ws, ws[1:]))
+    for i in (0, n - 2):  # the two ends
+        assert raw[offs[i]:offs[i + 1]] < raw[offs[i + 1]:offs[i + 2]]
+    got = coracle.table_digest(counts, offs, raw)
+    del counts, offs, raw
+    want, wtok = coracle.count_digest(data, nthreads=16)
+    assert tokens == wtok
+    assert got == want
+
+
 def test_c5_full_16gib_exact():
     cfg = corpus.CONFIGS["C5"]
     data = corpus.fill(cfg["kind"], cfg["seed"], 0, cfg["nbytes"])
