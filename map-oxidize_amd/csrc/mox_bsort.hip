@@ -424,7 +424,7 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_ties(const BRec* r, uint6
 extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r, uint64_t n, const uint64_t* fx, const uint64_t* tot,
                                                                    const uint32_t* rb_in, uint32_t* rb_out, unsigned int* nlrun,
                                                                    unsigned int* err, const uint64_t* offs, const uint8_t* bytes,
-                                                                   uint32_t level, BRec* sub, uint64_t* pos) {
+                                                                   uint32_t level, BRec* sub, uint32_t* pos) {
   const uint64_t m = tot[0] & 0xFFFFFFFFull, runs = tot[0] >> 32;
   const uint32_t run_base = *rb_in;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -443,7 +443,7 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gather_ties(const BRec* r
     o.idx = b.idx;
     o.run = run_base + (uint32_t)((f >> 32) + (head ? 1 : 0));
     sub[c] = o;
-    pos[c] = j;
+    pos[c] = (uint32_t)j;  // (tables of < 2^32 words)
   }
 }
 // The subset's runs sorted by key in LDS: a workgroup loads SEG_CH subset
@@ -538,7 +538,7 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_longsort(BRec* S, const u
     __syncthreads();
   }
 }
-extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub, const uint64_t* tot, const uint64_t* pos, BRec* r) {
+extern "C" __global__ __launch_bounds__(256) void k_bs_put_ties(const BRec* sub, const uint64_t* tot, const uint32_t* pos, BRec* r) {
   const uint64_t m = tot[0] & 0xFFFFFFFFull;
   for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < m; c += (uint64_t)gridDim.x * blockDim.x) r[pos[c]] = sub[c];
 }
@@ -651,7 +651,8 @@ struct BSort {
   BRec *a, *b;                // records, ping-pong
   unsigned long long* gh;     // OS_DIGITS x 256 global histograms (device)
   uint64_t* gs;               // ... their exclusive scans
-  uint64_t* status;           // look-back status words: 256 per tile, one region per digit pass
+  uint64_t* status;           // look-back status words: 256 per tile, one region per digit pass (or one reused region)
+  bool one_region;            // one status region, zeroed again before every pass (big tables)
   unsigned int* err;          // look-back timeout flag
   unsigned int* tick;         // OS_DIGITS tile tickets (one per digit pass), just below status
   unsigned long long* h_gh;   // pinned host copy of gh
@@ -669,15 +670,20 @@ int radix_sort(mox_engine* e, BSort& s, uint64_t n, int nd) {
   HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, (size_t)nd * 256 * 8, hipMemcpyDeviceToHost, st));
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   if (ntiles > 0x7FFFFFFFull) return fail(MOX_EINVAL, "bytewise sort: too many tiles");
-  // zero the tile tickets and the status words of every pass at once (a region per digit)
-  HIPCHK(hipMemsetAsync(s.tick, 0, TICK_BYTES + (size_t)nd * ntiles * 256 * 8, st));
+  // zero the tile tickets and the status words of every pass at once (a region per
+  // digit; a big table's single region is zeroed again before each later pass)
+  const size_t region = (size_t)ntiles * 256 * 8;
+  HIPCHK(hipMemsetAsync(s.tick, 0, TICK_BYTES + (s.one_region ? 1 : (size_t)nd) * region, st));
   HIPCHK(hipStreamSynchronize(st));
+  bool first = true;
   for (int d = 0; d < nd; d++) {
     bool uniform = false;
     for (int v = 0; v < 256; v++) uniform |= s.h_gh[d * 256 + v] == n;
     if (uniform) continue;  // every record has the same digit: the order stays
+    if (s.one_region && !first) HIPCHK(hipMemsetAsync(s.status, 0, region, st));
+    first = false;
     hipLaunchKernelGGL(k_os_pass, dim3((uint32_t)ntiles), dim3(OS_THREADS), 0, st, (const BRec*)s.a, s.b, n, d,
-                       (const uint64_t*)s.gs, s.status + (size_t)d * ntiles * 256, s.err, s.tick + d);
+                       (const uint64_t*)s.gs, s.status + (s.one_region ? 0 : (size_t)d * ntiles * 256), s.err, s.tick + d);
     HIPCHK(hipGetLastError());
     std::swap(s.a, s.b);
   }
@@ -698,10 +704,12 @@ void bsort_free(mox_engine* e) {
 
 // The engine's result table (e->res) in bytewise order, on its GPU: the
 // sorted copy lives in s_counts / s_offs / s_bytes and becomes the result.
-// Scratch (s_tmp) is engine-owned and reused across calls: about 88 bytes per
-// word plus the look-back status (6 bytes per word).  When it does not fit next
-// to the engine's pass buffers (C4 at 16 GiB: 1.37e9 words, ~120 GB), the six
-// big record arrays borrow the pass scratch that is dead once a table is built
+// Scratch (s_tmp) is engine-owned and reused across calls: about 60 bytes per
+// word (76 in the checked mode, which keeps the tie subset apart) plus the
+// look-back status (6 bytes per word, or 0.5 when a table's per-digit regions
+// would pass 256 MiB and one region is reused).  When it does not fit next to
+// the engine's pass buffers (C4 at 16 GiB: 1.37e9 words, ~84 GB), the big
+// record arrays borrow the pass scratch that is dead once a table is built
 // (cold regions, split buffers, reduce outputs, weighted records; the table
 // itself is never borrowed) and only the rest is allocated.
 // One attempt; returns -1 (nothing changed in e->res) when an eager level met
@@ -722,10 +730,17 @@ int bsort_once(mox_engine* e, bool checked) {
   hipStream_t st = e->stream;
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   // scratch: records A, B, subset S, payload | run flags, positions | status | gh, gs | scan sums | totals, err
-  const uint64_t rec = 16 * n, u64n = 8 * n, stb = 8ull * OS_DIGITS * 256 * ntiles, sums = 8ull * scan_sum_words(n);
+  // (a table whose per-digit status regions would pass 256 MiB reuses one region)
+  const bool one_region = 8ull * OS_DIGITS * 256 * ntiles > (256ull << 20);
+  // (every array a multiple of 256 bytes: what follows stays aligned for its 8-byte atomics)
+  const uint64_t rec = (16 * n + 255) & ~255ull, u64n = (8 * n + 255) & ~255ull, u32n = (4 * n + 255) & ~255ull;
+  const uint64_t sums = 8ull * scan_sum_words(n);
+  const uint64_t stb = 8ull * (one_region ? 1 : OS_DIGITS) * 256 * ntiles;
   const unsigned int lrun_cap = (unsigned int)std::min<uint64_t>(1u << 20, n / 4 + 16);  // k_bs_longsort's run list
   const uint64_t small = 8ull * lrun_cap + TICK_BYTES + stb + 2 * OS_DIGITS * 256 * 8 + sums + 256;
-  const uint64_t big[6] = {rec, rec, rec, rec, u64n, u64n};  // A, B, S, pay, fin, pos
+  // A, B, S (the tie subset: in the checked mode only; else the radix pass's
+  // free ping-pong buffer), pay, fin, pos
+  const uint64_t big[6] = {rec, rec, checked ? rec : 0, rec, u64n, u32n};
   uint8_t* bp[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int rc;
   if ((rc = grow_dev(e->s_counts, 8 * n + 64)) || (rc = grow_dev(e->s_offs, 8 * (n + 1) + 64)) || (rc = grow_dev(e->s_bytes, nb + 64)))
@@ -746,6 +761,7 @@ int bsort_once(mox_engine* e, bool checked) {
                    {(uint8_t*)w.ui, w.ui ? w.uniq_cap * 4 : 0}};
     need = small;
     for (int k = 0; k < 6; k++) {
+      if (!big[k]) continue;
       for (auto& sl : slab)
         if (sl.p && sl.left >= big[k]) {
           bp[k] = sl.p;
@@ -757,22 +773,32 @@ int bsort_once(mox_engine* e, bool checked) {
       if (!bp[k]) need += big[k];
     }
     rc = grow_dev(e->s_tmp, need);
+    if (rc) {
+      size_t fr = 0, to = 0;
+      (void)hipMemGetInfo(&fr, &to);
+      (void)hipGetLastError();
+      int nbor = 0;
+      for (uint8_t* p : bp) nbor += p != nullptr;
+      return fail(MOX_ENOMEM, "bytewise sort: %llu words need %llu scratch bytes besides %d borrowed arrays; %zu of %zu bytes free",
+                  (unsigned long long)n, (unsigned long long)need, nbor, fr, to);
+    }
   }
   if (rc) return rc;
   if (!e->h_bsort) HIPCHK(hipHostMalloc((void**)&e->h_bsort, OS_DIGITS * 256 * 8 + 64, hipHostMallocDefault));
   uint8_t* q = (uint8_t*)e->s_tmp.p;
   for (int k = 0; k < 6; k++)
-    if (!bp[k]) { bp[k] = q; q += big[k]; }
+    if (!bp[k] && big[k]) { bp[k] = q; q += big[k]; }
   BRec* A = (BRec*)bp[0];
   BRec* B = (BRec*)bp[1];
-  BRec* S = (BRec*)bp[2];
+  BRec* S = (BRec*)bp[2];  // (nullptr unless checked: then the free ping-pong buffer below)
   BPay* pay = (BPay*)bp[3];
   uint64_t* fin = (uint64_t*)bp[4];
-  uint64_t* pos = (uint64_t*)bp[5];
+  uint32_t* pos = (uint32_t*)bp[5];
   uint2* lrun = (uint2*)q; q += 8ull * lrun_cap;
   BSort s;
   s.tick = (unsigned int*)q; q += TICK_BYTES;
   s.status = (uint64_t*)q; q += stb;
+  s.one_region = one_region;
   s.gh = (unsigned long long*)q; q += OS_DIGITS * 256 * 8;
   s.gs = (uint64_t*)q; q += OS_DIGITS * 256 * 8;
   uint64_t* ssum = (uint64_t*)q; q += sums;
@@ -787,7 +813,8 @@ int bsort_once(mox_engine* e, bool checked) {
   s.b = B;
   if ((rc = radix_sort(e, s, n, 8))) return rc;
   BRec* R = s.a;                 // sorted (A or B)
-  BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner
+  BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner (checked), or the subset
+  if (!checked) S = S2;
   // levels 1, 2, ...: runs of words sharing every compared byte, re-sorted on
   // the next window (by run: short runs in LDS by k_bs_segsort, runs of up to
   // RUN_LMAX by k_bs_longsort).  The first EAGER_LEVELS levels (words up to 21
@@ -845,7 +872,7 @@ int bsort_once(mox_engine* e, bool checked) {
       run_base += (uint32_t)runs;
     }
     hipLaunchKernelGGL(k_bs_put_ties, dim3(grid_for(m)), dim3(256), 0, st, (const BRec*)sorted, (const uint64_t*)lt,
-                       (const uint64_t*)pos, R);
+                       (const uint32_t*)pos, R);
     HIPCHK(hipGetLastError());
   }
   // the sorted table: counts and lengths, offsets by a scan, bytes

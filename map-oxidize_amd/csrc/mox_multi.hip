@@ -30,7 +30,11 @@ int grow_dev(DevBuf& b, size_t bytes) {
   b.cap = 0;
   size_t want = std::max<size_t>(bytes + bytes / 4, 4096);
   hipError_t err = hipMalloc(&b.p, want);
-  if (err != hipSuccess) return fail(MOX_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(err));
+  if (err != hipSuccess) {
+    b.p = nullptr;
+    (void)hipGetLastError();  // the failed allocation's error is not a later launch's (callers may fall back)
+    return fail(MOX_ENOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(err));
+  }
   b.cap = want;
   return MOX_OK;
 }

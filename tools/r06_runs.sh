@@ -21,6 +21,7 @@
 #   evab     bench line with / without the k_map timing events (interleaved)
 #   overlap  tools/overlap_probe.py: one engine's async C2 passes vs two engines' at once
 #   c2       the C2 bench line without the CPU baseline (value, k_map, sorted-result line)
+#   c2prof   rocprofv3 kernel stats of that bench line (sort kernels)
 #   varpar   a build variant (VAR=name: build/var_name) through the parity subset and the
 #            full-size C2 async parity test
 #   pmc      k_map FETCH/WRITE traffic at C2 and SQ counters of k_map
@@ -113,6 +114,13 @@ overlap)
 c2)
   timeout -k 10 400 python -u bench.py --no-cpu-baseline > $O/bench_c2.json 2> $O/bench_c2.err; step "bench C2" $?
   python3 -c "import json;d=json.loads(open('$O/bench_c2.json').read().strip().splitlines()[-1]);print(d['value'], d['roofline']['avg_launch_ms'], d['sorted_result'])"
+  ;;
+c2prof)
+  # rocprofv3 kernel stats of the C2 bench (no CPU baseline): the sort kernels' averages
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c2p -o run -- \
+    python3 bench.py --no-cpu-baseline > $O/c2p_under_rocprof.log 2>&1; step "rocprof C2" $?
+  f=$(ls $O/c2p/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] || f=$(ls $O/c2p/run_kernel_stats.csv)
+  cut -d, -f1-4 "$f" | grep -E "k_ss_|k_os_pass|k_bs_|k_scan|k_map|k_reduce\"" ; true
   ;;
 varpar)
   # a build variant (build/var_$VAR) through the parity subset and the full-size
