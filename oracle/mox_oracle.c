@@ -24,10 +24,12 @@
  * §8(c)).  This restatement is cross-checked against an independent Python
  * restatement (oracle/pyoracle.py: Python's strict UTF-8 decoder, an explicit
  * White_Space set and str.lower()) and the known-answer table of SURVEY.md §0.1.
- * Case data: Unicode 14.0.0 from ICU 70.1 (map-oxidize_amd/csrc/mox_unicode_tables.h
- * is the shared DATA; this file's code is independent of the GPU code).  The
- * lowercase map, Final_Sigma and White_Space are pinned to ICU's own answers in
- * tests/test_unicode_pin.py (tests/golden/unicode_icu70.json).
+ * Case data: Unicode 14.0.0 from ICU 70.1, in the oracle's own tables
+ * (oracle/mox_oracle_case.h, written by oracle/gen_case_tables.py from the ICU
+ * fixture tests/golden/unicode_icu70.json); neither the product's table header
+ * nor its lookup code is used here.  tests/test_unicode_pin.py pins the
+ * product header, and this oracle, to the same ICU answers (lowercase map,
+ * Final_Sigma probes, White_Space).
  */
 #include "mox_oracle.h"
 
@@ -35,7 +37,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../map-oxidize_amd/csrc/mox_unicode_tables.h"
+#include "mox_oracle_case.h" /* the oracle's own tables, from the ICU 70.1 fixture (gen_case_tables.py) */
 
 /* ---- UTF-8 validation (Rust core::str::from_utf8 rules) ---- */
 int64_t moxo_utf8_invalid_at(const uint8_t* s, uint64_t n) {
@@ -97,25 +99,30 @@ int moxo_is_whitespace(uint32_t c) {
   }
 }
 
-static int in_ranges(uint32_t c, const uint32_t* lo, const uint32_t* hi, int n) {
+static int in_ranges(uint32_t c, const moxo_range_t* r, int n) {
   int a = 0, b = n - 1;
   while (a <= b) {
     int m = (a + b) >> 1;
-    if (c < lo[m]) b = m - 1;
-    else if (c > hi[m]) a = m + 1;
+    if (c < r[m].lo) b = m - 1;
+    else if (c > r[m].hi) a = m + 1;
     else return 1;
   }
   return 0;
 }
-static int is_cased(uint32_t c) { return in_ranges(c, mox_cased_lo, mox_cased_hi, MOX_CASED_N); }
-static int is_ci(uint32_t c) { return in_ranges(c, mox_ci_lo, mox_ci_hi, MOX_CI_N); }
-static uint32_t lower1(uint32_t c) {
-  int a = 0, b = MOX_LOWER_N - 1;
+static int is_cased(uint32_t c) { return in_ranges(c, moxo_cased, MOXO_CASED_N); }
+static int is_ci(uint32_t c) { return in_ranges(c, moxo_ci, MOXO_CI_N); }
+/* lowercase of c: one or two code points (*second = 0: one) */
+static uint32_t lower1(uint32_t c, uint32_t* second) {
+  int a = 0, b = MOXO_LOWER_N - 1;
+  *second = 0;
   while (a <= b) {
     int m = (a + b) >> 1;
-    if (c < mox_lower_src[m]) b = m - 1;
-    else if (c > mox_lower_src[m]) a = m + 1;
-    else return mox_lower_dst[m];
+    if (c < moxo_lower[m].cp) b = m - 1;
+    else if (c > moxo_lower[m].cp) a = m + 1;
+    else {
+      *second = moxo_lower[m].l1;
+      return moxo_lower[m].l0;
+    }
   }
   return c;
 }
@@ -148,9 +155,10 @@ uint64_t moxo_lowercase(const uint8_t* s, uint64_t n, uint8_t* out) {
       o += (uint64_t)enc(fin ? 0x3C2 : 0x3C3, out + o);
       continue;
     }
-    uint32_t l = lower1(c);
-    if (l == MOX_LOWER_SPECIAL_I_DOT) { o += (uint64_t)enc(0x69, out + o); o += (uint64_t)enc(0x307, out + o); }
-    else o += (uint64_t)enc(l, out + o);
+    uint32_t l2;
+    const uint32_t l = lower1(c, &l2);
+    o += (uint64_t)enc(l, out + o);
+    if (l2) o += (uint64_t)enc(l2, out + o);
   }
   free(cps);
   return o;

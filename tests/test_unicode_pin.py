@@ -105,3 +105,16 @@ def test_unicode14_changes_are_kats(fx):
     assert coracle.lowercase("A᜴Σ".encode()).endswith("σ".encode())
     # a Unicode 14.0 case pair: U+2C2F GLAGOLITIC CAPITAL LETTER CAUDATE CHRIVI
     assert coracle.lowercase("Ⱟ".encode()) == "ⱟ".encode()
+
+
+def test_oracle_case_header_is_generated_from_the_fixture():
+    """The oracle's own case tables (oracle/mox_oracle_case.h, not the product's
+    header) are exactly what oracle/gen_case_tables.py writes from the ICU 70.1
+    fixture."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_case_tables", os.path.join(ROOT, "oracle", "gen_case_tables.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    assert open(os.path.join(ROOT, "oracle", "mox_oracle_case.h")).read() == gen.build_text()
+    src = open(os.path.join(ROOT, "oracle", "mox_oracle.c")).read()
+    assert "mox_unicode_tables.h" not in src.replace("mox_unicode_tables.h is", "")
