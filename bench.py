@@ -332,6 +332,9 @@ def main_group(a):
             "gathered_table": {"n": table_n, "bytes": table_bytes, "tokens": table_tokens,
                                "order": "bytewise (sorted exchange: each member sorts its byte range on its GPU "
                                         "inside the timed step; sort_bytes = the slowest member's sort)"},
+            "note": "exchange_ms = the slowest member's splitters + counts + pack + payload copies + reduce-only "
+                    "pass, without its bytewise sort (phases_ms.sort_bytes); step_wall ≈ local_passes + exchange "
+                    "+ sort_bytes + gather",
         },
         "same_work_n1": n1,
         "check_sum_counts_eq_tokens": ok,
@@ -533,7 +536,8 @@ def main():
             "hash_order": {"value": round(total / (el_hash / a.steps) / 1e9, 3), "ms_per_step": round(el_hash / a.steps * 1e3, 4),
                            "note": "the same steps without the sort at rank 0"} if el_hash else None,
             "note": "exchange = sampled byte-range splitters + counts all-to-all + pack + payload all-to-all "
-                    "(RCCL send/recv in one group) + reduce-only pass + the rank's bytewise sort of its range; "
+                    "(RCCL send/recv in one group) + reduce-only pass; sort_bytes = the rank's bytewise sort of its "
+                    "range, after the exchange; "
                     "gather = every rank's sorted table to rank 0 (mox_gather) in rank order, inside the timed step",
         }
     else:

@@ -137,7 +137,7 @@ typedef struct mox_stats {
   double ms_finalize;      /* table materialisation */
   double ms_h2d;           /* host -> device corpus copy (mox_count / mox_count_file) */
   double ms_d2h;           /* table fetch */
-  double ms_exchange;      /* multi-GPU all-to-all + final reduce */
+  double ms_exchange;      /* multi-GPU all-to-all + final reduce (not the sorted exchange's sort: ms_sort) */
   uint64_t reduce_units;   /* reduce work units (partitions, or their sub-buckets when split) */
   uint32_t split_partitions; /* partitions split by the high-cardinality path */
   uint32_t async_reruns;   /* async passes re-run synchronously (overflow), cumulative over the engine */

@@ -2695,27 +2695,29 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
     sd += d[j];
     sr += c[j];              // output region: records, no padding
   }
+  __shared__ uint32_t ncat[4];
+  __shared__ unsigned long long gcat[4];
+  if (tid < 4) ncat[tid] = 0;  // (ordered before the adds below by block_exscan's barriers)
   uint64_t tc, tw, tr;
   uint64_t ec = block_exscan(sc, wsum, tc);
   uint64_t ew = block_exscan(sd, wsum, tw);
   uint64_t er = block_exscan(sr, wsum, tr);
   const uint64_t kb = w.sp_off[b], wb = w.spw_off[b], rb = w.rec_off[b];
+  // work lists of the unit kernels: each unit's rank inside this workgroup's
+  // share of its list (LDS), then one global add per list and workgroup (the
+  // lists' order is free: units are placed by their descriptors)
+  uint32_t cat[SUB_PER_T], lr[SUB_PER_T];
 #pragma unroll
   for (int j = 0; j < SUB_PER_T; j++) {
     const uint32_t sb = SUB_PER_T * tid + j;
+    cat[j] = 3;  // none
     if (sb < nsub) {
       const uint32_t u = u0 + sb;
       if (MOX_CHK(w, u < U_MAX, CHK_UNIT)) w.udesc[u] = UnitDesc{kb + ec, wb + ew, rb + er + ew, c[j], d[j], b, kk};
-      if (d[j] == 0 && c[j] > SMALL_CAP && c[j] <= 2 * SMALL_CAP) {  // count-1, up to twice sort1's size: k_reduce_sort2
-        const unsigned long long q = atomicAdd(&w.ctl->n_mid, 1ull);
-        if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.mid_units[q] = u;
-      } else if (c[j] + d[j] > SMALL_CAP) {
-        const unsigned long long q = atomicAdd(&w.ctl->n_big, 1ull);
-        if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.big_units[q] = u;
-      } else if (d[j] != 0) {  // weighted records, <= SMALL_CAP in all: k_reduce_small
-        const unsigned long long q = atomicAdd(&w.ctl->n_small, 1ull);
-        if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) w.small_units[q] = u;
-      }
+      if (d[j] == 0 && c[j] > SMALL_CAP && c[j] <= 2 * SMALL_CAP) cat[j] = 0;  // count-1, up to twice sort1's size: k_reduce_sort2
+      else if (c[j] + d[j] > SMALL_CAP) cat[j] = 1;                            // k_reduce
+      else if (d[j] != 0) cat[j] = 2;  // weighted records, <= SMALL_CAP in all: k_reduce_small
+      if (cat[j] < 3) lr[j] = atomicAdd(&ncat[cat[j]], 1u);
       cc[sb] = (uint32_t)ec;
       cw[sb] = (uint32_t)ew;
       pst[sb] = PS_EMPTY;
@@ -2725,6 +2727,16 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
     er += c[j];
   }
   __syncthreads();
+  if (tid < 3 && ncat[tid]) gcat[tid] = atomicAdd(tid == 0 ? &w.ctl->n_mid : tid == 1 ? &w.ctl->n_big : &w.ctl->n_small,
+                                                  (unsigned long long)ncat[tid]);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < SUB_PER_T; j++)
+    if (cat[j] < 3) {
+      const unsigned long long q = gcat[cat[j]] + lr[j];
+      uint32_t* list = cat[j] == 0 ? w.mid_units : cat[j] == 1 ? w.big_units : w.small_units;
+      if (MOX_CHK(w, q < U_MAX, CHK_UNIT)) list[q] = u0 + SUB_PER_T * tid + j;
+    }
   uint4* ok = w.split_k + kb;
   // (the lambda runs under a per-record lane mask; the pair loop is the same
   // wave-level loop as k_map's cold_pair)
@@ -2757,7 +2769,10 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   // slice opens (2^kk) / qf sub-buckets, which exceeds that only for qf = 2 and
   // kk = 12 (a 257..512-workgroup map grid); such a slice takes the pair path
   const bool stage_fits = ((1u << kk) >> (qf == 4u ? 2u : 1u)) <= 1024u;
-  if (sliced && stage_fits && MOX_SPLIT_STAGE) {
+  if (w.b_recs[b] == 0) {
+    // no cold records (the exchange's and mox_reduce_pairs' reduce passes):
+    // only the weighted records below
+  } else if (sliced && stage_fits && MOX_SPLIT_STAGE) {
     SplitStage S;
     S.stage = reinterpret_cast<uint4*>(xs);
     S.sidx = reinterpret_cast<uint16_t*>(xs + SST_CH * 16);
@@ -2776,10 +2791,20 @@ extern "C" __global__ __launch_bounds__(1024) void k_split_scatter(Work w) {
   }
   const uint64_t w0 = w.w_off[b], w1 = w.w_off[b + 1];
   WRec* ow = w.split_w + wb;
-  for (uint64_t i = w0 + tid; i < w1; i += blockDim.x) {
-    const WRec r = w.w_sorted[i];
-    const uint32_t p = atomicAdd(&cw[hbits(key_hash(r.w0, r.w1), NB_LOG2, kk)], 1u);
-    if (MOX_CHK(w, p < tw && wb + p < w.split_w_cap, CHK_SPLIT_W)) ow[p] = r;
+  constexpr int WB = 4;  // weighted records per thread and round, all loads issued before the first is used
+  for (uint64_t i0 = w0 + tid; i0 < w1; i0 += WB * blockDim.x) {
+    WRec r[WB];
+#pragma unroll
+    for (int q = 0; q < WB; q++) {
+      const uint64_t i = i0 + (uint64_t)q * blockDim.x;
+      if (i < w1) r[q] = w.w_sorted[i];
+    }
+#pragma unroll
+    for (int q = 0; q < WB; q++)
+      if (i0 + (uint64_t)q * blockDim.x < w1) {
+        const uint32_t p = atomicAdd(&cw[hbits(key_hash(r[q].w0, r[q].w1), NB_LOG2, kk)], 1u);
+        if (MOX_CHK(w, p < tw && wb + p < w.split_w_cap, CHK_SPLIT_W)) ow[p] = r[q];
+      }
   }
   __syncthreads();
   if (sliced && MOX_SPLIT_STAGE) return;  // (no pair slots)

@@ -868,9 +868,12 @@ int group_run(mox_engine* e, const std::vector<Corpus>& c, const std::vector<uin
     words_local += G.m[i]->stats.uniques;
     ms_map += G.m[i]->stats.ms_map / G.n;  // MOX_F_TIMING(_MAP): the members' mean map-kernel time
   }
-  const auto t1 = std::chrono::steady_clock::now();
   if ((rc = group_exchange(G))) return rc;
-  const double ms_x = ms_since(t1);
+  // the exchange without the sorted exchange's bytewise sorts (reported as
+  // ms_sort), as one rank's mox_exchange reports it: the slowest member's
+  // time from its x_begin to the end of its reduce pass (reduce_received)
+  double ms_x = 0;
+  for (int i = 0; i < G.n; i++) ms_x = std::max(ms_x, G.m[i]->stats.ms_exchange);
   uint64_t xs = 0, xr = 0;
   for (int i = 0; i < G.n; i++) {
     xs += G.m[i]->stats.x_bytes_sent;

@@ -68,6 +68,16 @@ n2)
   python3 tools/step_timeline.py $O/n2tr 30 > $O/n2_step_timeline.txt; step "step timeline N2" $?
   tail -3 $O/n2_step_timeline.txt
   ;;
+abn2)
+  # interleaved N = 2 engine-group bench lines of build variants: AB_VARS="v1 v2 v1 v2"
+  k=0
+  for v in $AB_VARS; do
+    k=$((k+1)); f=$O/abn2_${k}_${v}
+    MOX_LIB=build/var_$v/libmox.so timeout -k 10 400 python -u bench.py --gpus 2 --xport host --device 0 --steps 5 --warmup 2 > $f.json 2> $f.err
+    rc=$?; [ $rc -eq 0 ] || { tail -3 $f.err; step "abn2 $v" $rc; }
+    python3 -c "import json;d=json.loads(open('$f.json').read().strip().splitlines()[-1]);m=d['multi_gpu'];h=d['hash_order'];print('$v', d['value'], 'exchange', m['exchange_ms'], 'sort', d['phases_ms']['sort_bytes'], 'hash', h['value'], h['phases_ms']['exchange'])"
+  done
+  ;;
 lines)
   timeout -k 10 420 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --workload C5 > $O/bench_c5.json 2> $O/bench_c5.err; step "bench C5" $?
   cut -c1-200 $O/bench_c5.json
