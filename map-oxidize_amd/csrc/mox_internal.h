@@ -106,8 +106,15 @@ constexpr int SUB_BITS_MAX = 12;
 constexpr int SUB_N = 1 << SUB_BITS_MAX;
 constexpr int U_MAX = NB * SUB_N;           // reduce units
 constexpr int SUB_PER_T = SUB_N / 1024;     // sub-buckets per thread in the 1024-thread unit kernels
-constexpr uint32_t SPLIT_MIN = 2048;        // records below which a partition is never split (= k_reduce's RED_CAP: at most
-                                            // that many distinct keys, one table pass)
+#ifndef MOX_SPLIT_MIN
+#define MOX_SPLIT_MIN 8192
+#endif
+// records up to which a partition is never split: k_reduce takes it whole, in
+// at most 4 table sub-passes of RED_CAP distinct keys (the exchange's reduce
+// pass at C3, ~3.3 K weighted records per partition: 2048 -> 8192 took its
+// span from 556 to 517 us and the N = 2 exchange from 1.07-1.10 to
+// 0.86-0.88 ms, profiles/r06/split_min_ab_g31.txt)
+constexpr uint32_t SPLIT_MIN = MOX_SPLIT_MIN;
 constexpr uint32_t SPLIT_TARGET = 320;      // records per sub-bucket aimed at
 constexpr uint32_t SMALL_CAP = 512;         // sub-buckets up to this many records: k_reduce_small
 #ifndef MOX_S1_WG

@@ -78,6 +78,14 @@ abn2)
     python3 -c "import json;d=json.loads(open('$f.json').read().strip().splitlines()[-1]);m=d['multi_gpu'];h=d['hash_order'];print('$v', d['value'], 'exchange', m['exchange_ms'], 'sort', d['phases_ms']['sort_bytes'], 'hash', h['value'], h['phases_ms']['exchange'])"
   done
   ;;
+n2prof)
+  # kernel trace of an N = 2 group bench (VAR=name: build/var_name), the exchange reduce passes' kernels
+  L=${VAR:+build/var_$VAR/libmox.so}; L=${L:-map-oxidize_amd/mox/libmox.so}
+  MOX_LIB=$L timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d $O/n2k_${VAR:-tree} -o run -- \
+    python3 bench.py --gpus 2 --xport host --device 0 --steps 3 --warmup 1 > $O/n2k_${VAR:-tree}.log 2>&1; step "rocprof N2 ${VAR:-tree}" $?
+  python3 tools/xpass_kernels.py $O/n2k_${VAR:-tree} > $O/xpass_${VAR:-tree}.txt; step "xpass ${VAR:-tree}" $?
+  cat $O/xpass_${VAR:-tree}.txt
+  ;;
 lines)
   timeout -k 10 420 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --workload C5 > $O/bench_c5.json 2> $O/bench_c5.err; step "bench C5" $?
   cut -c1-200 $O/bench_c5.json
