@@ -17,9 +17,10 @@
 // counters in LDS), publishes its digit counts and finds its global offsets by
 // a decoupled look-back over the tiles before it (agent-scope status words),
 // stages the tile in LDS in digit order and writes each digit's run with
-// consecutive stores.  One up-front kernel histograms every digit; digits whose
-// value is the same for every record are skipped (the run id at level 0, zero
-// bytes every word shares).
+// consecutive stores.  One up-front kernel histograms every digit; a pass over
+// a digit whose value is the same for every record is a copy (the pass reads
+// the histogram itself: no host round trip between the histogram and the
+// passes).
 //
 // Ties after a level are words that share the window and both go on past it
 // (aux == 8 on both sides).  Their maximal runs are re-sorted by the radix
@@ -120,6 +121,19 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_init(const uint64_t* offs
   }
 }
 
+// The sort's control words before k_bs_init, one launch instead of a memset
+// each: flags (err, 3 words), the digit histograms (gh), the level totals and
+// run-id bases (total, 16 words; rbs[0] = 1: level 0's run ids end at 1), the
+// pass tickets and look-back status words (tick, nst words).
+extern "C" __global__ __launch_bounds__(256) void k_bs_zero(unsigned int* err, unsigned long long* gh, uint64_t* total,
+                                                            uint64_t* tick, uint64_t nst) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  if (t < 3) err[t] = 0;
+  if (t < OS_DIGITS * 256) gh[t] = 0;
+  if (t < 8) total[t] = t == 4 ? 1ull : 0ull;  // total + 4 = rbs (u32): rbs[0] = 1, rbs[1] = 0
+  for (uint64_t i = t; i < nst; i += stride) tick[i] = 0;
+}
+
 // Histograms of digits 0 .. nd - 1 over every record: GH_BLOCKS blocks, one
 // contiguous share of the records each, per-wave LDS histograms (a hot digit
 // value contends within one wave only), then one global add per non-zero bin
@@ -172,6 +186,7 @@ extern "C" __global__ __launch_bounds__(256) void k_bs_gscan(const unsigned long
 // zero at launch.
 extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass(const BRec* __restrict__ in, BRec* __restrict__ out,
                                                                        uint64_t n, int d, const uint64_t* __restrict__ gs,
+                                                                       const unsigned long long* __restrict__ gh,
                                                                        uint64_t* status, unsigned int* err,
                                                                        unsigned int* tick) {
   __shared__ __attribute__((aligned(16))) BRec stage[OS_TILE];
@@ -187,6 +202,7 @@ extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass
   const uint64_t t0 = (uint64_t)tile * OS_TILE;
   const uint32_t tn = (uint32_t)(n - t0 < (uint64_t)OS_TILE ? n - t0 : (uint64_t)OS_TILE);
   for (int w = 0; w < OS_WAVES; w++) wcnt[w][tid] = 0;
+  const unsigned long long ghv = gh[d * 256 + tid];  // (in flight with the records)
   // records of wave wv: tile positions wv * 64 ITEMS + i * 64 + lane (input order = (wv, i, lane))
   BRec rec[OS_ITEMS];
   typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -198,7 +214,16 @@ extern "C" __global__ __launch_bounds__(OS_THREADS, OS_WG_PER_CU) void k_os_pass
     rec[i].run = x.z;
     rec[i].idx = x.w;
   }
-  __syncthreads();
+  // every record has the same digit (the histogram holds n in one bin): the
+  // order stays, the pass is a copy (no look-back: every tile takes this branch)
+  if (__syncthreads_or(ghv == n)) {
+#pragma unroll
+    for (int i = 0; i < OS_ITEMS; i++) {
+      const uint32_t p = (uint32_t)(wv * 64 * OS_ITEMS + i * 64 + lane);
+      if (p < tn) out[t0 + p] = rec[i];
+    }
+    return;
+  }
   // stable rank inside the wave: lanes with the same digit by 8 bit-sliced
   // ballots; the lowest such lane advances the wave's counter for the digit
   const uint64_t lt = (1ull << lane) - 1ull;
@@ -655,35 +680,32 @@ struct BSort {
   bool one_region;            // one status region, zeroed again before every pass (big tables)
   unsigned int* err;          // look-back timeout flag
   unsigned int* tick;         // OS_DIGITS tile tickets (one per digit pass), just below status
-  unsigned long long* h_gh;   // pinned host copy of gh
 };
 
 // LSD radix sort of s.a[0, n) by its first nd digits (key bytes 0..7, then
-// run bytes), one onesweep pass per digit that is not the same for every
-// record; the result ends in s.a.  One host read (the histograms) per sort.
-int radix_sort(mox_engine* e, BSort& s, uint64_t n, int nd) {
+// run bytes), one onesweep pass per digit (a copy for a digit that is the same
+// for every record); the result ends in s.a.  No host round trip.  zeroed:
+// gh, the tickets and the status regions were zeroed by k_bs_zero (the first
+// sort of a bsort_once); else (the checked mode's subset sorts) here.
+int radix_sort(mox_engine* e, BSort& s, uint64_t n, int nd, bool zeroed) {
   if (n < 2) return MOX_OK;
   hipStream_t st = e->stream;
-  HIPCHK(hipMemsetAsync(s.gh, 0, (size_t)nd * 256 * 8, st));
-  hipLaunchKernelGGL(k_bs_ghist, dim3(GH_BLOCKS), dim3(256), 0, st, (const BRec*)s.a, n, nd, s.gh);
-  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const unsigned long long*)s.gh, nd, s.gs);
-  HIPCHK(hipMemcpyAsync(s.h_gh, s.gh, (size_t)nd * 256 * 8, hipMemcpyDeviceToHost, st));
   const uint64_t ntiles = (n + OS_TILE - 1) / OS_TILE;
   if (ntiles > 0x7FFFFFFFull) return fail(MOX_EINVAL, "bytewise sort: too many tiles");
-  // zero the tile tickets and the status words of every pass at once (a region per
-  // digit; a big table's single region is zeroed again before each later pass)
+  // the tile tickets and the status words of every pass (a region per digit; a
+  // big table's single region is zeroed again before each later pass)
   const size_t region = (size_t)ntiles * 256 * 8;
-  HIPCHK(hipMemsetAsync(s.tick, 0, TICK_BYTES + (s.one_region ? 1 : (size_t)nd) * region, st));
-  HIPCHK(hipStreamSynchronize(st));
-  bool first = true;
+  if (!zeroed) {
+    HIPCHK(hipMemsetAsync(s.gh, 0, (size_t)nd * 256 * 8, st));
+    HIPCHK(hipMemsetAsync(s.tick, 0, TICK_BYTES + (s.one_region ? 1 : (size_t)nd) * region, st));
+  }
+  hipLaunchKernelGGL(k_bs_ghist, dim3(GH_BLOCKS), dim3(256), 0, st, (const BRec*)s.a, n, nd, s.gh);
+  hipLaunchKernelGGL(k_bs_gscan, dim3(1), dim3(256), 0, st, (const unsigned long long*)s.gh, nd, s.gs);
   for (int d = 0; d < nd; d++) {
-    bool uniform = false;
-    for (int v = 0; v < 256; v++) uniform |= s.h_gh[d * 256 + v] == n;
-    if (uniform) continue;  // every record has the same digit: the order stays
-    if (s.one_region && !first) HIPCHK(hipMemsetAsync(s.status, 0, region, st));
-    first = false;
+    if (s.one_region && d) HIPCHK(hipMemsetAsync(s.status, 0, region, st));
     hipLaunchKernelGGL(k_os_pass, dim3((uint32_t)ntiles), dim3(OS_THREADS), 0, st, (const BRec*)s.a, s.b, n, d,
-                       (const uint64_t*)s.gs, s.status + (s.one_region ? 0 : (size_t)d * ntiles * 256), s.err, s.tick + d);
+                       (const uint64_t*)s.gs, (const unsigned long long*)s.gh,
+                       s.status + (s.one_region ? 0 : (size_t)d * ntiles * 256), s.err, s.tick + d);
     HIPCHK(hipGetLastError());
     std::swap(s.a, s.b);
   }
@@ -804,14 +826,18 @@ int bsort_once(mox_engine* e, bool checked) {
   uint64_t* ssum = (uint64_t*)q; q += sums;
   uint64_t* total = (uint64_t*)q; q += 64;  // [0] subset size [1] runs
   s.err = (unsigned int*)q;
-  s.h_gh = e->h_bsort;
   uint64_t* h_tot = (uint64_t*)(e->h_bsort + OS_DIGITS * 256);
-  HIPCHK(hipMemsetAsync(s.err, 0, 12, st));  // [0] look-back timeout [1] radix fallback [2] long runs (k_bs_segsort)
+  // err: [0] look-back timeout [1] radix fallback [2] long runs (k_bs_segsort); gh; total / rbs; tickets + status
+  {
+    const uint64_t nst = (TICK_BYTES + (one_region ? 1 : 8) * (uint64_t)ntiles * 256 * 8) / 8;  // level 0: 8 digits
+    hipLaunchKernelGGL(k_bs_zero, dim3((uint32_t)std::min<uint64_t>(4096, std::max<uint64_t>(16, (nst + 255) / 256))), dim3(256), 0,
+                       st, s.err, s.gh, total, (uint64_t*)s.tick, nst);
+  }
   // level 0: every word by its first 7 bytes and length class
   hipLaunchKernelGGL(k_bs_init, dim3(grid_for(n)), dim3(256), 0, st, r.offs, r.bytes, r.counts, n, A, pay, s.err);
   s.a = A;
   s.b = B;
-  if ((rc = radix_sort(e, s, n, 8))) return rc;
+  if ((rc = radix_sort(e, s, n, 8, true))) return rc;
   BRec* R = s.a;                 // sorted (A or B)
   BRec* S2 = R == A ? B : A;     // the other one is free: the subset's ping-pong partner (checked), or the subset
   if (!checked) S = S2;
@@ -829,14 +855,31 @@ int bsort_once(mox_engine* e, bool checked) {
   unsigned int* longrun = s.err + 1;  // [0] a run past RUN_LMAX or the list  [1] listed long runs
   uint64_t* lvt = total;                                // lvt[level % 4]: the level's scan total (m | runs << 32)
   uint32_t* rbs = (uint32_t*)(total + 4);               // rbs[level % 4]: the level's first run id
-  HIPCHK(hipMemsetD32Async((hipDeviceptr_t)rbs, 1u, 1, st));  // level 0's run ids end at 1
-  uint32_t run_base = 1;  // checked mode only
+  uint32_t run_base = 1;  // checked mode only (rbs[0] = 1: k_bs_zero)
+  uint64_t* oc = (uint64_t*)e->s_counts.p;
+  uint64_t* oo = (uint64_t*)e->s_offs.p;
+  // the sorted table: counts and lengths, offsets by a scan, bytes
+  auto output = [&]() -> int {
+    hipLaunchKernelGGL(k_bs_out1, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, oc, oo);
+    if (int rc2 = scan_u64(e, oo, n, oo + n, ssum)) return rc2;
+    hipLaunchKernelGGL(k_bs_out2, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, r.bytes,
+                       (const uint64_t*)oo, (uint8_t*)e->s_bytes.p);
+    HIPCHK(hipGetLastError());
+    return MOX_OK;
+  };
+  bool out_done = false;  // the output kernels ran after the last level
   for (uint32_t level = 1;; level++) {
     uint64_t* lt = lvt + (level & 3);
     hipLaunchKernelGGL(k_bs_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, fin);
     if ((rc = scan_u64(e, fin, n, lt, ssum))) return rc;
     uint64_t m = n, runs = 0;
     if (checked || level > EAGER_LEVELS) {
+      // the first level that reads its size back usually finds no tie left (no
+      // word tied on 21 bytes): the output kernels go first, on speculation, so
+      // that the one read-back also completes the sort (redone after the last
+      // level otherwise)
+      const bool spec = !checked && level == EAGER_LEVELS + 1;
+      if (spec && (rc = output())) return rc;
       HIPCHK(hipMemcpyAsync(h_tot, lt, 8, hipMemcpyDeviceToHost, st));
       HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 8, hipMemcpyDeviceToHost, st));
       HIPCHK(hipStreamSynchronize(st));
@@ -847,7 +890,10 @@ int bsort_once(mox_engine* e, bool checked) {
       if (fl1 && !checked) return -1;  // a long run in an eager level: run again, checked
       m = h_tot[0] & 0xFFFFFFFFull;
       runs = h_tot[0] >> 32;
-      if (m == 0) break;
+      if (m == 0) {
+        out_done = spec;
+        break;
+      }
     }
     hipLaunchKernelGGL(k_bs_gather_ties, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const uint64_t*)fin,
                        (const uint64_t*)lt, (const uint32_t*)(rbs + ((level - 1) & 3)), rbs + (level & 3), longrun + 1, s.err,
@@ -866,7 +912,7 @@ int bsort_once(mox_engine* e, bool checked) {
         s.b = S2;
         const uint64_t top = (uint64_t)run_base + runs;  // run ids < top: bytes of run id to sort on
         const int nrb = top < (1ull << 8) ? 1 : top < (1ull << 16) ? 2 : top < (1ull << 24) ? 3 : 4;
-        if ((rc = radix_sort(e, s, m, 8 + nrb))) return rc;
+        if ((rc = radix_sort(e, s, m, 8 + nrb, false))) return rc;
         sorted = s.a;
       }
       run_base += (uint32_t)runs;
@@ -875,18 +921,13 @@ int bsort_once(mox_engine* e, bool checked) {
                        (const uint32_t*)pos, R);
     HIPCHK(hipGetLastError());
   }
-  // the sorted table: counts and lengths, offsets by a scan, bytes
-  uint64_t* oc = (uint64_t*)e->s_counts.p;
-  uint64_t* oo = (uint64_t*)e->s_offs.p;
-  hipLaunchKernelGGL(k_bs_out1, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, oc, oo);
-  if ((rc = scan_u64(e, oo, n, oo + n, ssum))) return rc;
-  hipLaunchKernelGGL(k_bs_out2, dim3(grid_for(n)), dim3(256), 0, st, (const BRec*)R, n, (const BPay*)pay, r.bytes,
-                     (const uint64_t*)oo, (uint8_t*)e->s_bytes.p);
-  HIPCHK(hipGetLastError());
-  // complete: the callers time the sort on the host clock (ms_sort), so the
-  // output kernels above must be inside it
-  HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
-  HIPCHK(hipStreamSynchronize(st));
+  if (!out_done) {
+    if ((rc = output())) return rc;
+    // complete: the callers time the sort on the host clock (ms_sort), so the
+    // output kernels above must be inside it
+    HIPCHK(hipMemcpyAsync(h_tot + 2, s.err, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+  }  // (else the last level's read-back came after them and read the flags)
   if ((uint32_t)h_tot[2] & 1u) return fail(MOX_EHIP, "bytewise sort: a look-back wait timed out");
   if ((uint32_t)h_tot[2] & 4u) return fail(MOX_ENOMEM, "bytewise sort: a word of 16 MiB or more (sorted on the host)");
   r.counts = oc;

@@ -86,6 +86,16 @@ n2prof)
   python3 tools/xpass_kernels.py $O/n2k_${VAR:-tree} > $O/xpass_${VAR:-tree}.txt; step "xpass ${VAR:-tree}" $?
   cat $O/xpass_${VAR:-tree}.txt
   ;;
+abs)
+  # interleaved C2 bench lines of build variants (AB_VARS): value and the sorted-result line
+  k=0
+  for v in $AB_VARS; do
+    k=$((k+1)); f=$O/abs_${k}_${v}
+    MOX_LIB=build/var_$v/libmox.so timeout -k 10 300 python -u bench.py --no-cpu-baseline ${AB_ARGS:-} > $f.json 2> $f.err
+    rc=$?; [ $rc -eq 0 ] || { tail -3 $f.err; step "abs $v" $rc; }
+    python3 -c "import json;d=json.loads(open('$f.json').read().strip().splitlines()[-1]);s=d['sorted_result'];print('$v', d['value'], 'sorted', s['value'], 'sort_ms', s.get('sort_bytes_ms'))"
+  done
+  ;;
 lines)
   timeout -k 10 420 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline --workload C5 > $O/bench_c5.json 2> $O/bench_c5.err; step "bench C5" $?
   cut -c1-200 $O/bench_c5.json
@@ -139,6 +149,8 @@ c2prof)
     python3 bench.py --no-cpu-baseline > $O/c2p_under_rocprof.log 2>&1; step "rocprof C2" $?
   f=$(ls $O/c2p/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] || f=$(ls $O/c2p/run_kernel_stats.csv)
   cut -d, -f1-4 "$f" | grep -E "k_ss_|k_os_pass|k_bs_|k_scan|k_map|k_reduce\"" ; true
+  python3 tools/sort_timeline.py $O/c2p > $O/sort_timeline.txt; step "sort timeline" $?
+  tail -1 $O/sort_timeline.txt
   ;;
 varpar)
   # a build variant (build/var_$VAR) through the parity subset and the full-size
