@@ -223,6 +223,34 @@ def test_device_sort_run_past_the_segment_sort():
     assert all(cnt[w] == c for w, c in got)
 
 
+@pytest.mark.parametrize("checked", [False, True])
+def test_device_sort_uniform_digits(monkeypatch, checked):
+    """Tables where some radix digits hold the same value for every word: words
+    of 1-2 bytes (window bytes 2..6 are zero everywhere) and words behind one
+    shared 5-byte prefix.  k_os_pass reads the digit histogram itself and
+    copies such a pass instead of ranking it (no host read between the
+    histogram and the passes); the order equals Python's bytes order."""
+    if checked:
+        monkeypatch.setenv("MOX_BSORT_CHECKED", "1")
+    rng = random.Random(123)
+    letters = b"abcdefghijklmnopqrstuvwxyz0123456789"
+    short = sorted({bytes(rng.choice(letters) for _ in range(rng.randint(1, 2))) for _ in range(3000)})
+    pref = sorted({b"zzzzz" + bytes(rng.choice(letters) for _ in range(rng.randint(0, 14))) for _ in range(20000)})
+    for words in (short, pref):
+        shuffled = words[:]
+        rng.shuffle(shuffled)
+        e = mox.Engine(device=0, flags=mox.MOX_F_SORT_BYTES)
+        try:
+            t = e.reduce_pairs(shuffled, list(range(1, len(shuffled) + 1)))
+            got = list(t.items())
+            t.close()
+        finally:
+            e.close()
+        assert [w for w, _ in got] == words
+        cnt = dict(zip(shuffled, range(1, len(shuffled) + 1)))
+        assert all(cnt[w] == c for w, c in got)
+
+
 def test_device_sort_large_tables():
     """24 MiB of Zipf text + 48 MiB of C4-like tokens: the device-sorted
     table equals the oracle's sorted table array for array."""
