@@ -414,8 +414,17 @@ Caps grow_for(mox_engine* e, const Ctl& h) {
   if (h.overflow & OVF_TABLE) need.table_cap = h.n_total + h.n_total / 4 + 1024;
   if (h.overflow & OVF_BYTES) need.bytes_cap = h.bytes_total + h.bytes_total / 4 + 65536;
   if (h.overflow & OVF_SPLIT) {
-    need.split_k_cap = std::max<uint64_t>(need.split_k_cap, h.split_k + h.split_k / 8 + 4096);
-    need.split_w_cap = std::max<uint64_t>(need.split_w_cap, h.split_w + h.split_w / 8 + 4096);
+    uint64_t k = h.split_k + h.split_k / 8 + 4096, wv = h.split_w + h.split_w / 8 + 4096;
+    // a second overflow: which partitions split is decided from a sample taken
+    // anew by every attempt, so the asks can keep rising past an eighth; take
+    // the bound every split layout fits in (each partition split at most into
+    // SUB_N sub-buckets of even starts: split_span <= records + SUB_N + 1)
+    if (need.split_k_cap || need.split_w_cap) {  // (the caps are 0 until the first OVF_SPLIT)
+      k = std::max<uint64_t>(k, h.cold_recs + h.cold_recs / 8 + (uint64_t)NB * (SUB_N + 2));
+      wv = std::max<uint64_t>(wv, h.w_total + h.w_total / 8 + 4096);
+    }
+    need.split_k_cap = std::max<uint64_t>(need.split_k_cap, k);
+    need.split_w_cap = std::max<uint64_t>(need.split_w_cap, wv);
   }
   // a table overflow also means the byte estimate is stale
   if (h.overflow & OVF_TABLE) need.bytes_cap = std::max(need.bytes_cap, need.table_cap * 16);
@@ -564,7 +573,7 @@ int run_corpus(mox_engine* e, const Corpus& c) {
     if (!h.overflow) break;
     if (h.overflow & OVF_REDUCE)
       return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
-    if (attempt >= 4) return fail(MOX_ENOMEM, "buffer growth did not converge (overflow mask 0x%x)", h.overflow);
+    if (attempt >= GROW_RETRIES) return fail(MOX_ENOMEM, "buffer growth did not converge (overflow mask 0x%x)", h.overflow);
     Caps need = grow_for(e, h);
     e->stats.retries++;
     if ((rc = ensure_caps(e, need))) return rc;

@@ -63,6 +63,12 @@ __global__ void k_gather_offs(const uint8_t* recv, GDir d, uint64_t* out);
 }
 
 namespace mox_host {
+// Buffer-growth reruns of one pass: every overflow kind grows its buffers in
+// one step, but an attempt that overflowed early (cold regions, the split
+// layout) does not reach the later checks (table, bytes), so the kinds can be
+// met one attempt after another
+constexpr int GROW_RETRIES = 8;
+
 
 // thread-local last error (mox_last_error) and the status-returning setter
 extern thread_local std::string g_err;

@@ -1032,7 +1032,7 @@ int reduce_received(mox_engine* e, uint64_t rs, uint64_t rb, uint64_t r_long, co
     if ((rc = check_failed(h))) return rc;
     if (!h.overflow) break;
     if (h.overflow & OVF_REDUCE) return fail(MOX_ENOMEM, "a reduce partition holds more distinct words than it can split by hash");
-    if (attempt >= 4) return fail(MOX_ENOMEM, "exchange buffer growth did not converge (overflow mask 0x%x)", h.overflow);
+    if (attempt >= GROW_RETRIES) return fail(MOX_ENOMEM, "exchange buffer growth did not converge (overflow mask 0x%x)", h.overflow);
     e->stats.retries++;
     if ((rc = ensure_caps(e, grow_for(e, h)))) return rc;
   }
