@@ -294,7 +294,8 @@ void launch_reduce_tail(mox_engine* e, const Corpus& c, const Seq& q) {
   q.step("k_unit_uniq_scan");
   hipLaunchKernelGGL(k_final_scan, dim3(1), dim3(NB), 0, s, w);
   q.step("k_final_scan");
-  hipLaunchKernelGGL(k_mat, dim3(1024), dim3(256), 0, s, w, c);  // grid >= NB long-table slices
+  // 6 four-wave workgroups per CU (k_mat's occupancy), at least one per long-table slice
+  hipLaunchKernelGGL(k_mat, dim3(std::max(NB, 6 * e->n_cu)), dim3(256), 0, s, w, c);
   q.step("k_mat");
   q.rec(5);
 }

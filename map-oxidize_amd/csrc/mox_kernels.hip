@@ -4061,7 +4061,9 @@ extern "C" __global__ __launch_bounds__(64 * MAT_WAVES) void k_mat(Work w, Corpu
   // wave each, up to 512 words per batch with all their loads issued at once
   // (count-1 units: the (index, count) pairs, then the key gathers from the
   // unit's split_k range)
-  constexpr int MB = 8;  // words per lane per batch
+  // words per lane per batch: 4 keeps k_mat at 76 VGPRs, 6 waves per SIMD (8:
+  // 114 VGPRs, 4 waves; C4 16 GiB k_mat 12.1-12.4 -> 11.5-11.7 ms, g42)
+  constexpr int MB = 4;
   for (uint32_t u = blockIdx.x * MAT_WAVES + wv; u < U; u += gridDim.x * MAT_WAVES) {
     const UnitDesc ud = w.udesc[u];
     if (ud.in_n == UNIT_WHOLE) continue;
