@@ -26,6 +26,9 @@
 #            full-size C2 async parity test
 #   pmc      k_map FETCH/WRITE traffic at C2 and SQ counters of k_map
 #   smoke    __graft_entry__.smoke()
+#   abn2     interleaved N = 2 engine-group bench lines of build variants (AB_VARS)
+#   n2prof   kernel trace of an N = 2 group bench (VAR=name) and the exchange reduce passes' kernels
+#   abs      interleaved C2 bench lines of build variants (AB_VARS): value and the sorted-result line
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 TAG=$1; shift
