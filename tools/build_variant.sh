@@ -12,7 +12,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/build/var_$NAME
 mkdir -p $OUT
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result"
-K="-mllvm -amdgpu-sched-strategy=max-memory-clause"
+K=${KFLAGS:-"-mllvm -amdgpu-sched-strategy=max-memory-clause"}  # KFLAGS: another kernel scheduler for an A/B
 C=${SRC:-$ROOT/map-oxidize_amd/csrc}
 rm -f $OUT/*.o $OUT/libmox.so
 $H $K $FLAGS -c $C/mox_kernels.hip -o $OUT/k.o & P1=$!
